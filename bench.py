@@ -1,0 +1,156 @@
+"""bench.py -- pods scheduled/s + node-evaluations/s for the FGD replay of the
+Alibaba openb trace on MI355X (BASELINE.json metric; configs[1] = C2).
+
+Workload (one "step"): the C2 job -- openb GPU nodes (1213) x openb_pod_list_default,
+FGD (gpuSelMethod FGD), tune 1.3, shuffled, seeds 42..51 -> 10 independent
+simulated clusters replayed to completion on the device.  Per GPU the work is
+fixed (rank k replays seeds 42+10k .. 51+10k): weak scaling, replicas only, no
+collective on the data path.
+
+One JSON line on rank 0.  Extra keys: node_evals_per_s, roofline (dominant
+kernel k_step, HBM-bound by SURVEY §8(d)'s 32 B per node-evaluation), and
+cpu_baseline (the C oracle -- a restatement of the Go path -- on the host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-scheduler-simulator_amd"))
+
+import ksim  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+BYTES_PER_NODE_EVAL = 32
+BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
+
+
+def cpu_baseline(trace, seed, threads):
+    """Oracle ("port") on the host: one full seed replay (~11k events), FGD, `threads` workers."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers
+    import pyoracle as O
+    rp = trace.replay(seed=seed, tune_ratio=1.3, shuffle=True)
+    nodes = helpers.oracle_nodes(trace, rp)
+    ev = helpers.oracle_events(trace, rp)
+    tp = helpers.oracle_typical(trace)
+    t0 = time.perf_counter()
+    O.run_events(nodes, tp, ev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=len(ev) / dt, unit="pods/s", cores=threads, kind="port",
+                node_evals_per_s=len(ev) * trace.num_nodes / dt,
+                sample="openb default, seed %d, full replay (%d events x %d nodes), FGD, %d worker threads "
+                       "(parallelize.Until fan-out); host nproc=%d" % (seed, len(ev), trace.num_nodes, threads,
+                                                                        os.cpu_count()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--replicas", type=int, default=10, help="seeds per GPU (C2: 10)")
+    ap.add_argument("--nodes-per-block", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import torch
+
+    if world == 1:
+        torch.cuda.set_device(0)
+
+    trace = ksim.Trace.openb("default")
+    seeds = [42 + args.replicas * rank + i for i in range(args.replicas)]
+    eng = _engine_on(local, trace, seeds, args.nodes_per_block)
+    total_events = eng.total_events
+
+    for _ in range(args.warmup):
+        eng.run()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    dev_ms = 0.0
+    for _ in range(args.steps):
+        dev_ms += eng.run()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    steps_per_run = eng.last_run_steps()
+    # roofline: mean k_step duration over every step of one replay, hipEvent-timed on the engine stream
+    kern_us = eng.time_steps(steps_per_run)
+    bytes_per_launch = total_events / steps_per_run * (BYTES_PER_NODE_EVAL * trace.num_nodes + BYTES_PER_POD)
+    achieved = bytes_per_launch / (kern_us * 1e-6) / 1e9
+
+    pods_total = total_events * args.steps * world
+    value = pods_total / dt
+    line = {
+        "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "pods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1000.0 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32+f64",
+        "data": "Alibaba openb trace (data/openb, from the reference's data/csv), documented event order",
+        "config": {"workload": "C2: openb 1213 GPU nodes x openb_pod_list_default, FGD, tune 1.3, shuffled, "
+                               "%d seeds per GPU replayed to completion" % args.replicas,
+                   "replicas_per_gpu": args.replicas, "events_per_gpu": total_events,
+                   "parallelism": "replicas%d" % world},
+        "node_evals_per_s": value * trace.num_nodes,
+        "device_ms_per_step": dev_ms / args.steps,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_step", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(trace, seeds[0], args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _engine_on(device, trace, seeds, nodes_per_block):
+    arr, n = trace.typical()
+    eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block)
+    total = 0
+    for r, s in enumerate(seeds):
+        rp = trace.replay(seed=s, tune_ratio=1.3, shuffle=True)
+        eng.set_nodes(r, rp.nodes)
+        eng.set_typical(r, arr, n)
+        eng.set_policy(r, "FGD")
+        eng.load_events(r, rp.events, rp.n)
+        total += rp.n
+    eng.total_events = total
+    return eng
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * ksim_engine.h -- the drop-in C ABI of the MI355X scoring engine.
+ *
+ * It replaces, for one simulated cluster ("replica") or a batch of them, the
+ * per-pod Filter+Score pass of the reference kube-scheduler framework plugins
+ * (Fr4nz83/kubernetes-scheduler-simulator @ 2024_08_07, paths relative to that
+ * tree):
+ *
+ *   framework.FilterPlugin.Filter      vendor/k8s.io/kubernetes/pkg/scheduler/framework/interface.go:278-291
+ *     = NodeResourcesFit.fitsRequest   vendor/.../framework/plugins/noderesources/fit.go:230-290
+ *     ∧ GpuSharePlugin.Filter          pkg/simulator/plugin/open_gpu_share.go:81-118
+ *   framework.ScorePlugin.Score        interface.go:333-338
+ *     FGDScorePlugin.Score             pkg/simulator/plugin/fgd_score.go:44-91
+ *     BestFitScorePlugin.Score         pkg/simulator/plugin/best_fit_score.go:33-53 (+NormalizeScore :59-61)
+ *     DotProductScorePlugin.Score      pkg/simulator/plugin/dot_product_score.go:45-58 (merge, max)
+ *     GpuPackingScorePlugin.Score      pkg/simulator/plugin/gpu_packing_score.go:35-61
+ *     GpuClusteringScorePlugin.Score   pkg/simulator/plugin/gpu_clustering_score.go:32-56
+ *     RandomScorePlugin.PreScore/Score pkg/simulator/plugin/random_score.go:42-68
+ *   selectHost                         vendor/.../core/generic_scheduler.go:187-212
+ *   ReservePlugin.Reserve/Unreserve    interface.go:350-361; open_gpu_share.go:178-218
+ *     allocateGpuIdFunc[gpuSelMethod]  open_gpu_share.go:39, :252-343; fgd_score.go:153-156
+ *   BindPlugin.Bind (state scatter)    pkg/simulator/plugin/simon.go:42-120
+ *
+ * Conventions: plain C types only; every pointer is borrowed for the duration
+ * of the call (cgo rule: C never retains Go memory); return 0 on success or a
+ * negative KSIM_E* code (ksim_strerror).  An engine is single-writer: calls on
+ * one engine must be serialised by the caller (scheduling cycles are serial in
+ * the reference, scheduler.go:441).
+ *
+ * The product library (libksim_hip.so) requires a gfx950 device: there is no
+ * CPU fallback.  Without a usable device every compute call returns
+ * KSIM_ENODEV.
+ */
+#ifndef KSIM_ENGINE_H
+#define KSIM_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSIM_ABI_VERSION 1
+#define KSIM_MAX_GPU 8          /* pkg/type/const.go:52 MaxNumGpuPerNode */
+#define KSIM_MAX_TYPES 32       /* GPU-model vocabulary size (bit i of a type mask) */
+#define KSIM_MAX_TYPICAL 256
+#define KSIM_NUM_TAGS 9         /* GpuClustering affinity tags: share-gpu, 1-gpu .. 8-gpu */
+#define KSIM_TYPE_ANY 0xFFFFFFFFu
+
+enum ksim_status {
+    KSIM_OK = 0,
+    KSIM_EINVAL = -1,     /* bad argument (null pointer, index out of range) */
+    KSIM_ENOMEM = -2,     /* host or device allocation failed */
+    KSIM_EHIP = -3,       /* HIP runtime error */
+    KSIM_ERANGE = -4,     /* value outside the engine's encodings (e.g. > 8 GPUs, milli > 1000) */
+    KSIM_ESTATE = -5,     /* call out of order (e.g. run before events are loaded) */
+    KSIM_ENOTSUP = -6,    /* policy/config not supported */
+    KSIM_ENODEV = -7,     /* no gfx950 device */
+    KSIM_EIO = -8         /* trace file unreadable / malformed */
+};
+
+/* Score plugins (one per replica; pkg/type/const.go:8-14) */
+enum ksim_policy {
+    KSIM_POLICY_FGD = 0,
+    KSIM_POLICY_BESTFIT = 1,
+    KSIM_POLICY_DOTPROD = 2,        /* dimExtMethod=merge, normMethod=max (paper configuration) */
+    KSIM_POLICY_GPUPACKING = 3,
+    KSIM_POLICY_GPUCLUSTERING = 4,
+    KSIM_POLICY_RANDOM = 5
+};
+
+/* Open-Gpu-Share gpuSelMethod (pkg/type/config.go:36-42; "FGDScore" selects the FGD selector) */
+enum ksim_gpusel {
+    KSIM_GPUSEL_BEST = 0,
+    KSIM_GPUSEL_WORST = 1,
+    KSIM_GPUSEL_RANDOM = 2,
+    KSIM_GPUSEL_FGD = 3
+};
+
+/* Result status (framework.Status codes) */
+enum ksim_result_status { KSIM_SCHEDULED = 0, KSIM_UNSCHEDULABLE = 1, KSIM_ERROR = 2, KSIM_DELETED = 3 };
+
+/* A node: allocatable + current usage.  Mirrors what GetNodeResourceViaNodeInfo
+ * (pkg/utils/utils.go:1053-1075) and the open-gpu-share cache
+ * (pkg/type/open-gpu-share/cache/gpunodeinfo.go) read from v1.Node/NodeInfo. */
+typedef struct {
+    int64_t  cpu_alloc_milli;      /* node.Status.Allocatable cpu, milli */
+    int64_t  mem_alloc_mib;        /* allocatable memory, MiB */
+    int32_t  pods_alloc;           /* allocatable pods */
+    int32_t  gpu_count;            /* alibabacloud.com/gpu-count, 0..8 */
+    int32_t  gpu_type;             /* model id in the caller's vocabulary, 0..31 */
+    uint32_t name_rank;            /* rank of node.Name in byte-wise order (selectHost tie-break) */
+    int64_t  cpu_used_milli;       /* nodeInfo.Requested.MilliCPU */
+    int64_t  mem_used_mib;         /* nodeInfo.Requested.Memory, MiB */
+    int32_t  pods_used;            /* len(nodeInfo.Pods) */
+    int32_t  gpu_used_milli[KSIM_MAX_GPU]; /* DeviceInfo.GetUsedGpuMilli per device */
+    int32_t  tag_count[KSIM_NUM_TAGS];     /* pods per GpuClustering tag on the node */
+    int32_t  reserved;
+} ksim_node;
+
+/* A pod (creation or deletion event).  PodResource (pkg/type/resource.go:51-58)
+ * plus the Filter request vector (fit.go computePodResourceRequest). */
+typedef struct {
+    int64_t  cpu_milli;            /* summed container cpu request (Filter, Requested) */
+    int64_t  cpu_nz_milli;         /* GetNonzeroRequests cpu (Score's PodResource.MilliCpu) */
+    int64_t  mem_mib;              /* summed container memory request, MiB */
+    int32_t  gpu_milli;            /* alibabacloud.com/gpu-milli (per GPU), 0..1000 */
+    int32_t  gpu_count;            /* alibabacloud.com/gpu-count, 0..8 */
+    uint32_t type_mask;            /* accepted models (gpu-card-model pipe list); KSIM_TYPE_ANY = none given */
+    int32_t  is_delete;            /* 1: deletion event */
+    int32_t  ref;                  /* deletion: index (same stream) of the creation event */
+    int32_t  reserved;
+} ksim_pod;
+
+/* One target-workload entry (TargetPod, resource.go:14-17). */
+typedef struct {
+    int64_t  cpu_milli;            /* PodResource.MilliCpu */
+    int32_t  gpu_milli;
+    int32_t  gpu_count;
+    uint32_t type_mask;
+    int32_t  reserved;
+    double   freq;                 /* Percentage, 0..1 */
+} ksim_typical;
+
+/* Outcome of one scheduling cycle. */
+typedef struct {
+    int32_t node;                  /* node index (input order), -1 if none */
+    int32_t gpu_mask;              /* devices assigned by Reserve (bit g = GPU g) */
+    int64_t score;                 /* winning total weighted score (0 on the single-feasible shortcut) */
+    int32_t n_feasible;            /* nodes that passed Filter */
+    int32_t status;                /* enum ksim_result_status */
+} ksim_result;
+
+typedef struct ksim_engine ksim_engine;
+
+/* Engine configuration (0 = default). */
+typedef struct {
+    int32_t device;                /* HIP device ordinal */
+    int32_t nodes_per_block;       /* nodes per workgroup in the step kernel (default 32) */
+    int32_t steps_per_graph;       /* pod steps captured per hipGraph (default 256) */
+    int32_t reserved;
+} ksim_config;
+
+const char* ksim_strerror(int code);
+int  ksim_abi_version(void);
+int  ksim_device_count(void);      /* gfx950 devices visible; 0 when none */
+
+/* Lifecycle.  n_replicas independent clusters of n_nodes each share one device. */
+int  ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim_engine** out);
+void ksim_engine_destroy(ksim_engine* e);
+
+/* Per-replica setup.  set_nodes resets that replica's cluster state. */
+int  ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes);
+int  ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp, int n);
+int  ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed);
+
+/* Plugin-level entry points (no state change).  For one pod, Filter + Score
+ * every node of the replica: feasible[n] (0/1), score[n] (the plugin's Score
+ * before NormalizeScore), gpu_mask[n] (the GPU set the plugin's selector would
+ * pick, FGD/Random policies).  `step` seeds the Random contract.  This is the
+ * batch a Go PreScore shim stores in CycleState so Filter/Score are lookups. */
+int  ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, int32_t step,
+                              uint8_t* feasible, int32_t* score, int32_t* gpu_mask);
+
+/* Reserve + Bind `pod` on `node` (GPU selection by the replica's gpusel) and
+ * Unreserve/delete.  *gpu_mask_out receives the devices assigned. */
+int  ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t step,
+                         int32_t* gpu_mask_out);
+int  ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask);
+
+/* One full scheduling cycle (Filter, Score, NormalizeScore, selectHost, Reserve, Bind). */
+int  ksim_engine_schedule(ksim_engine* e, int replica, const ksim_pod* pod, int32_t step, ksim_result* out);
+
+/* Whole-trace device loop: load each replica's event stream, run every replica
+ * to completion on the device (hipGraph-captured pod steps), fetch results.
+ * ksim_engine_run restarts every replica from the state given to set_nodes. */
+int  ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events, int n);
+int  ksim_engine_run(ksim_engine* e);
+int  ksim_engine_get_results(ksim_engine* e, int replica, ksim_result* out, int n);
+int  ksim_engine_get_nodes(ksim_engine* e, int replica, ksim_node* out);
+
+/* Measurement.  Restarts from the set_nodes state and runs the first `n_steps`
+ * pod steps of every replica as eager launches with an event pair around every
+ * step kernel; returns the mean step-kernel duration in microseconds. */
+int  ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us);
+/* Device wall time of the last ksim_engine_run (ms), from hipEvents on the run stream. */
+int  ksim_engine_last_run_ms(ksim_engine* e, double* ms);
+/* Steps executed by the last run (max events over replicas). */
+int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

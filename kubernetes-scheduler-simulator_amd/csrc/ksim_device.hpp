@@ -1,0 +1,405 @@
+// ksim_device.hpp -- device-side data layout and the per-node math of the
+// Filter+Score path (gfx950).  Every function cites the reference Go code it
+// restates (paths relative to Fr4nz83/kubernetes-scheduler-simulator @ 2024_08_07).
+//
+// Compiled with -ffp-contract=off: Go (amd64, GOAMD64=v1) never fuses a*b+c,
+// and every fp64 expression below keeps Go's evaluation order so that the
+// fragmentation amounts are bit-identical to the reference.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ksim {
+
+constexpr int kMaxGpu = 8;
+constexpr int kMilli = 1000;         // open-gpu-share/utils/const.go:14
+constexpr int kMaxSpecCpu = 128000;  // const.go:16
+constexpr int kMaxSpecGpu = 8000;    // const.go:18
+constexpr int kNumTags = 9;
+constexpr int kMaxTypical = 256;
+
+// One node of one replica in HBM: 32 B, read once per pod step.
+struct __align__(16) NodeRec {
+  int32_t cpu_left;    // Allocatable.MilliCPU - Requested.MilliCPU
+  int32_t mem_left;    // MiB
+  uint16_t gl[kMaxGpu];  // milli-GPU left per device (0 beyond gpu_cnt)
+  int16_t pods_left;   // AllowedPodNumber - len(Pods)
+  uint8_t gpu_cnt;
+  uint8_t gpu_type;    // model id, 0..31
+  uint32_t name_rank;  // byte-wise rank of the node name
+};
+static_assert(sizeof(NodeRec) == 32, "NodeRec must stay 32 B");
+
+// Register image of a NodeRec: eight dwords, fields extracted with shifts so
+// that no per-lane array ever lands in scratch (gl(g) is only called with
+// compile-time g inside unrolled loops).
+struct NodeV {
+  int32_t cpu_left;
+  int32_t mem_left;
+  uint32_t g[4];     // two u16 milli-left values per dword
+  uint32_t meta;     // pods_left (i16) | gpu_cnt << 16 | gpu_type << 24
+  uint32_t name_rank;
+  __device__ __forceinline__ int gl(int i) const {
+    const uint32_t w = i < 2 ? g[0] : (i < 4 ? g[1] : (i < 6 ? g[2] : g[3]));
+    return (int)((i & 1) ? (w >> 16) : (w & 0xffffu));
+  }
+  __device__ __forceinline__ int pods_left() const { return (int)(int16_t)(meta & 0xffffu); }
+  __device__ __forceinline__ int gpu_cnt() const { return (int)((meta >> 16) & 0xffu); }
+  __device__ __forceinline__ int gpu_type() const { return (int)(meta >> 24); }
+  __device__ __forceinline__ int total() const {
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += gl(i);
+    return t;
+  }
+};
+
+__device__ __forceinline__ NodeV load_node(const NodeRec* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1];
+  NodeV n;
+  n.cpu_left = (int32_t)a.x;
+  n.mem_left = (int32_t)a.y;
+  n.g[0] = a.z; n.g[1] = a.w; n.g[2] = b.x; n.g[3] = b.y;
+  n.meta = b.z;
+  n.name_rank = b.w;
+  return n;
+}
+__device__ __forceinline__ void store_node(NodeRec* p, const NodeV& n) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4((uint32_t)n.cpu_left, (uint32_t)n.mem_left, n.g[0], n.g[1]);
+  q[1] = make_uint4(n.g[2], n.g[3], n.meta, n.name_rank);
+}
+
+// One event of one replica: 32 B.
+struct __align__(16) PodDev {
+  int32_t cpu_req;   // Filter / Requested
+  int32_t cpu_nz;    // Score (non-zero default)
+  int32_t mem;       // MiB
+  int16_t milli;     // per-GPU milli
+  int8_t num;        // GPU count
+  int8_t tag;        // -1 no-gpu, 0 share-gpu, k "k-gpu", -2 invalid (reference panics)
+  uint32_t tmask;    // accepted model bitmask
+  int32_t ref;       // deletion: creation index
+  uint32_t flags;    // kPodDelete
+  int32_t pad;
+};
+static_assert(sizeof(PodDev) == 32, "PodDev must stay 32 B");
+constexpr uint32_t kPodDelete = 1u;
+
+// Typical-pod table entry, host layout (staged into LDS as int4 + double).
+struct TypDev {
+  int32_t cpu;
+  int32_t milli;
+  int32_t num_eff;  // max(GpuNumber, 1): CanNodeHostPodOnGpuMemory (frag.go:447-458)
+  uint32_t tmask;
+  double freq;
+};
+static_assert(sizeof(TypDev) == 24, "TypDev must stay 24 B");
+
+struct ResultDev {  // == ksim_result
+  int32_t node;
+  int32_t gpu_mask;
+  int64_t score;
+  int32_t n_feasible;
+  int32_t status;
+};
+static_assert(sizeof(ResultDev) == 24, "ResultDev must match ksim_result");
+
+struct ReplicaDev {
+  int32_t policy;
+  int32_t gpusel;
+  uint64_t seed;
+  int32_t n_events;
+  int32_t nt;
+  const TypDev* tp;
+  const PodDev* ev;
+  ResultDev* res;
+  NodeRec* nodes;
+  uint16_t* tags;  // [N][16]
+};
+
+// Per-replica cross-workgroup accumulators for one step (reset by the last block).
+struct __align__(64) Accum {
+  unsigned long long best;  // packed argmax key
+  int32_t nfeas;
+  int32_t err;
+  int32_t lo;               // BestFit NormalizeScore: min raw score
+  int32_t hi;               // max raw score
+  uint32_t ticket;
+  int32_t pad[9];
+};
+
+enum : int { POL_FGD = 0, POL_BESTFIT = 1, POL_DOTPROD = 2, POL_PACKING = 3, POL_CLUSTERING = 4, POL_RANDOM = 5 };
+enum : int { SEL_BEST = 0, SEL_WORST = 1, SEL_RANDOM = 2, SEL_FGD = 3 };
+enum : int { ST_OK = 0, ST_UNSCHED = 1, ST_ERROR = 2, ST_DELETED = 3 };
+
+// ---------------------------------------------------------------------------
+// Go math.Exp, portable algorithm (Go src/math/exp.go).  Identical operation
+// sequence to oracle/fgd_oracle.c orc_go_exp.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double go_exp(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01;
+  const double Ln2Lo = 1.90821492927058770002e-10;
+  const double Log2e = 1.44269504088896338700e+00;
+  const double Overflow = 7.09782712893383973096e+02;
+  const double Underflow = -7.45133219101941108420e+02;
+  const double NearZero = 1.0 / (double)(1 << 28);
+  const double P1 = 1.66666666666666657415e-01;
+  const double P2 = -2.77777777770155933842e-03;
+  const double P3 = 6.61375632143793436117e-05;
+  const double P4 = -1.65339022054652515390e-06;
+  const double P5 = 4.13813679705723846039e-08;
+  if (x != x) return x;
+  if (x > Overflow) return __longlong_as_double(0x7ff0000000000000LL);
+  if (x < Underflow) return 0.0;
+  if (-NearZero < x && x < NearZero) return 1 + x;
+  int k = 0;
+  if (x < 0) k = (int)(Log2e * x - 0.5);
+  else if (x > 0) k = (int)(Log2e * x + 0.5);
+  double hi = x - (double)k * Ln2Hi;
+  double lo = (double)k * Ln2Lo;
+  double r = hi - lo;
+  double t = r * r;
+  double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+  double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
+  int k1 = k / 2, k2 = k - k1;
+  double a = __longlong_as_double((long long)(1023 + k1) << 52);
+  double b = __longlong_as_double((long long)(1023 + k2) << 52);
+  return (y * a) * b;
+}
+
+// plugin_utils.go:76-78
+__device__ __forceinline__ double go_sigmoid(double x) { return 1.0 / (1.0 + go_exp(-x)); }
+
+// fgd_score.go:123 fragScore = int64(sigmoid((cur-new)/1000) * MaxNodeScore)
+__device__ __forceinline__ int fgd_frag_score(double cur, double nw) {
+  return (int)(go_sigmoid((cur - nw) / 1000) * (double)100);
+}
+
+// ---------------------------------------------------------------------------
+// F(state) = NodeGpuShareFragAmountScore (frag.go:200-203)
+//          = FragAmountSumExceptQ3 (frag.go:411-418) of NodeGpuShareFragAmount
+//            (frag.go:148-188) with GetNodePodFrag (frag.go:460-493).
+// Each bin is a sequential fp64 sum in typical-pod order; a bin a typical pod
+// does not touch receives +0.0, which leaves every non-negative sum bit-exact.
+// Bin Q3 (index 2) is not part of F and is not accumulated here.
+// tpi[t] = {MilliCpu, MilliGpu, max(GpuNumber,1), type mask}, tpf[t] = freq.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, int T,
+                                         const int4* __restrict__ tpi, const double* __restrict__ tpf) {
+  int total = 0;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) total += gl[g];  // GetGpuMilliLeftTotal (frag.go:224-229)
+  const double dtot = (double)total;
+  double b0 = 0.0, b1 = 0.0, b3 = 0.0, b4 = 0.0, b5 = 0.0, b6 = 0.0;
+  for (int t = 0; t < T; ++t) {
+    const int4 q = tpi[t];
+    const double f = tpf[t];
+    const double x = f * dtot;          // freq * float64(gpuMilliLeftTotal)
+    const bool cpu_ok = cpuL >= q.x;
+    if (q.y == 0) {                     // CPU-only typical pod: XL / XR (frag.go:463-469)
+      b4 += cpu_ok ? x : 0.0;
+      b5 += cpu_ok ? 0.0 : x;
+    } else {
+      const bool acc = (q.w & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+      int cnt = 0, frag = 0;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g) {
+        const bool ge = gl[g] >= q.y;
+        cnt += ge ? 1 : 0;               // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+        frag += ge ? 0 : gl[g];          // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+      }
+      const bool gpu_ok = cnt >= q.z;
+      const double y = f * (double)frag;  // freq * float64(gpuFragMilli)
+      const bool q3 = acc && gpu_ok && cpu_ok;
+      const bool q2 = acc && !gpu_ok && cpu_ok;
+      b0 += (acc && !gpu_ok && !cpu_ok) ? x : 0.0;  // Q1
+      b1 += q3 ? y : (q2 ? x : 0.0);                 // Q2 (Q3 splits its frag part here)
+      b3 += (acc && gpu_ok && !cpu_ok) ? x : 0.0;   // Q4
+      b6 += acc ? 0.0 : x;                           // NA
+    }
+  }
+  double out = 0.0;
+  out += b0;
+  out += b1;
+  out += b3;
+  out += b4;
+  out += b5;
+  out += b6;
+  return out;
+}
+
+__device__ __forceinline__ void unpack_gl(const NodeV& n, int (&gl)[kMaxGpu]) {
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) gl[g] = n.gl(g);
+}
+
+// Filter: fitsRequest (fit.go:230-290) ∧ GpuSharePlugin.Filter (open_gpu_share.go:81-118)
+//         ∧ GpuNodeInfo.AllocateGpuId (gpunodeinfo.go:136-204).
+__device__ __forceinline__ bool filter_node(const NodeV& n, const PodDev& p) {
+  if (n.pods_left() < 1) return false;
+  if (!(p.cpu_req == 0 && p.mem == 0)) {
+    if (n.cpu_left < p.cpu_req) return false;
+    if (n.mem_left < p.mem) return false;
+  }
+  if (p.milli <= 0) return true;
+  const int cnt = n.gpu_cnt();
+  if (cnt == 0) return false;
+  if ((p.tmask & (1u << n.gpu_type())) == 0u) return false;
+  if (p.num <= 0) return false;
+  if (p.num == 1) {
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) any |= (g < cnt) && (n.gl(g) >= p.milli);
+    return any;
+  }
+  // multi-GPU two-pointer greedy: a device can host floor(idle/milli) slots
+  int slots = 0;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g)
+    if (g < cnt) slots += n.gl(g) / p.milli;
+  return slots >= p.num;
+}
+
+__device__ __forceinline__ bool is_share_pod(const PodDev& p) { return p.num == 1 && p.milli < kMilli; }
+
+// GPUs selected by NodeResource.Sub (resource.go:454-480): ascending stable
+// order of milli left, first `num` devices with left >= milli.  Returns mask;
+// *ok=false when Sub would return its early error (state left unchanged).
+__device__ __forceinline__ unsigned sub_gpu_mask(const int (&gl)[kMaxGpu], int gpu_cnt, int cpuL, const PodDev& p,
+                                                 bool* ok) {
+  *ok = !(cpuL < p.cpu_nz || gpu_cnt < p.num);
+  if (!*ok || p.num <= 0) return 0u;
+  unsigned taken = 0u;
+  for (int k = 0; k < p.num; ++k) {
+    int best = -1, bv = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      const bool cand = g < gpu_cnt && !((taken >> g) & 1u) && gl[g] >= p.milli;
+      if (cand && (best < 0 || gl[g] < bv)) { best = g; bv = gl[g]; }
+    }
+    if (best < 0) break;
+    taken |= 1u << best;
+  }
+  return taken;
+}
+
+// AllocateExclusiveGpuId (resource.go:383-403): lowest-index fully free GPUs.
+// Returns -1 where the reference panics.
+__device__ __forceinline__ int exclusive_gpu_mask(const NodeV& n, const PodDev& p) {
+  int req = (int)p.milli * (int)p.num;
+  int mask = 0;
+  const int cnt = n.gpu_cnt();
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) {
+    if (req > 0 && g < cnt && n.gl(g) == kMilli) {
+      mask |= 1 << g;
+      req -= kMilli;
+    }
+  }
+  return req > 0 ? -1 : mask;
+}
+
+// getBestFitScore (best_fit_score.go:66-97); -1 = error
+__device__ __forceinline__ int bestfit_score(const NodeV& n, const PodDev& p, int total) {
+  const double f0 = (double)n.cpu_left, r0 = (double)p.cpu_nz;
+  const double f1 = (double)total, r1 = (double)((int)p.milli * (int)p.num);
+  double s = 0;
+  if (f0 < r0) return -1;
+  s += (f0 - r0) / (double)kMaxSpecCpu * 0.5;
+  if (f1 < r1) return -1;
+  s += (f1 - r1) / (double)kMaxSpecGpu * 0.5;
+  s = (1.0 - s) * (double)100;
+  return (int)s;
+}
+
+// calculateDotProductScore with merge/max (dot_product_score.go:64-100,
+// utils.go:1274-1342, resource.go:296-328, utils.go:1220-1248)
+__device__ __forceinline__ int dotprod_score(const NodeV& n, const PodDev& p, int total) {
+  if (n.cpu_left < p.cpu_nz) return 0;
+  const double a0 = (double)n.cpu_left / (double)kMaxSpecCpu;
+  const double a1 = (double)total / (double)kMaxSpecGpu;
+  const double c0 = (double)p.cpu_nz / (double)kMaxSpecCpu;
+  const double c1 = (double)((int)p.milli * (int)p.num) / (double)kMaxSpecGpu;
+  double cur = 0;
+  cur += a0 * c0;
+  cur += a1 * c1;
+  cur /= (double)2;
+  cur = 1 - cur;
+  double score = -1;
+  if (score < cur) score = cur;
+  return (int)((double)100 * score);
+}
+
+// getPackingScore (gpu_packing_score.go:71-117); *err on allocation failure
+__device__ __forceinline__ int packing_score(const NodeV& n, const PodDev& p, bool* err) {
+  *err = false;
+  const int cnt = n.gpu_cnt();
+  int ff = 0;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) ff += (g < cnt && n.gl(g) == kMilli) ? 1 : 0;
+  if (ff == cnt) {
+    const int s = 100 / 3 - ff;
+    return s > ff ? s : ff;
+  }
+  unsigned taken = 0u;
+  int ffuse = 0, req = p.num, r = 0;
+  for (int k = 0; k < kMaxGpu && req > 0; ++k) {
+    int best = -1, bv = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      const int v = n.gl(g);
+      const bool cand = g < cnt && !((taken >> g) & 1u) && v >= p.milli;
+      if (cand && (best < 0 || v < bv)) { best = g; bv = v; }
+    }
+    if (best < 0) break;
+    taken |= 1u << best;
+    --req;
+    if (bv == kMilli) ++ffuse;
+    r += bv * 100 / kMilli;
+  }
+  if (req != 0) {
+    *err = true;
+    return 0;
+  }
+  if (ffuse > 0) {
+    const int s = 100 / 2 - ffuse;
+    return s > 100 / 3 ? s : 100 / 3;
+  }
+  const int s = 100 - r / 10;
+  return s > 100 / 2 ? s : 100 / 2;
+}
+
+// GpuClusteringScorePlugin.Score (gpu_clustering_score.go:32-56)
+__device__ __forceinline__ int clustering_score(const uint16_t* tags, int pod_tag, int total) {
+  if (pod_tag < 0) return 0;
+  int distinct = 0;
+#pragma unroll
+  for (int k = 0; k < kNumTags; ++k) distinct += tags[k] > 0 ? 1 : 0;
+  const int base = (100 / 4) * (kMaxSpecGpu - total) / kMaxSpecGpu;
+  if (tags[pod_tag] > 0) return distinct == 1 ? base + 100 * 3 / 4 : base + 100 * 2 / 4;
+  return distinct == 0 ? base + 100 / 4 : base;
+}
+
+// Random contract: splitmix64 finaliser.
+__device__ __host__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ULL;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebULL;
+  x ^= x >> 31;
+  return x;
+}
+__device__ __forceinline__ uint64_t rand_node_key(uint64_t seed, int step, uint32_t rank) {
+  return mix64(mix64(seed ^ 0xA0761D6478BD642FULL) ^ (((uint64_t)(uint32_t)step << 32) | rank));
+}
+__device__ __forceinline__ uint64_t rand_gpu_key(uint64_t node_key, int g) { return mix64(node_key ^ (uint64_t)(0x100 + g)); }
+
+// Packed argmax key: [63:40] score (24 b) | [39:8] ~name_rank | [7:0] gpu index + 1.
+__device__ __forceinline__ unsigned long long pack_key(unsigned score, uint32_t rank, int gpu) {
+  return ((unsigned long long)(score & 0xFFFFFFu) << 40) | ((unsigned long long)(0xFFFFFFFFu - rank) << 8) |
+         (unsigned long long)((gpu + 1) & 0xFF);
+}
+
+}  // namespace ksim

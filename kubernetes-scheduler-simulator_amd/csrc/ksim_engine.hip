@@ -1,0 +1,987 @@
+// ksim_engine.hip -- MI355X (gfx950) scoring engine for the simulator's per-pod
+// Filter+Score pass, behind the C ABI of include/ksim_engine.h.
+//
+// Device layout (HBM, struct-of-records, replica-major):
+//   NodeRec  nodes[R][N]   32 B: cpu/mem left, 8 x u16 milli-GPU left, pods left,
+//                          gpu count, model id, name rank
+//   uint16   tags[R][N][16] GpuClustering affinity counts
+//   PodDev   ev_r[E_r]      32 B per event, per replica
+//   TypDev   tp[R][256]     typical-pod table (staged into LDS per workgroup)
+//   ResultDev res_r[E_r]    24 B per event
+//
+// One pod step of every replica is ONE kernel launch (k_step):
+//   workgroup (256 threads) = one replica x `nodes_per_block` nodes
+//   phase 1  one thread per node: Filter; cheap policies score here
+//   phase 2  FGD only: the (node, candidate placement) pairs of the workgroup
+//            are compacted into an LDS work list and every thread evaluates
+//            F = NodeGpuShareFragAmountScore of one candidate state against the
+//            LDS-staged typical table (sequential fp64 bins, bit-exact)
+//   phase 3  per node: score = int64(sigmoid((F0-Fk)/1000)*100), packed
+//            argmax key (score | ~name_rank | gpu), workgroup max-reduce
+//   commit   relaxed agent-scope atomics into the replica's Accum; the
+//            workgroup that takes the last ticket reads the winner, runs
+//            Reserve's GPU selector on it and scatters the Bind update.
+// Steps are captured K at a time into a hipGraph (kernel i reads step = base+i;
+// a one-thread kernel advances base) so a whole trace replays with no host
+// round trip per pod.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "ksim_device.hpp"
+#include "ksim_engine.h"
+
+using namespace ksim;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kNBMax = 64;
+constexpr int kMaxCand = 9;
+constexpr int kTagStride = 16;
+
+struct StepArgs {
+  ReplicaDev* reps;
+  Accum* acc;
+  int N;
+  int NB;
+  int bpr;        // workgroups per replica
+  int rep_first;  // first replica of this launch
+  const int* base;
+  int step_off;
+  const PodDev* pod_override;  // single-pod calls
+  ResultDev* res_override;
+  int mode;  // 0: commit (Reserve+Bind), 1: Filter+Score outputs only
+  uint8_t* out_feas;
+  int32_t* out_score;
+  int32_t* out_gpu;
+};
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = __shfl_xor(v, o, 64);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// allocateGpuId (open_gpu_share.go:252-283) on one node: the replica's gpuSelMethod.
+// fgd_gpu: the FGD selector's device for share pods (first max-score index), -1 if none.
+// Returns the GPU mask, 0 for pods without GPU milli, -1 where the reference panics / returns "".
+__device__ int select_gpus(const NodeV& n, const PodDev& p, int gpusel, int fgd_gpu, uint64_t seed, int step) {
+  if (p.milli <= 0) return 0;                                         // open_gpu_share.go:185-187
+  if (p.milli < kMilli && p.num > 1) return -1;                       // :266-268 panic
+  if (!is_share_pod(p)) return exclusive_gpu_mask(n, p);              // exclusive branch of every selector
+  switch (gpusel) {
+    case SEL_FGD:                                                     // fgd_score.go:153-156
+      return fgd_gpu < 0 ? -1 : (1 << fgd_gpu);
+    case SEL_RANDOM: {                                                // :325-343 (Random contract)
+      const uint64_t nk = rand_node_key(seed, step, n.name_rank);
+      int pick = -1;
+      uint64_t best = 0;
+      for (int g = 0; g < kMaxGpu; ++g) {
+        if (g < n.gpu_cnt() && n.gl(g) >= p.milli) {
+          const uint64_t k = rand_gpu_key(nk, g);
+          if (pick < 0 || k > best) { best = k; pick = g; }
+        }
+      }
+      return pick < 0 ? -1 : (1 << pick);
+    }
+    case SEL_WORST: {                                                 // :305-323
+      int c = -1, cv = 0;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g) {
+        const int v = n.gl(g);
+        if (g < n.gpu_cnt() && v >= p.milli && (c < 0 || v > cv)) { c = g; cv = v; }
+      }
+      return c < 0 ? -1 : (1 << c);
+    }
+    default: {                                                        // best fit, :285-303
+      int c = -1, cv = 0;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g) {
+        const int v = n.gl(g);
+        if (g < n.gpu_cnt() && v >= p.milli && (c < 0 || v < cv)) { c = g; cv = v; }
+      }
+      return c < 0 ? -1 : (1 << c);
+    }
+  }
+}
+
+// Bind: scheduler cache assume (Requested += pod), open-gpu-share cache
+// AddOrUpdatePod (devices += milli), NodeInfo.Pods += pod (affinity tags).
+__device__ void apply_bind(NodeRec* nr, uint16_t* tags, const PodDev& p, int mask, int sign) {
+  NodeV n = load_node(nr);
+  n.cpu_left -= sign * p.cpu_req;
+  n.mem_left -= sign * p.mem;
+  const int pods = n.pods_left() - sign;
+  n.meta = (n.meta & 0xffff0000u) | ((uint32_t)pods & 0xffffu);
+  const uint32_t d = (uint32_t)(sign * (int)p.milli) & 0xffffu;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) {
+    // u16 lanes never borrow across halves: 0 <= left - milli and left + milli <= 1000
+    if ((mask >> g) & 1) n.g[g >> 1] = (g & 1) ? n.g[g >> 1] - (d << 16) : ((n.g[g >> 1] & 0xffff0000u) | ((n.g[g >> 1] - d) & 0xffffu));
+  }
+  store_node(nr, n);
+  if (p.tag >= 0) tags[p.tag] = (uint16_t)((int)tags[p.tag] + sign);
+}
+
+__global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
+  const int r = a.rep_first + (int)blockIdx.x / a.bpr;
+  const int b = (int)blockIdx.x % a.bpr;
+  const int tid = (int)threadIdx.x;
+  const ReplicaDev rp = a.reps[r];
+  const int step = (a.base ? *a.base : 0) + a.step_off;
+  if (!a.pod_override && step >= rp.n_events) return;
+  const PodDev p = a.pod_override ? *a.pod_override : rp.ev[step];
+  ResultDev* res_slot = a.res_override ? a.res_override : (rp.res + step);
+
+  if (p.flags & kPodDelete) {
+    // simulator.go:416-422 deletePod -> informer DeleteFunc -> GpuSharePlugin.removePod
+    if (a.mode == 0 && b == 0 && tid == 0) {
+      ResultDev out{-1, 0, 0, 0, ST_DELETED};
+      if (p.ref >= 0 && p.ref < step) {
+        const ResultDev c = rp.res[p.ref];
+        if (c.node >= 0) {
+          const PodDev cp = rp.ev[p.ref];
+          apply_bind(rp.nodes + c.node, rp.tags + (size_t)c.node * kTagStride, cp, c.gpu_mask, -1);
+          out.node = c.node;
+          out.gpu_mask = c.gpu_mask;
+        }
+      }
+      *res_slot = out;
+    }
+    return;
+  }
+
+  __shared__ NodeRec s_node[kNBMax];
+  __shared__ int s_off[kNBMax + 1];
+  __shared__ uint8_t s_item_node[kNBMax * kMaxCand];
+  __shared__ uint8_t s_item_code[kNBMax * kMaxCand];
+  __shared__ double s_F[kNBMax * kMaxCand];
+  __shared__ int4 s_tpi[kMaxTypical];
+  __shared__ double s_tpf[kMaxTypical];
+  __shared__ unsigned long long s_rkey[kBlock / 64];
+  __shared__ int s_rcnt[kBlock / 64], s_rerr[kBlock / 64], s_rlo[kBlock / 64], s_rhi[kBlock / 64];
+
+  const int n0 = b * a.NB;
+  const int nb = max(0, min(a.NB, a.N - n0));
+  const bool fgd = rp.policy == POL_FGD;
+  const bool share = is_share_pod(p);
+
+  if (fgd) {
+    for (int t = tid; t < rp.nt; t += kBlock) {
+      const TypDev q = rp.tp[t];
+      s_tpi[t] = make_int4(q.cpu, q.milli, q.num_eff, (int)q.tmask);
+      s_tpf[t] = q.freq;
+    }
+  }
+
+  // ---- phase 1: Filter (+ cheap scores) ----
+  bool feas = false, err = false;
+  int raw = 0, nc = 0, gpu = -1;
+  NodeV n{};
+  if (tid < nb) {
+    n = load_node(rp.nodes + n0 + tid);
+    store_node(&s_node[tid], n);
+    feas = filter_node(n, p);
+    if (feas) {
+      const int total = n.total();
+      switch (rp.policy) {
+        case POL_FGD: {
+          if (share) {
+            int c = 1;
+#pragma unroll
+            for (int g = 0; g < kMaxGpu; ++g) c += (g < n.gpu_cnt() && n.gl(g) >= p.milli) ? 1 : 0;
+            nc = c;
+          } else {
+            nc = 2;
+          }
+          break;
+        }
+        case POL_BESTFIT:
+          raw = bestfit_score(n, p, total);
+          if (raw < 0) { err = true; raw = 0; }
+          break;
+        case POL_DOTPROD:
+          raw = dotprod_score(n, p, total);
+          break;
+        case POL_PACKING: {
+          bool perr = false;
+          raw = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
+          err = perr;
+          break;
+        }
+        case POL_CLUSTERING:
+          if (p.tag == -2) err = true;
+          else raw = clustering_score(rp.tags + (size_t)(n0 + tid) * kTagStride, p.tag, total);
+          break;
+        default:  // POL_RANDOM: RandomScorePlugin.PreScore pick, as a 24-bit hash key
+          raw = (int)(rand_node_key(rp.seed, step, n.name_rank) >> 40);
+          break;
+      }
+    }
+  }
+
+  // ---- phase 2: FGD candidate evaluation over a compacted work list ----
+  if (fgd) {
+    if (tid < 64) {  // wave 0: exclusive scan of candidate counts
+      int v = tid < nb ? nc : 0;
+      int incl = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int w = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += w;
+      }
+      s_off[tid] = incl - v;
+      if (tid == 63) s_off[64] = incl;
+    }
+    __syncthreads();
+    if (tid < nb && nc > 0) {
+      int o = s_off[tid];
+      s_item_node[o] = (uint8_t)tid;
+      s_item_code[o] = 0;  // current state
+      ++o;
+      if (share) {
+#pragma unroll
+        for (int g = 0; g < kMaxGpu; ++g) {
+          if (g < n.gpu_cnt() && n.gl(g) >= p.milli) {
+            s_item_node[o] = (uint8_t)tid;
+            s_item_code[o] = (uint8_t)(1 + g);  // fgd_score.go:111-118 candidate on GPU g
+            ++o;
+          }
+        }
+      } else {
+        s_item_node[o] = (uint8_t)tid;
+        s_item_code[o] = 9;  // fgd_score.go:137-141 NodeResource.Sub
+      }
+    }
+    __syncthreads();
+    const int items = s_off[64];
+    for (int j = tid; j < items; j += kBlock) {
+      const NodeV m = load_node(&s_node[s_item_node[j]]);
+      const int code = s_item_code[j];
+      int gl[kMaxGpu];
+      unpack_gl(m, gl);
+      int cpuL = m.cpu_left;
+      if (code >= 1 && code <= 8) {
+        cpuL -= p.cpu_nz;
+#pragma unroll
+        for (int g = 0; g < kMaxGpu; ++g) gl[g] -= (g == code - 1) ? (int)p.milli : 0;
+      } else if (code == 9) {
+        bool ok = false;
+        const unsigned sm = sub_gpu_mask(gl, m.gpu_cnt(), cpuL, p, &ok);
+        if (ok) {
+          cpuL -= p.cpu_nz;
+#pragma unroll
+          for (int g = 0; g < kMaxGpu; ++g)
+            if ((sm >> g) & 1u) gl[g] -= p.milli;
+        }
+      }
+      s_F[j] = frag_F(cpuL, gl, 1u << m.gpu_type(), rp.nt, s_tpi, s_tpf);
+    }
+    __syncthreads();
+    if (tid < nb && feas) {
+      const int o = s_off[tid];
+      const double F0 = s_F[o];
+      if (share) {
+        int best = -1, bs = 0;
+        for (int k = 1; k < nc; ++k) {
+          const int fs = fgd_frag_score(F0, s_F[o + k]);
+          if (best < 0 || fs > bs) { bs = fs; best = s_item_code[o + k] - 1; }
+        }
+        raw = bs;
+        gpu = best;
+      } else {
+        raw = fgd_frag_score(F0, s_F[o + 1]);
+      }
+    }
+  }
+
+  if (a.mode == 1) {
+    if (tid < nb) {
+      a.out_feas[n0 + tid] = feas ? 1 : 0;
+      a.out_score[n0 + tid] = feas ? raw : 0;
+      a.out_gpu[n0 + tid] = feas ? select_gpus(n, p, rp.gpusel, gpu, rp.seed, step) : 0;
+    }
+    return;
+  }
+
+  // ---- phase 3: workgroup reduction of the packed argmax key ----
+  unsigned long long key = feas ? pack_key((unsigned)raw, n.name_rank, gpu) : 0ull;
+  int cnt = feas ? 1 : 0;
+  int lo = feas ? raw : 0x7fffffff, hi = feas ? raw : -1;
+  key = wave_max_u64(key);
+  cnt = wave_sum_i(cnt);
+  const int e = wave_max_i(err ? 1 : 0);
+  lo = wave_min_i(lo);
+  hi = wave_max_i(hi);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) { s_rkey[w] = key; s_rcnt[w] = cnt; s_rerr[w] = e; s_rlo[w] = lo; s_rhi[w] = hi; }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int i = 1; i < kBlock / 64; ++i) {
+    key = s_rkey[i] > key ? s_rkey[i] : key;
+    cnt += s_rcnt[i];
+    lo = min(lo, s_rlo[i]);
+    hi = max(hi, s_rhi[i]);
+  }
+  int errb = s_rerr[0] | s_rerr[1] | s_rerr[2] | s_rerr[3];
+
+  // ---- commit: last workgroup of the replica finishes the cycle ----
+  Accum* ac = a.acc + r;
+  if (cnt > 0) {
+    __hip_atomic_fetch_max(&ac->best, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&ac->nfeas, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_min(&ac->lo, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(&ac->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (errb) __hip_atomic_fetch_or(&ac->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every contribution performed before the ticket
+  const unsigned t = __hip_atomic_fetch_add(&ac->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != (unsigned)(a.bpr - 1)) return;
+
+  const unsigned long long best = __hip_atomic_exchange(&ac->best, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nfeas = __hip_atomic_exchange(&ac->nfeas, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int anyerr = __hip_atomic_exchange(&ac->err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int glo = __hip_atomic_exchange(&ac->lo, 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ghi = __hip_atomic_exchange(&ac->hi, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&ac->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+  if (nfeas > 0) {
+    const uint32_t wrank = 0xFFFFFFFFu - (uint32_t)((best >> 8) & 0xFFFFFFFFull);
+    const int wscore = (int)(best >> 40);
+    const int wgpu = (int)(best & 0xFF) - 1;
+    // find the winner's index: ranks are unique, the key carries ~rank; the
+    // node index is recovered from the rank->index table built on the host.
+    (void)wrank;
+    out.status = ST_OK;
+    if (nfeas > 1) {
+      if (anyerr) out.status = ST_ERROR;  // framework.go:650-656: a Score error aborts the cycle
+      else if (rp.policy == POL_BESTFIT) out.score = (ghi > glo ? 100 : 0) * 1000LL;  // NormalizeScore
+      else if (rp.policy == POL_RANDOM) out.score = 100 * 1000LL;
+      else out.score = (long long)wscore * 1000LL;
+    }
+    (void)glo;
+    if (out.status == ST_OK) {
+      // the rank -> node index map lives right after the replica's tags (see host)
+      const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
+      const int node = rank2idx[wrank];
+      NodeRec* nr = rp.nodes + node;
+      const NodeV wn = load_node(nr);
+      const int mask = select_gpus(wn, p, rp.gpusel, wgpu, rp.seed, step);
+      if (mask < 0) {
+        out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
+        out.score = 0;
+      } else {
+        apply_bind(nr, rp.tags + (size_t)node * kTagStride, p, mask, +1);
+        out.node = node;
+        out.gpu_mask = mask;
+      }
+    }
+  }
+  *res_slot = out;
+}
+
+__global__ void k_advance(int* base, int k) { *base += k; }
+
+// Reserve on an explicit node (ksim_engine_reserve): candidate F values for the
+// FGD selector are evaluated by one workgroup, then thread 0 binds.
+__global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, int r, PodDev p, int node, int step,
+                                                int* out_mask, int sign, int mask_in) {
+  const ReplicaDev rp = reps[r];
+  __shared__ int4 s_tpi[kMaxTypical];
+  __shared__ double s_tpf[kMaxTypical];
+  __shared__ double s_F[kMaxCand];
+  const int tid = (int)threadIdx.x;
+  NodeRec* nr = rp.nodes + node;
+  uint16_t* tg = rp.tags + (size_t)node * kTagStride;
+  if (sign < 0) {
+    if (tid == 0) apply_bind(nr, tg, p, mask_in, -1);
+    return;
+  }
+  const NodeV n = load_node(nr);
+  const bool need_fgd = rp.gpusel == SEL_FGD && is_share_pod(p) && p.milli > 0;
+  if (need_fgd) {
+    for (int t = tid; t < rp.nt; t += 64) {
+      const TypDev q = rp.tp[t];
+      s_tpi[t] = make_int4(q.cpu, q.milli, q.num_eff, (int)q.tmask);
+      s_tpf[t] = q.freq;
+    }
+    __syncthreads();
+    if (tid < kMaxCand) {
+      int gl[kMaxGpu];
+      unpack_gl(n, gl);
+      int cpuL = n.cpu_left;
+      bool valid = true;
+      if (tid > 0) {
+        cpuL -= p.cpu_nz;
+#pragma unroll
+        for (int g = 0; g < kMaxGpu; ++g) {
+          if (g == tid - 1) {
+            valid = g < n.gpu_cnt() && gl[g] >= p.milli;
+            gl[g] -= valid ? (int)p.milli : 0;
+          }
+        }
+      }
+      s_F[tid] = valid ? frag_F(cpuL, gl, 1u << n.gpu_type(), rp.nt, s_tpi, s_tpf) : 0.0;
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  int fgd_gpu = -1;
+  if (need_fgd) {
+    int bs = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      if (g < n.gpu_cnt() && n.gl(g) >= p.milli) {
+        const int fs = fgd_frag_score(s_F[0], s_F[1 + g]);
+        if (fgd_gpu < 0 || fs > bs) { bs = fs; fgd_gpu = g; }
+      }
+    }
+  }
+  const int mask = select_gpus(n, p, rp.gpusel, fgd_gpu, rp.seed, step);
+  *out_mask = mask;
+  if (mask >= 0) apply_bind(nr, tg, p, mask, +1);
+}
+
+#define KSIM_HIP(x)                                \
+  do {                                             \
+    hipError_t _e = (x);                           \
+    if (_e != hipSuccess) {                        \
+      std::fprintf(stderr, "ksim: %s failed: %s\n", #x, hipGetErrorString(_e)); \
+      return KSIM_EHIP;                            \
+    }                                              \
+  } while (0)
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Host engine object
+// ---------------------------------------------------------------------------
+struct ksim_engine {
+  int device = 0;
+  int N = 0, R = 0, NB = 32, bpr = 0, K = 256;
+  hipStream_t stream = nullptr;
+  NodeRec* d_nodes = nullptr;
+  NodeRec* d_nodes_init = nullptr;  // cluster state given to set_nodes (run() restarts from it)
+  uint16_t* d_tags = nullptr;  // per replica: N*16 u16 tags, then N int rank->index
+  uint16_t* d_tags_init = nullptr;
+  size_t tags_stride = 0;      // u16 elements per replica
+  TypDev* d_tp = nullptr;
+  Accum* d_acc = nullptr;
+  ReplicaDev* d_reps = nullptr;
+  int* d_base = nullptr;
+  int* d_scratch = nullptr;     // single-pod calls: [0] mask
+  PodDev* d_pod = nullptr;      // single-pod calls
+  ResultDev* d_res1 = nullptr;  // single-pod calls
+  uint8_t* d_feas = nullptr;
+  int32_t* d_score = nullptr;
+  int32_t* d_gpu = nullptr;
+  std::vector<ReplicaDev> reps;
+  std::vector<std::vector<ksim_node>> h_nodes;  // caller's static node fields per replica
+  std::vector<PodDev*> d_ev;
+  std::vector<ResultDev*> d_res;
+  std::vector<int> n_events;
+  std::vector<int> nt;
+  hipGraphExec_t graph = nullptr;
+  int graph_R = -1;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0;
+  int64_t last_steps = 0;
+};
+
+static int check_gfx950(int dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= dev) return KSIM_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return KSIM_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KSIM_ENODEV;
+  return KSIM_OK;
+}
+
+static int upload_reps(ksim_engine* e) {
+  KSIM_HIP(hipMemcpyAsync(e->d_reps, e->reps.data(), sizeof(ReplicaDev) * e->R, hipMemcpyHostToDevice, e->stream));
+  return KSIM_OK;
+}
+
+extern "C" {
+
+const char* ksim_strerror(int code) {
+  switch (code) {
+    case KSIM_OK: return "ok";
+    case KSIM_EINVAL: return "invalid argument";
+    case KSIM_ENOMEM: return "out of memory";
+    case KSIM_EHIP: return "HIP runtime error";
+    case KSIM_ERANGE: return "value outside engine encoding";
+    case KSIM_ESTATE: return "call out of order";
+    case KSIM_ENOTSUP: return "not supported";
+    case KSIM_ENODEV: return "no gfx950 device";
+    case KSIM_EIO: return "trace I/O error";
+    default: return "unknown error";
+  }
+}
+
+int ksim_abi_version(void) { return KSIM_ABI_VERSION; }
+
+int ksim_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  int c = 0;
+  for (int i = 0; i < n; ++i)
+    if (check_gfx950(i) == KSIM_OK) ++c;
+  return c;
+}
+
+int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim_engine** out) {
+  if (!out || n_nodes <= 0 || n_replicas <= 0) return KSIM_EINVAL;
+  *out = nullptr;
+  const int dev = cfg ? cfg->device : 0;
+  int rc = check_gfx950(dev);
+  if (rc) return rc;
+  KSIM_HIP(hipSetDevice(dev));
+  ksim_engine* e = new ksim_engine();
+  e->device = dev;
+  e->N = n_nodes;
+  e->R = n_replicas;
+  if (cfg && cfg->nodes_per_block > 0) e->NB = std::min(cfg->nodes_per_block, kNBMax);
+  if (cfg && cfg->steps_per_graph > 0) e->K = cfg->steps_per_graph;
+  e->bpr = (n_nodes + e->NB - 1) / e->NB;
+  e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
+  KSIM_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  KSIM_HIP(hipMalloc(&e->d_nodes, sizeof(NodeRec) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_tags, sizeof(uint16_t) * e->tags_stride * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_nodes_init, sizeof(NodeRec) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_tags_init, sizeof(uint16_t) * e->tags_stride * n_replicas));
+  KSIM_HIP(hipMemset(e->d_nodes, 0, sizeof(NodeRec) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMemset(e->d_nodes_init, 0, sizeof(NodeRec) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMemset(e->d_tags_init, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_tp, sizeof(TypDev) * kMaxTypical * (size_t)n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_acc, sizeof(Accum) * (size_t)n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_reps, sizeof(ReplicaDev) * (size_t)n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_base, sizeof(int) * 4));
+  KSIM_HIP(hipMalloc(&e->d_scratch, sizeof(int) * 4));
+  KSIM_HIP(hipMalloc(&e->d_pod, sizeof(PodDev)));
+  KSIM_HIP(hipMalloc(&e->d_res1, sizeof(ResultDev)));
+  KSIM_HIP(hipMalloc(&e->d_feas, (size_t)n_nodes));
+  KSIM_HIP(hipMalloc(&e->d_score, sizeof(int32_t) * n_nodes));
+  KSIM_HIP(hipMalloc(&e->d_gpu, sizeof(int32_t) * n_nodes));
+  KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
+  std::vector<Accum> acc(n_replicas);
+  for (auto& a : acc) {
+    std::memset(&a, 0, sizeof a);
+    a.lo = 0x7fffffff;
+    a.hi = -1;
+  }
+  KSIM_HIP(hipMemcpy(e->d_acc, acc.data(), sizeof(Accum) * n_replicas, hipMemcpyHostToDevice));
+  e->reps.resize(n_replicas);
+  e->h_nodes.resize(n_replicas);
+  e->d_ev.assign(n_replicas, nullptr);
+  e->d_res.assign(n_replicas, nullptr);
+  e->n_events.assign(n_replicas, 0);
+  e->nt.assign(n_replicas, 0);
+  for (int r = 0; r < n_replicas; ++r) {
+    ReplicaDev& rp = e->reps[r];
+    std::memset(&rp, 0, sizeof rp);
+    rp.policy = POL_FGD;
+    rp.gpusel = SEL_FGD;
+    rp.tp = e->d_tp + (size_t)r * kMaxTypical;
+    rp.nodes = e->d_nodes + (size_t)r * n_nodes;
+    rp.tags = e->d_tags + (size_t)r * e->tags_stride;
+  }
+  KSIM_HIP(hipEventCreate(&e->ev0));
+  KSIM_HIP(hipEventCreate(&e->ev1));
+  rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  *out = e;
+  return KSIM_OK;
+}
+
+void ksim_engine_destroy(ksim_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->graph) (void)hipGraphExecDestroy(e->graph);
+  for (auto p : e->d_ev) (void)hipFree(p);
+  for (auto p : e->d_res) (void)hipFree(p);
+  void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
+                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu};
+  for (void* p : bufs) (void)hipFree(p);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+static int to_pod_dev(const ksim_pod& s, PodDev* d) {
+  if (s.gpu_milli < 0 || s.gpu_milli > kMilli || s.gpu_count < 0 || s.gpu_count > kMaxGpu) return KSIM_ERANGE;
+  if (s.cpu_milli < 0 || s.cpu_milli > 0x3fffffff || s.cpu_nz_milli < 0 || s.cpu_nz_milli > 0x3fffffff ||
+      s.mem_mib < 0 || s.mem_mib > 0x3fffffff)
+    return KSIM_ERANGE;
+  std::memset(d, 0, sizeof *d);
+  d->cpu_req = (int32_t)s.cpu_milli;
+  d->cpu_nz = (int32_t)s.cpu_nz_milli;
+  d->mem = (int32_t)s.mem_mib;
+  d->milli = (int16_t)s.gpu_milli;
+  d->num = (int8_t)s.gpu_count;
+  // GetGpuAffinityFromPodAnnotation (open-gpu-share/utils/pod.go:111-123)
+  if (s.gpu_count == 0) d->tag = -1;
+  else if (s.gpu_count == 1 && s.gpu_milli < kMilli) d->tag = 0;
+  else if (s.gpu_milli == kMilli) d->tag = (int8_t)s.gpu_count;
+  else d->tag = -2;
+  d->tmask = s.type_mask;
+  d->ref = s.ref;
+  d->flags = s.is_delete ? kPodDelete : 0u;
+  return KSIM_OK;
+}
+
+int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
+  if (!e || !nodes || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  std::vector<NodeRec> h(e->N);
+  std::vector<uint16_t> tags(e->tags_stride, 0);
+  int* rank2idx = reinterpret_cast<int*>(tags.data() + (size_t)e->N * kTagStride);
+  std::vector<char> seen(e->N, 0);
+  for (int i = 0; i < e->N; ++i) {
+    const ksim_node& s = nodes[i];
+    if (s.gpu_count < 0 || s.gpu_count > kMaxGpu || s.gpu_type < 0 || s.gpu_type >= KSIM_MAX_TYPES)
+      return KSIM_ERANGE;
+    if (s.name_rank >= (uint32_t)e->N || seen[s.name_rank]) return KSIM_EINVAL;
+    seen[s.name_rank] = 1;
+    const int64_t cpu_left = s.cpu_alloc_milli - s.cpu_used_milli;
+    const int64_t mem_left = s.mem_alloc_mib - s.mem_used_mib;
+    const int64_t pods_left = (int64_t)s.pods_alloc - s.pods_used;
+    if (cpu_left < -0x3fffffff || cpu_left > 0x3fffffff || mem_left < -0x3fffffff || mem_left > 0x3fffffff ||
+        pods_left > 32767 || pods_left < -32768)
+      return KSIM_ERANGE;
+    NodeRec& n = h[i];
+    std::memset(&n, 0, sizeof n);
+    n.cpu_left = (int32_t)cpu_left;
+    n.mem_left = (int32_t)mem_left;
+    n.pods_left = (int16_t)pods_left;
+    n.gpu_cnt = (uint8_t)s.gpu_count;
+    n.gpu_type = (uint8_t)s.gpu_type;
+    n.name_rank = s.name_rank;
+    for (int g = 0; g < kMaxGpu; ++g) {
+      const int left = g < s.gpu_count ? kMilli - s.gpu_used_milli[g] : 0;
+      if (left < 0 || left > kMilli) return KSIM_ERANGE;
+      n.gl[g] = (uint16_t)left;
+    }
+    for (int k = 0; k < kNumTags; ++k) tags[(size_t)i * kTagStride + k] = (uint16_t)s.tag_count[k];
+    rank2idx[s.name_rank] = i;
+  }
+  e->h_nodes[replica].assign(nodes, nodes + e->N);
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(e->reps[replica].nodes, h.data(), sizeof(NodeRec) * e->N, hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_tags + (size_t)replica * e->tags_stride, tags.data(), sizeof(uint16_t) * e->tags_stride,
+                          hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_nodes_init + (size_t)replica * e->N, h.data(), sizeof(NodeRec) * e->N,
+                          hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_tags_init + (size_t)replica * e->tags_stride, tags.data(),
+                          sizeof(uint16_t) * e->tags_stride, hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp, int n) {
+  if (!e || replica < 0 || replica >= e->R || n < 0 || (n > 0 && !tp)) return KSIM_EINVAL;
+  std::vector<TypDev> h;
+  for (int i = 0; i < n; ++i) {
+    // frag.go:154-158: entries with freq outside [0,1] are skipped
+    if (tp[i].freq < 0 || tp[i].freq > 1 || tp[i].freq != tp[i].freq) continue;
+    if (tp[i].gpu_milli < 0 || tp[i].gpu_milli > 0x7fff || tp[i].cpu_milli > 0x3fffffff || tp[i].cpu_milli < -0x3fffffff)
+      return KSIM_ERANGE;
+    TypDev d;
+    d.cpu = (int32_t)tp[i].cpu_milli;
+    d.milli = tp[i].gpu_milli;
+    d.num_eff = std::max(tp[i].gpu_count, 1);
+    d.tmask = tp[i].type_mask;
+    d.freq = tp[i].freq;
+    h.push_back(d);
+  }
+  if ((int)h.size() > kMaxTypical) return KSIM_ERANGE;
+  KSIM_HIP(hipSetDevice(e->device));
+  if (!h.empty())
+    KSIM_HIP(hipMemcpyAsync(e->d_tp + (size_t)replica * kMaxTypical, h.data(), sizeof(TypDev) * h.size(),
+                            hipMemcpyHostToDevice, e->stream));
+  e->reps[replica].nt = (int)h.size();
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed) {
+  if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  if (policy < POL_FGD || policy > POL_RANDOM || gpusel < SEL_BEST || gpusel > SEL_FGD) return KSIM_ENOTSUP;
+  e->reps[replica].policy = policy;
+  e->reps[replica].gpusel = gpusel;
+  e->reps[replica].seed = seed;
+  KSIM_HIP(hipSetDevice(e->device));
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+static StepArgs base_args(ksim_engine* e) {
+  StepArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.reps = e->d_reps;
+  a.acc = e->d_acc;
+  a.N = e->N;
+  a.NB = e->NB;
+  a.bpr = e->bpr;
+  return a;
+}
+
+int ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, int32_t step, uint8_t* feasible,
+                             int32_t* score, int32_t* gpu_mask) {
+  if (!e || !pod || replica < 0 || replica >= e->R || !feasible || !score || !gpu_mask) return KSIM_EINVAL;
+  PodDev p;
+  int rc = to_pod_dev(*pod, &p);
+  if (rc) return rc;
+  if (p.flags & kPodDelete) return KSIM_EINVAL;
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(e->d_pod, &p, sizeof p, hipMemcpyHostToDevice, e->stream));
+  StepArgs a = base_args(e);
+  a.rep_first = replica;
+  a.step_off = step;
+  a.pod_override = e->d_pod;
+  a.res_override = e->d_res1;
+  a.mode = 1;
+  a.out_feas = e->d_feas;
+  a.out_score = e->d_score;
+  a.out_gpu = e->d_gpu;
+  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a);
+  KSIM_HIP(hipGetLastError());
+  KSIM_HIP(hipMemcpyAsync(feasible, e->d_feas, e->N, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipMemcpyAsync(score, e->d_score, sizeof(int32_t) * e->N, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipMemcpyAsync(gpu_mask, e->d_gpu, sizeof(int32_t) * e->N, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_schedule(ksim_engine* e, int replica, const ksim_pod* pod, int32_t step, ksim_result* out) {
+  if (!e || !pod || !out || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  PodDev p;
+  int rc = to_pod_dev(*pod, &p);
+  if (rc) return rc;
+  if (p.flags & kPodDelete) return KSIM_EINVAL;  // deletions go through ksim_engine_unreserve
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(e->d_pod, &p, sizeof p, hipMemcpyHostToDevice, e->stream));
+  StepArgs a = base_args(e);
+  a.rep_first = replica;
+  a.step_off = step;
+  a.pod_override = e->d_pod;
+  a.res_override = e->d_res1;
+  a.mode = 0;
+  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a);
+  KSIM_HIP(hipGetLastError());
+  ResultDev r;
+  KSIM_HIP(hipMemcpyAsync(&r, e->d_res1, sizeof r, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  std::memcpy(out, &r, sizeof r);
+  return KSIM_OK;
+}
+
+int ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t step, int32_t* gpu_mask_out) {
+  if (!e || !pod || !gpu_mask_out || replica < 0 || replica >= e->R || node < 0 || node >= e->N) return KSIM_EINVAL;
+  PodDev p;
+  int rc = to_pod_dev(*pod, &p);
+  if (rc) return rc;
+  KSIM_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, replica, p, node, step, e->d_scratch, +1, 0);
+  KSIM_HIP(hipGetLastError());
+  int m = 0;
+  KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  *gpu_mask_out = m;
+  return m < 0 ? KSIM_ESTATE : KSIM_OK;
+}
+
+int ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask) {
+  if (!e || !pod || replica < 0 || replica >= e->R || node < 0 || node >= e->N) return KSIM_EINVAL;
+  PodDev p;
+  int rc = to_pod_dev(*pod, &p);
+  if (rc) return rc;
+  KSIM_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, replica, p, node, 0, e->d_scratch, -1,
+                     (int)gpu_mask);
+  KSIM_HIP(hipGetLastError());
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events, int n) {
+  if (!e || replica < 0 || replica >= e->R || n < 0 || (n > 0 && !events)) return KSIM_EINVAL;
+  std::vector<PodDev> h(n);
+  for (int i = 0; i < n; ++i) {
+    int rc = to_pod_dev(events[i], &h[i]);
+    if (rc) return rc;
+    if ((h[i].flags & kPodDelete) && (h[i].ref < 0 || h[i].ref >= i)) return KSIM_EINVAL;
+  }
+  KSIM_HIP(hipSetDevice(e->device));
+  if (e->d_ev[replica]) { KSIM_HIP(hipFree(e->d_ev[replica])); e->d_ev[replica] = nullptr; }
+  if (e->d_res[replica]) { KSIM_HIP(hipFree(e->d_res[replica])); e->d_res[replica] = nullptr; }
+  const size_t ne = (size_t)std::max(n, 1);
+  KSIM_HIP(hipMalloc(&e->d_ev[replica], sizeof(PodDev) * ne));
+  KSIM_HIP(hipMalloc(&e->d_res[replica], sizeof(ResultDev) * ne));
+  if (n > 0) KSIM_HIP(hipMemcpyAsync(e->d_ev[replica], h.data(), sizeof(PodDev) * n, hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipMemsetAsync(e->d_res[replica], 0xff, sizeof(ResultDev) * ne, e->stream));
+  e->n_events[replica] = n;
+  e->reps[replica].ev = e->d_ev[replica];
+  e->reps[replica].res = e->d_res[replica];
+  e->reps[replica].n_events = n;
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+// Every replica back to the cluster state given to set_nodes (device-to-device).
+static int reset_state(ksim_engine* e) {
+  KSIM_HIP(hipMemcpyAsync(e->d_nodes, e->d_nodes_init, sizeof(NodeRec) * (size_t)e->N * e->R, hipMemcpyDeviceToDevice,
+                          e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride * e->R, hipMemcpyDeviceToDevice,
+                          e->stream));
+  return KSIM_OK;
+}
+
+static int build_graph(ksim_engine* e) {
+  if (e->graph && e->graph_R == e->R) return KSIM_OK;
+  if (e->graph) { (void)hipGraphExecDestroy(e->graph); e->graph = nullptr; }
+  hipGraph_t g;
+  KSIM_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+  StepArgs a = base_args(e);
+  a.rep_first = 0;
+  a.base = e->d_base;
+  for (int i = 0; i < e->K; ++i) {
+    a.step_off = i;
+    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
+  }
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_base, e->K);
+  KSIM_HIP(hipStreamEndCapture(e->stream, &g));
+  KSIM_HIP(hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0));
+  KSIM_HIP(hipGraphDestroy(g));
+  e->graph_R = e->R;
+  return KSIM_OK;
+}
+
+int ksim_engine_run(ksim_engine* e) {
+  if (!e) return KSIM_EINVAL;
+  int max_ev = 0;
+  for (int r = 0; r < e->R; ++r) {
+    if (!e->d_ev[r]) return KSIM_ESTATE;
+    max_ev = std::max(max_ev, e->n_events[r]);
+  }
+  KSIM_HIP(hipSetDevice(e->device));
+  int rc = build_graph(e);
+  if (rc) return rc;
+  const int reps = (max_ev + e->K - 1) / e->K;
+  KSIM_HIP(hipEventRecord(e->ev0, e->stream));
+  rc = reset_state(e);
+  if (rc) return rc;
+  KSIM_HIP(hipMemsetAsync(e->d_base, 0, sizeof(int), e->stream));
+  for (int i = 0; i < reps; ++i) KSIM_HIP(hipGraphLaunch(e->graph, e->stream));
+  KSIM_HIP(hipEventRecord(e->ev1, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  float ms = 0;
+  KSIM_HIP(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  e->last_ms = ms;
+  e->last_steps = max_ev;
+  return KSIM_OK;
+}
+
+int ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us) {
+  if (!e || !mean_kernel_us || n_steps <= 0) return KSIM_EINVAL;
+  KSIM_HIP(hipSetDevice(e->device));
+  std::vector<hipEvent_t> evs(2 * n_steps);
+  for (auto& x : evs) KSIM_HIP(hipEventCreate(&x));
+  int rc = reset_state(e);
+  if (rc) return rc;
+  StepArgs a = base_args(e);
+  a.rep_first = 0;
+  a.base = nullptr;
+  for (int i = 0; i < n_steps; ++i) {
+    a.step_off = i;
+    KSIM_HIP(hipEventRecord(evs[2 * i], e->stream));
+    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
+    KSIM_HIP(hipEventRecord(evs[2 * i + 1], e->stream));
+  }
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  double tot = 0;
+  for (int i = 0; i < n_steps; ++i) {
+    float ms = 0;
+    KSIM_HIP(hipEventElapsedTime(&ms, evs[2 * i], evs[2 * i + 1]));
+    tot += ms;
+  }
+  for (auto& x : evs) (void)hipEventDestroy(x);
+  *mean_kernel_us = tot * 1000.0 / n_steps;
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_ms(ksim_engine* e, double* ms) {
+  if (!e || !ms) return KSIM_EINVAL;
+  *ms = e->last_ms;
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps) {
+  if (!e || !steps) return KSIM_EINVAL;
+  *steps = e->last_steps;
+  return KSIM_OK;
+}
+
+int ksim_engine_get_results(ksim_engine* e, int replica, ksim_result* out, int n) {
+  if (!e || !out || replica < 0 || replica >= e->R || n < 0 || n > e->n_events[replica]) return KSIM_EINVAL;
+  if (n == 0) return KSIM_OK;
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(out, e->d_res[replica], sizeof(ResultDev) * n, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_get_nodes(ksim_engine* e, int replica, ksim_node* out) {
+  if (!e || !out || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  KSIM_HIP(hipSetDevice(e->device));
+  std::vector<NodeRec> h(e->N);
+  std::vector<uint16_t> tags(e->tags_stride);
+  KSIM_HIP(hipMemcpyAsync(h.data(), e->reps[replica].nodes, sizeof(NodeRec) * e->N, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipMemcpyAsync(tags.data(), e->d_tags + (size_t)replica * e->tags_stride, sizeof(uint16_t) * e->tags_stride,
+                          hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  if (e->h_nodes[replica].size() != (size_t)e->N) return KSIM_ESTATE;
+  for (int i = 0; i < e->N; ++i) {
+    ksim_node& o = out[i];
+    const NodeRec& n = h[i];
+    o = e->h_nodes[replica][i];  // static fields as given to set_nodes
+    o.cpu_used_milli = o.cpu_alloc_milli - n.cpu_left;
+    o.mem_used_mib = o.mem_alloc_mib - n.mem_left;
+    o.pods_used = o.pods_alloc - n.pods_left;
+    for (int g = 0; g < kMaxGpu; ++g) o.gpu_used_milli[g] = g < n.gpu_cnt ? kMilli - (int)n.gl[g] : 0;
+    for (int k = 0; k < kNumTags; ++k) o.tag_count[k] = tags[(size_t)i * kTagStride + k];
+  }
+  return KSIM_OK;
+}
+
+}  // extern "C"

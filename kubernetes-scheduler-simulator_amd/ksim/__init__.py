@@ -1,0 +1,355 @@
+"""ksim -- Python binding of libksim_hip.so (the MI355X scoring engine).
+
+A thin ctypes layer over the C ABI in include/ksim_engine.h and
+include/ksim_trace.h.  It mirrors the reference's plugin vocabulary
+(Filter / Score / Reserve / Unreserve / schedule cycle; FGDScore, BestFitScore,
+DotProductScore, GpuPackingScore, GpuClusteringScore, RandomScore) so tests and
+bench.py read like the reference's own tests.
+
+There is no CPU fallback: compute calls raise KsimError(KSIM_ENODEV) when no
+gfx950 device is present, and importing the extension fails loudly when
+lib/libksim_hip.so has not been built.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libksim_hip.so")
+DATA_DIR = os.path.join(REPO_DIR, "data", "openb")
+
+KSIM_OK, KSIM_EINVAL, KSIM_ENOMEM, KSIM_EHIP, KSIM_ERANGE, KSIM_ESTATE, KSIM_ENOTSUP, KSIM_ENODEV, KSIM_EIO = \
+    0, -1, -2, -3, -4, -5, -6, -7, -8
+KSIM_TYPE_ANY = 0xFFFFFFFF
+MAX_GPU = 8
+NUM_TAGS = 9
+
+POLICY = {"FGD": 0, "BestFit": 1, "DotProd": 2, "GpuPacking": 3, "GpuClustering": 4, "Random": 5}
+GPUSEL = {"best": 0, "worst": 1, "random": 2, "FGD": 3}
+# experiments/run_scripts/expected_run_scripts_0511.sh: policy -> gpuSelMethod
+DEFAULT_GPUSEL = {"FGD": "FGD", "BestFit": "best", "DotProd": "best", "GpuPacking": "best",
+                  "GpuClustering": "best", "Random": "random"}
+SCHEDULED, UNSCHEDULABLE, ERROR, DELETED = 0, 1, 2, 3
+
+
+class KsimError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib().ksim_strerror(code).decode() if _LIB is not None else str(code)
+        super().__init__("%s: %s (%d)" % (what, msg, code))
+
+
+class Node(C.Structure):
+    _fields_ = [("cpu_alloc_milli", C.c_int64), ("mem_alloc_mib", C.c_int64), ("pods_alloc", C.c_int32),
+                ("gpu_count", C.c_int32), ("gpu_type", C.c_int32), ("name_rank", C.c_uint32),
+                ("cpu_used_milli", C.c_int64), ("mem_used_mib", C.c_int64), ("pods_used", C.c_int32),
+                ("gpu_used_milli", C.c_int32 * MAX_GPU), ("tag_count", C.c_int32 * NUM_TAGS),
+                ("reserved", C.c_int32)]
+
+
+class Pod(C.Structure):
+    _fields_ = [("cpu_milli", C.c_int64), ("cpu_nz_milli", C.c_int64), ("mem_mib", C.c_int64),
+                ("gpu_milli", C.c_int32), ("gpu_count", C.c_int32), ("type_mask", C.c_uint32),
+                ("is_delete", C.c_int32), ("ref", C.c_int32), ("reserved", C.c_int32)]
+
+
+class Typical(C.Structure):
+    _fields_ = [("cpu_milli", C.c_int64), ("gpu_milli", C.c_int32), ("gpu_count", C.c_int32),
+                ("type_mask", C.c_uint32), ("reserved", C.c_int32), ("freq", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("node", C.c_int32), ("gpu_mask", C.c_int32), ("score", C.c_int64), ("n_feasible", C.c_int32),
+                ("status", C.c_int32)]
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("nodes_per_block", C.c_int32), ("steps_per_graph", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class TraceNode(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("cpu_milli", C.c_int64), ("mem_mib", C.c_int64),
+                ("gpu_count", C.c_int32), ("gpu_type", C.c_int32)]
+
+
+class TracePod(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("cpu_milli", C.c_int64), ("mem_mib", C.c_int64),
+                ("gpu_milli", C.c_int32), ("gpu_count", C.c_int32), ("type_mask", C.c_uint32),
+                ("gpu_spec", C.c_char * 64)]
+
+
+class TypicalCfg(C.Structure):
+    _fields_ = [("is_involved_cpu_pods", C.c_int32), ("pod_popularity_threshold", C.c_int32),
+                ("pod_increase_step", C.c_int32), ("reserved", C.c_int32), ("gpu_res_weight", C.c_double)]
+
+
+class ReplayCfg(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("tune_ratio", C.c_double), ("shuffle", C.c_int32), ("reserved", C.c_int32)]
+
+
+assert C.sizeof(Node) == 128 and C.sizeof(Pod) == 48 and C.sizeof(Typical) == 32 and C.sizeof(Result) == 24
+
+_LIB = None
+
+# name -> (restype, argtypes); the set must equal the functions declared in include/*.h
+_P = C.POINTER
+_VP = C.c_void_p
+SIGNATURES = {
+    "ksim_strerror": (C.c_char_p, [C.c_int]),
+    "ksim_abi_version": (C.c_int, []),
+    "ksim_device_count": (C.c_int, []),
+    "ksim_engine_create": (C.c_int, [_P(Config), C.c_int, C.c_int, _P(_VP)]),
+    "ksim_engine_destroy": (None, [_VP]),
+    "ksim_engine_set_nodes": (C.c_int, [_VP, C.c_int, _P(Node)]),
+    "ksim_engine_set_typical": (C.c_int, [_VP, C.c_int, _P(Typical), C.c_int]),
+    "ksim_engine_set_policy": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_uint64]),
+    "ksim_engine_filter_score": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int32, _P(C.c_uint8), _P(C.c_int32),
+                                           _P(C.c_int32)]),
+    "ksim_engine_reserve": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32, _P(C.c_int32)]),
+    "ksim_engine_unreserve": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32]),
+    "ksim_engine_schedule": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int32, _P(Result)]),
+    "ksim_engine_load_events": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int]),
+    "ksim_engine_run": (C.c_int, [_VP]),
+    "ksim_engine_get_results": (C.c_int, [_VP, C.c_int, _P(Result), C.c_int]),
+    "ksim_engine_get_nodes": (C.c_int, [_VP, C.c_int, _P(Node)]),
+    "ksim_engine_time_steps": (C.c_int, [_VP, C.c_int, _P(C.c_double)]),
+    "ksim_engine_last_run_ms": (C.c_int, [_VP, _P(C.c_double)]),
+    "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
+    "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
+    "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
+    "ksim_trace_free": (None, [_VP]),
+    "ksim_trace_num_nodes": (C.c_int, [_VP]),
+    "ksim_trace_num_pods": (C.c_int, [_VP]),
+    "ksim_trace_num_types": (C.c_int, [_VP]),
+    "ksim_trace_type_name": (C.c_int, [_VP, C.c_int, C.c_char_p, C.c_int]),
+    "ksim_trace_node_at": (C.c_int, [_VP, C.c_int, _P(TraceNode)]),
+    "ksim_trace_pod_at": (C.c_int, [_VP, C.c_int, _P(TracePod)]),
+    "ksim_trace_typical": (C.c_int, [_VP, _P(TypicalCfg), _P(Typical), C.c_int, _P(C.c_int)]),
+    "ksim_trace_replay": (C.c_int, [_VP, _P(ReplayCfg), _P(Pod), C.c_int, _P(C.c_int), _P(C.c_int32), _P(Node),
+                                    _P(C.c_int32)]),
+}
+
+
+def build(quiet=True):
+    """Compile libksim_hip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-C", PKG_DIR] + (["-s"] if quiet else [])
+    subprocess.run(cmd, check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libksim_hip.so not built (%s); run `make -C %s` or __graft_entry__.build()"
+                              % (LIB_PATH, PKG_DIR))
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what):
+    if rc != KSIM_OK:
+        raise KsimError(rc, what)
+    return rc
+
+
+def device_count():
+    return lib().ksim_device_count()
+
+
+# ---------------------------------------------------------------------------
+# trace / replay driver
+# ---------------------------------------------------------------------------
+class Trace:
+    """An openb trace (nodes + original workload) loaded by the C++ host driver."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def openb(cls, pod_list="default", data_dir=DATA_DIR, node_csv=None):
+        pod_csv = pod_list if pod_list.endswith(".csv") else os.path.join(data_dir, "openb_pod_list_%s.csv" % pod_list)
+        node_csv = node_csv or os.path.join(data_dir, "openb_node_list_gpu_node.csv")
+        h = _VP()
+        check(lib().ksim_trace_load_openb(node_csv.encode(), pod_csv.encode(), C.byref(h)), "ksim_trace_load_openb")
+        return cls(h)
+
+    def synthetic(self, n_nodes, n_pods, seed=0):
+        h = _VP()
+        check(lib().ksim_trace_synthetic(self.h, n_nodes, n_pods, seed, C.byref(h)), "ksim_trace_synthetic")
+        return Trace(h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _LIB is not None:
+            _LIB.ksim_trace_free(self.h)
+            self.h = None
+
+    @property
+    def num_nodes(self):
+        return lib().ksim_trace_num_nodes(self.h)
+
+    @property
+    def num_pods(self):
+        return lib().ksim_trace_num_pods(self.h)
+
+    def type_names(self):
+        out = []
+        buf = C.create_string_buffer(64)
+        for i in range(lib().ksim_trace_num_types(self.h)):
+            check(lib().ksim_trace_type_name(self.h, i, buf, 64), "type_name")
+            out.append(buf.value.decode())
+        return out
+
+    def nodes(self):
+        out = []
+        n = TraceNode()
+        for i in range(self.num_nodes):
+            check(lib().ksim_trace_node_at(self.h, i, C.byref(n)), "node_at")
+            out.append(dict(name=n.name.decode(), cpu=n.cpu_milli, mem=n.mem_mib, gpu=n.gpu_count, type=n.gpu_type))
+        return out
+
+    def pods(self):
+        out = []
+        p = TracePod()
+        for i in range(self.num_pods):
+            check(lib().ksim_trace_pod_at(self.h, i, C.byref(p)), "pod_at")
+            out.append(dict(name=p.name.decode(), cpu=p.cpu_milli, mem=p.mem_mib, milli=p.gpu_milli,
+                            num=p.gpu_count, mask=p.type_mask, spec=p.gpu_spec.decode()))
+        return out
+
+    def typical(self, threshold=95, step=1, involve_cpu=True, gpu_res_weight=0.0):
+        """GetTypicalPods with the paper's TypicalPodsConfig (generate_config_and_run.py:59-62)."""
+        cfg = TypicalCfg(1 if involve_cpu else 0, threshold, step, 0, gpu_res_weight)
+        n = C.c_int(0)
+        cap = 4096
+        arr = (Typical * cap)()
+        check(lib().ksim_trace_typical(self.h, C.byref(cfg), arr, cap, C.byref(n)), "ksim_trace_typical")
+        return arr, n.value
+
+    def replay(self, seed, tune_ratio=1.3, shuffle=True):
+        """Event stream + empty cluster for one replica (SortClusterPods + tuning + node naming)."""
+        cfg = ReplayCfg(seed, tune_ratio, 1 if shuffle else 0, 0)
+        nn = self.num_nodes
+        nodes = (Node * nn)()
+        prefix = (C.c_int32 * nn)()
+        n = C.c_int(0)
+        rc = lib().ksim_trace_replay(self.h, C.byref(cfg), None, 0, C.byref(n), None, nodes, prefix)
+        if rc not in (KSIM_OK, KSIM_ERANGE):
+            check(rc, "ksim_trace_replay")
+        cap = max(1, n.value)
+        events = (Pod * cap)()
+        pidx = (C.c_int32 * cap)()
+        check(lib().ksim_trace_replay(self.h, C.byref(cfg), events, cap, C.byref(n), pidx, nodes, prefix),
+              "ksim_trace_replay")
+        return Replay(events, n.value, np.ctypeslib.as_array(pidx)[: n.value].copy(), nodes,
+                      np.ctypeslib.as_array(prefix).copy())
+
+
+class Replay:
+    def __init__(self, events, n, pod_index, nodes, prefix):
+        self.events, self.n, self.pod_index, self.nodes, self.prefix = events, n, pod_index, nodes, prefix
+
+    def node_names(self, trace_nodes):
+        return ["%04d-%s" % (self.prefix[i], trace_nodes[i]["name"]) for i in range(len(trace_nodes))]
+
+
+# ---------------------------------------------------------------------------
+# engine
+# ---------------------------------------------------------------------------
+class Engine:
+    """R independent simulated clusters of N nodes on one MI355X."""
+
+    def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0):
+        self.N, self.R = n_nodes, n_replicas
+        cfg = Config(device, nodes_per_block, steps_per_graph, 0)
+        h = _VP()
+        check(lib().ksim_engine_create(C.byref(cfg), n_nodes, n_replicas, C.byref(h)), "ksim_engine_create")
+        self.h = h
+        self.n_events = [0] * n_replicas
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ksim_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def set_nodes(self, r, nodes):
+        check(lib().ksim_engine_set_nodes(self.h, r, nodes), "set_nodes")
+
+    def set_typical(self, r, tp, n):
+        check(lib().ksim_engine_set_typical(self.h, r, tp, n), "set_typical")
+
+    def set_policy(self, r, policy="FGD", gpusel=None, seed=0):
+        gs = gpusel or DEFAULT_GPUSEL[policy]
+        check(lib().ksim_engine_set_policy(self.h, r, POLICY[policy], GPUSEL[gs], seed), "set_policy")
+
+    # plugin-level entry points
+    def filter_score(self, r, pod, step=0):
+        feas = (C.c_uint8 * self.N)()
+        score = (C.c_int32 * self.N)()
+        gpu = (C.c_int32 * self.N)()
+        check(lib().ksim_engine_filter_score(self.h, r, C.byref(pod), step, feas, score, gpu), "filter_score")
+        return (np.ctypeslib.as_array(feas).copy(), np.ctypeslib.as_array(score).copy(),
+                np.ctypeslib.as_array(gpu).copy())
+
+    def reserve(self, r, pod, node, step=0):
+        m = C.c_int32(0)
+        rc = lib().ksim_engine_reserve(self.h, r, C.byref(pod), node, step, C.byref(m))
+        check(rc, "reserve")
+        return m.value
+
+    def unreserve(self, r, pod, node, gpu_mask):
+        check(lib().ksim_engine_unreserve(self.h, r, C.byref(pod), node, gpu_mask), "unreserve")
+
+    def schedule(self, r, pod, step=0):
+        res = Result()
+        check(lib().ksim_engine_schedule(self.h, r, C.byref(pod), step, C.byref(res)), "schedule")
+        return res
+
+    # whole-trace device loop
+    def load_events(self, r, events, n):
+        check(lib().ksim_engine_load_events(self.h, r, events, n), "load_events")
+        self.n_events[r] = n
+
+    def run(self):
+        check(lib().ksim_engine_run(self.h), "run")
+        ms = C.c_double(0)
+        check(lib().ksim_engine_last_run_ms(self.h, C.byref(ms)), "last_run_ms")
+        return ms.value
+
+    def last_run_steps(self):
+        s = C.c_int64(0)
+        check(lib().ksim_engine_last_run_steps(self.h, C.byref(s)), "last_run_steps")
+        return s.value
+
+    def time_steps(self, n_steps):
+        us = C.c_double(0)
+        check(lib().ksim_engine_time_steps(self.h, n_steps, C.byref(us)), "time_steps")
+        return us.value
+
+    def results(self, r):
+        n = self.n_events[r]
+        out = (Result * max(1, n))()
+        check(lib().ksim_engine_get_results(self.h, r, out, n), "get_results")
+        return [(out[i].node, out[i].gpu_mask, out[i].score, out[i].n_feasible, out[i].status) for i in range(n)]
+
+    def nodes(self, r):
+        out = (Node * self.N)()
+        check(lib().ksim_engine_get_nodes(self.h, r, out), "get_nodes")
+        return out
+
+
+def make_pod(cpu, milli=0, num=0, mem=0, type_mask=KSIM_TYPE_ANY, cpu_nz=None):
+    p = Pod()
+    p.cpu_milli, p.cpu_nz_milli, p.mem_mib = cpu, cpu if cpu_nz is None else cpu_nz, mem
+    p.gpu_milli, p.gpu_count, p.type_mask, p.ref = milli, num, type_mask, -1
+    return p

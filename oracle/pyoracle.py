@@ -1,0 +1,227 @@
+"""ctypes binding for oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product path (kubernetes-scheduler-simulator_amd/) never does.
+"""
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+MILLI = 1000
+Q1, Q2, Q3, Q4, XL, XR, NA = range(7)
+POL_FGD, POL_BESTFIT, POL_DOTPROD, POL_PACKING, POL_CLUSTERING, POL_RANDOM = range(6)
+SEL_BEST, SEL_WORST, SEL_RANDOM, SEL_FGD = range(4)
+TYPE_LEN = 64
+MAX_GPU_LIST = 16
+
+
+class PodResource(C.Structure):
+    _fields_ = [("milli_cpu", C.c_int64), ("milli_gpu", C.c_int64), ("gpu_number", C.c_int32),
+                ("gpu_type", C.c_char * TYPE_LEN)]
+
+
+class NodeResource(C.Structure):
+    _fields_ = [("milli_cpu_left", C.c_int64), ("milli_cpu_capacity", C.c_int64),
+                ("milli_gpu_left", C.c_int64 * MAX_GPU_LIST), ("n_gpu_left", C.c_int32),
+                ("gpu_number", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+
+
+class TargetPod(C.Structure):
+    _fields_ = [("res", PodResource), ("percentage", C.c_double)]
+
+
+class WorkloadPod(C.Structure):
+    _fields_ = [("cpu_milli", C.c_int64), ("has_cpu", C.c_int32), ("gpu_milli", C.c_int64),
+                ("gpu_number", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+
+
+class TypicalCfg(C.Structure):
+    _fields_ = [("is_involved_cpu_pods", C.c_int32), ("pod_popularity_threshold", C.c_int32),
+                ("pod_increase_step", C.c_int32), ("gpu_res_weight", C.c_double)]
+
+
+class NodeSpec(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("cpu_alloc", C.c_int64), ("mem_alloc", C.c_int64),
+                ("pods_alloc", C.c_int32), ("gpu_count", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+
+
+class Event(C.Structure):
+    _fields_ = [("cpu_req", C.c_int64), ("cpu_nz", C.c_int64), ("mem_req", C.c_int64),
+                ("gpu_milli", C.c_int64), ("gpu_number", C.c_int32), ("is_delete", C.c_int32),
+                ("ref", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+
+
+class Result(C.Structure):
+    _fields_ = [("node", C.c_int32), ("gpu_mask", C.c_int32), ("score", C.c_int64),
+                ("n_feasible", C.c_int32), ("status", C.c_int32)]
+
+
+class Report(C.Structure):
+    _fields_ = [("frag_bins", C.c_double * 7), ("used_nodes", C.c_int64), ("used_gpus", C.c_int64),
+                ("used_gpu_milli", C.c_int64), ("total_gpus", C.c_int64), ("arrived_gpu_milli", C.c_int64),
+                ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64)]
+
+
+class Policy(C.Structure):
+    _fields_ = [("policy", C.c_int32), ("gpu_sel", C.c_int32), ("seed", C.c_uint64), ("threads", C.c_int32)]
+
+
+class NodeState(C.Structure):
+    _fields_ = [("cpu_left", C.c_int64), ("mem_left", C.c_int64), ("pods", C.c_int32),
+                ("gpu_left", C.c_int32 * 8)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        P = C.POINTER
+        L.orc_get_node_pod_frag.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_get_gpu_milli_left_total.argtypes = [P(NodeResource)]
+        L.orc_get_gpu_milli_left_total.restype = C.c_int64
+        L.orc_get_gpu_frag_milli.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_get_gpu_frag_milli.restype = C.c_int64
+        L.orc_node_gpu_share_frag_amount.argtypes = [P(NodeResource), P(TargetPod), C.c_int, P(C.c_double)]
+        L.orc_frag_amount_sum_except_q3.argtypes = [P(C.c_double)]
+        L.orc_frag_amount_sum_except_q3.restype = C.c_double
+        L.orc_node_gpu_share_frag_amount_score.argtypes = [P(NodeResource), P(TargetPod), C.c_int]
+        L.orc_node_gpu_share_frag_amount_score.restype = C.c_double
+        L.orc_go_exp.argtypes = [C.c_double]
+        L.orc_go_exp.restype = C.c_double
+        L.orc_sigmoid.argtypes = [C.c_double]
+        L.orc_sigmoid.restype = C.c_double
+        L.orc_node_sub.argtypes = [P(NodeResource), P(PodResource), P(NodeResource)]
+        L.orc_node_add.argtypes = [P(NodeResource), P(PodResource), P(C.c_int), C.c_int, P(NodeResource)]
+        L.orc_allocate_exclusive_gpu_id.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_flatten_milli_gpu.argtypes = [P(NodeResource), C.c_char_p, C.c_int]
+        L.orc_fgd_score.argtypes = [P(NodeResource), P(PodResource), P(TargetPod), C.c_int, P(C.c_int)]
+        L.orc_fgd_score.restype = C.c_int64
+        L.orc_best_fit_score.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_best_fit_score.restype = C.c_int64
+        L.orc_dot_product_score.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_dot_product_score.restype = C.c_int64
+        L.orc_packing_score.argtypes = [P(NodeResource), P(PodResource), P(C.c_int)]
+        L.orc_packing_score.restype = C.c_int64
+        L.orc_clustering_score.argtypes = [P(NodeResource), P(PodResource), C.c_int, P(C.c_int32)]
+        L.orc_clustering_score.restype = C.c_int64
+        L.orc_normalize_score.argtypes = [P(C.c_int64), C.c_int]
+        L.orc_alloc_gpu_best_fit.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_get_typical_pods.argtypes = [P(WorkloadPod), C.c_int, TypicalCfg, P(TargetPod), C.c_int]
+        L.orc_run_events_state.argtypes = [P(NodeSpec), C.c_int, P(TargetPod), C.c_int, Policy, P(Event),
+                                           C.c_int, P(Result), P(Report), P(NodeState)]
+        L.orc_mix64.argtypes = [C.c_uint64]
+        L.orc_mix64.restype = C.c_uint64
+        _LIB = L
+    return _LIB
+
+
+def _b(s):
+    return s.encode() if isinstance(s, str) else s
+
+
+def node_res(cpu_left, gpu_left, gpu_number=None, gpu_type="", cpu_cap=0):
+    n = NodeResource()
+    n.milli_cpu_left = cpu_left
+    n.milli_cpu_capacity = cpu_cap
+    for i, v in enumerate(gpu_left):
+        n.milli_gpu_left[i] = v
+    n.n_gpu_left = len(gpu_left)
+    n.gpu_number = len(gpu_left) if gpu_number is None else gpu_number
+    n.gpu_type = _b(gpu_type)
+    return n
+
+
+def pod_res(cpu, milli, num, gpu_type=""):
+    p = PodResource()
+    p.milli_cpu, p.milli_gpu, p.gpu_number, p.gpu_type = cpu, milli, num, _b(gpu_type)
+    return p
+
+
+def typical(list_of_tuples):
+    """[(cpu, milli, num, type, freq), ...] -> ctypes array"""
+    arr = (TargetPod * max(1, len(list_of_tuples)))()
+    for i, (cpu, milli, num, typ, freq) in enumerate(list_of_tuples):
+        arr[i].res = pod_res(cpu, milli, num, typ)
+        arr[i].percentage = freq
+    return arr, len(list_of_tuples)
+
+
+def frag_bins(node, tp):
+    arr, nt = tp
+    out = (C.c_double * 7)()
+    lib().orc_node_gpu_share_frag_amount(C.byref(node), arr, nt, out)
+    return list(out)
+
+
+def frag_score(node, tp):
+    arr, nt = tp
+    return lib().orc_node_gpu_share_frag_amount_score(C.byref(node), arr, nt)
+
+
+def fgd_score(node, pod, tp):
+    arr, nt = tp
+    m = C.c_int(0)
+    s = lib().orc_fgd_score(C.byref(node), C.byref(pod), arr, nt, C.byref(m))
+    return s, m.value
+
+
+def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_weight=0.0):
+    """workload: list of (cpu_milli, gpu_milli, gpu_number, gpu_type)"""
+    n = len(workload)
+    arr = (WorkloadPod * max(1, n))()
+    for i, (cpu, milli, num, typ) in enumerate(workload):
+        arr[i].cpu_milli, arr[i].has_cpu, arr[i].gpu_milli, arr[i].gpu_number = cpu, 1, milli, num
+        arr[i].gpu_type = _b(typ)
+    out = (TargetPod * max(1, n))()
+    cfg = TypicalCfg(1 if involve_cpu else 0, threshold, step, gpu_res_weight)
+    k = lib().orc_get_typical_pods(arr, n, cfg, out, n)
+    assert k >= 0
+    return [(out[i].res.milli_cpu, out[i].res.milli_gpu, out[i].res.gpu_number,
+             out[i].res.gpu_type.decode(), out[i].percentage) for i in range(k)]
+
+
+def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
+               with_report=False):
+    """nodes: list of dicts {name,cpu,mem,pods,gpu,model}; events: list of dicts
+    {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]"""
+    nn = len(nodes)
+    ns = (NodeSpec * nn)()
+    for i, d in enumerate(nodes):
+        ns[i].name = _b(d["name"])
+        ns[i].cpu_alloc, ns[i].mem_alloc = d["cpu"], d["mem"]
+        ns[i].pods_alloc, ns[i].gpu_count = d.get("pods", 1001), d["gpu"]
+        ns[i].gpu_type = _b(d.get("model", ""))
+    tp, nt = typical(typical_list)
+    ne = len(events)
+    ev = (Event * max(1, ne))()
+    for i, e in enumerate(events):
+        ev[i].cpu_req, ev[i].cpu_nz, ev[i].mem_req = e["cpu"], e.get("cpu_nz", e["cpu"]), e["mem"]
+        ev[i].gpu_milli, ev[i].gpu_number = e["milli"], e["num"]
+        ev[i].is_delete, ev[i].ref = e.get("delete", 0), e.get("ref", -1)
+        ev[i].gpu_type = _b(e.get("type", ""))
+    res = (Result * max(1, ne))()
+    rep = (Report * max(1, ne))() if with_report else None
+    st = (NodeState * nn)()
+    pol = Policy(policy, gpu_sel, seed, threads)
+    rc = lib().orc_run_events_state(ns, nn, tp, nt, pol, ev, ne, res, rep, st)
+    assert rc == 0
+    results = [(res[i].node, res[i].gpu_mask, res[i].score, res[i].n_feasible, res[i].status) for i in range(ne)]
+    state = [(st[i].cpu_left, st[i].mem_left, st[i].pods, list(st[i].gpu_left)) for i in range(nn)]
+    reports = None
+    if with_report:
+        reports = [dict(frag_bins=list(rep[i].frag_bins), used_nodes=rep[i].used_nodes,
+                        used_gpus=rep[i].used_gpus, used_gpu_milli=rep[i].used_gpu_milli,
+                        total_gpus=rep[i].total_gpus, arrived_gpu_milli=rep[i].arrived_gpu_milli,
+                        used_cpu_milli=rep[i].used_cpu_milli, arrived_cpu_milli=rep[i].arrived_cpu_milli)
+                   for i in range(ne)]
+    return results, state, reports

@@ -1,0 +1,50 @@
+"""Shared test helpers: build matching engine and oracle inputs from one trace.
+
+The engine gets the product's encodings (type bitmasks, name ranks, typical
+table from the C++ host driver); the oracle gets strings (GPU model names,
+"%04d-<name>" node names) and computes its own typical table, so the encodings
+are checked rather than shared.
+"""
+import ksim
+import pyoracle as O
+
+
+def oracle_typical(trace, threshold=95, step=1):
+    wl = [(p["cpu"], p["milli"], p["num"], p["spec"] if p["num"] > 0 else "") for p in trace.pods()]
+    return O.get_typical_pods(wl, threshold=threshold, step=step)
+
+
+def product_typical_list(trace, threshold=95, step=1):
+    arr, n = trace.typical(threshold=threshold, step=step)
+    return arr, n
+
+
+def oracle_nodes(trace, replay):
+    tn = trace.nodes()
+    names = replay.node_names(tn)
+    types = trace.type_names()
+    return [dict(name=names[i], cpu=tn[i]["cpu"], mem=tn[i]["mem"], pods=1001, gpu=tn[i]["gpu"],
+                 model=types[tn[i]["type"]] if tn[i]["gpu"] > 0 else "") for i in range(len(tn))]
+
+
+def oracle_events(trace, replay, limit=None):
+    pods = trace.pods()
+    n = replay.n if limit is None else min(limit, replay.n)
+    out = []
+    for k in range(n):
+        p = pods[replay.pod_index[k]]
+        out.append(dict(cpu=p["cpu"], cpu_nz=p["cpu"], mem=p["mem"], milli=p["milli"], num=p["num"],
+                        type=p["spec"] if p["num"] > 0 else ""))
+    return out
+
+
+def subset_nodes(replay, keep):
+    """Engine nodes for a subset of node indices, re-ranked by their relative order."""
+    import ctypes as C
+    sub = (ksim.Node * len(keep))()
+    ranks = sorted(range(len(keep)), key=lambda j: replay.nodes[keep[j]].name_rank)
+    rank_of = {j: r for r, j in enumerate(ranks)}
+    for j, i in enumerate(keep):
+        C.memmove(C.byref(sub[j]), C.byref(replay.nodes[i]), C.sizeof(ksim.Node))
+        sub[j].name_rank = rank_of[j]
+    return sub

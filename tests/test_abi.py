@@ -1,0 +1,75 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (no GPU needed)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import ksim
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("ksim_engine.h", "ksim_trace.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(ksim_[a-z_0-9]+)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 25
+    L = ksim.lib()
+    for n in sorted(names):
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", ksim.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (ksim_[a-z_0-9]+)", out))
+    assert names <= exported
+    # the Python binding covers exactly the declared surface
+    assert set(ksim.SIGNATURES) == names
+
+
+def test_struct_layouts_match_c():
+    src = os.path.join(ROOT, "tests", "golden", "abi_sizes.c")
+    exe = "/tmp/ksim_abi_sizes"
+    subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe], check=True)
+    got = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
+    want = [C.sizeof(t) for t in (ksim.Node, ksim.Pod, ksim.Typical, ksim.Result, ksim.Config, ksim.TraceNode,
+                                  ksim.TracePod, ksim.TypicalCfg, ksim.ReplayCfg)]
+    assert got == want
+
+
+def test_abi_version_and_errors():
+    L = ksim.lib()
+    assert L.ksim_abi_version() == 1
+    for code in range(0, -9, -1):
+        assert L.ksim_strerror(code)
+    # null / bad arguments are rejected before any device work
+    assert L.ksim_engine_create(None, 0, 1, None) == ksim.KSIM_EINVAL
+
+
+def test_no_cpu_fallback_without_device():
+    if ksim.device_count() > 0:
+        pytest.skip("a gfx950 device is present")
+    with pytest.raises(ksim.KsimError) as ei:
+        ksim.Engine(16, 1)
+    assert ei.value.code == ksim.KSIM_ENODEV
+
+
+def test_product_does_not_reference_oracle():
+    # the product library must not link or name anything under oracle/
+    out = subprocess.run(["nm", "-D", ksim.LIB_PATH], capture_output=True, text=True).stdout
+    assert "orc_" not in out
+    deps = subprocess.run(["ldd", ksim.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in deps
+    for root, _, files in os.walk(ksim.PKG_DIR):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")):
+                txt = open(os.path.join(root, f)).read()
+                assert "pyoracle" not in txt and "liboracle" not in txt, f
