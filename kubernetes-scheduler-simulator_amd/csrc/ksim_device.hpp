@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define KSIM_HD __host__ __device__ __forceinline__
+
 namespace ksim {
 
 constexpr int kMaxGpu = 8;
@@ -39,14 +41,14 @@ struct NodeV {
   uint32_t g[4];     // two u16 milli-left values per dword
   uint32_t meta;     // pods_left (i16) | gpu_cnt << 16 | gpu_type << 24
   uint32_t name_rank;
-  __device__ __forceinline__ int gl(int i) const {
+  KSIM_HD int gl(int i) const {
     const uint32_t w = i < 2 ? g[0] : (i < 4 ? g[1] : (i < 6 ? g[2] : g[3]));
     return (int)((i & 1) ? (w >> 16) : (w & 0xffffu));
   }
-  __device__ __forceinline__ int pods_left() const { return (int)(int16_t)(meta & 0xffffu); }
-  __device__ __forceinline__ int gpu_cnt() const { return (int)((meta >> 16) & 0xffu); }
-  __device__ __forceinline__ int gpu_type() const { return (int)(meta >> 24); }
-  __device__ __forceinline__ int total() const {
+  KSIM_HD int pods_left() const { return (int)(int16_t)(meta & 0xffffu); }
+  KSIM_HD int gpu_cnt() const { return (int)((meta >> 16) & 0xffu); }
+  KSIM_HD int gpu_type() const { return (int)(meta >> 24); }
+  KSIM_HD int total() const {
     int t = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) t += gl(i);
@@ -54,7 +56,7 @@ struct NodeV {
   }
 };
 
-__device__ __forceinline__ NodeV load_node(const NodeRec* p) {
+KSIM_HD NodeV load_node(const NodeRec* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   const uint4 a = q[0], b = q[1];
   NodeV n;
@@ -65,7 +67,7 @@ __device__ __forceinline__ NodeV load_node(const NodeRec* p) {
   n.name_rank = b.w;
   return n;
 }
-__device__ __forceinline__ void store_node(NodeRec* p, const NodeV& n) {
+KSIM_HD void store_node(NodeRec* p, const NodeV& n) {
   uint4* q = reinterpret_cast<uint4*>(p);
   q[0] = make_uint4((uint32_t)n.cpu_left, (uint32_t)n.mem_left, n.g[0], n.g[1]);
   q[1] = make_uint4(n.g[2], n.g[3], n.meta, n.name_rank);
@@ -138,7 +140,7 @@ enum : int { ST_OK = 0, ST_UNSCHED = 1, ST_ERROR = 2, ST_DELETED = 3 };
 // Go math.Exp, portable algorithm (Go src/math/exp.go).  Identical operation
 // sequence to oracle/fgd_oracle.c orc_go_exp.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double go_exp(double x) {
+KSIM_HD double go_exp(double x) {
   const double Ln2Hi = 6.93147180369123816490e-01;
   const double Ln2Lo = 1.90821492927058770002e-10;
   const double Log2e = 1.44269504088896338700e+00;
@@ -151,7 +153,7 @@ __device__ __forceinline__ double go_exp(double x) {
   const double P4 = -1.65339022054652515390e-06;
   const double P5 = 4.13813679705723846039e-08;
   if (x != x) return x;
-  if (x > Overflow) return __longlong_as_double(0x7ff0000000000000LL);
+  if (x > Overflow) return __builtin_bit_cast(double, 0x7ff0000000000000LL);
   if (x < Underflow) return 0.0;
   if (-NearZero < x && x < NearZero) return 1 + x;
   int k = 0;
@@ -164,16 +166,16 @@ __device__ __forceinline__ double go_exp(double x) {
   double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
   double y = 1 - ((lo - (r * c) / (2 - c)) - hi);
   int k1 = k / 2, k2 = k - k1;
-  double a = __longlong_as_double((long long)(1023 + k1) << 52);
-  double b = __longlong_as_double((long long)(1023 + k2) << 52);
+  double a = __builtin_bit_cast(double, (long long)(1023 + k1) << 52);
+  double b = __builtin_bit_cast(double, (long long)(1023 + k2) << 52);
   return (y * a) * b;
 }
 
 // plugin_utils.go:76-78
-__device__ __forceinline__ double go_sigmoid(double x) { return 1.0 / (1.0 + go_exp(-x)); }
+KSIM_HD double go_sigmoid(double x) { return 1.0 / (1.0 + go_exp(-x)); }
 
 // fgd_score.go:123 fragScore = int64(sigmoid((cur-new)/1000) * MaxNodeScore)
-__device__ __forceinline__ int fgd_frag_score(double cur, double nw) {
+KSIM_HD int fgd_frag_score(double cur, double nw) {
   return (int)(go_sigmoid((cur - nw) / 1000) * (double)100);
 }
 
@@ -186,7 +188,7 @@ __device__ __forceinline__ int fgd_frag_score(double cur, double nw) {
 // Bin Q3 (index 2) is not part of F and is not accumulated here.
 // tpi[t] = {MilliCpu, MilliGpu, max(GpuNumber,1), type mask}, tpf[t] = freq.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, int T,
+KSIM_HD double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, int T,
                                          const int4* __restrict__ tpi, const double* __restrict__ tpf) {
   int total = 0;
 #pragma unroll
@@ -230,14 +232,14 @@ __device__ __forceinline__ double frag_F(int cpuL, const int (&gl)[kMaxGpu], uin
   return out;
 }
 
-__device__ __forceinline__ void unpack_gl(const NodeV& n, int (&gl)[kMaxGpu]) {
+KSIM_HD void unpack_gl(const NodeV& n, int (&gl)[kMaxGpu]) {
 #pragma unroll
   for (int g = 0; g < kMaxGpu; ++g) gl[g] = n.gl(g);
 }
 
 // Filter: fitsRequest (fit.go:230-290) ∧ GpuSharePlugin.Filter (open_gpu_share.go:81-118)
 //         ∧ GpuNodeInfo.AllocateGpuId (gpunodeinfo.go:136-204).
-__device__ __forceinline__ bool filter_node(const NodeV& n, const PodDev& p) {
+KSIM_HD bool filter_node(const NodeV& n, const PodDev& p) {
   if (n.pods_left() < 1) return false;
   if (!(p.cpu_req == 0 && p.mem == 0)) {
     if (n.cpu_left < p.cpu_req) return false;
@@ -262,12 +264,12 @@ __device__ __forceinline__ bool filter_node(const NodeV& n, const PodDev& p) {
   return slots >= p.num;
 }
 
-__device__ __forceinline__ bool is_share_pod(const PodDev& p) { return p.num == 1 && p.milli < kMilli; }
+KSIM_HD bool is_share_pod(const PodDev& p) { return p.num == 1 && p.milli < kMilli; }
 
 // GPUs selected by NodeResource.Sub (resource.go:454-480): ascending stable
 // order of milli left, first `num` devices with left >= milli.  Returns mask;
 // *ok=false when Sub would return its early error (state left unchanged).
-__device__ __forceinline__ unsigned sub_gpu_mask(const int (&gl)[kMaxGpu], int gpu_cnt, int cpuL, const PodDev& p,
+KSIM_HD unsigned sub_gpu_mask(const int (&gl)[kMaxGpu], int gpu_cnt, int cpuL, const PodDev& p,
                                                  bool* ok) {
   *ok = !(cpuL < p.cpu_nz || gpu_cnt < p.num);
   if (!*ok || p.num <= 0) return 0u;
@@ -287,7 +289,7 @@ __device__ __forceinline__ unsigned sub_gpu_mask(const int (&gl)[kMaxGpu], int g
 
 // AllocateExclusiveGpuId (resource.go:383-403): lowest-index fully free GPUs.
 // Returns -1 where the reference panics.
-__device__ __forceinline__ int exclusive_gpu_mask(const NodeV& n, const PodDev& p) {
+KSIM_HD int exclusive_gpu_mask(const NodeV& n, const PodDev& p) {
   int req = (int)p.milli * (int)p.num;
   int mask = 0;
   const int cnt = n.gpu_cnt();
@@ -302,7 +304,7 @@ __device__ __forceinline__ int exclusive_gpu_mask(const NodeV& n, const PodDev& 
 }
 
 // getBestFitScore (best_fit_score.go:66-97); -1 = error
-__device__ __forceinline__ int bestfit_score(const NodeV& n, const PodDev& p, int total) {
+KSIM_HD int bestfit_score(const NodeV& n, const PodDev& p, int total) {
   const double f0 = (double)n.cpu_left, r0 = (double)p.cpu_nz;
   const double f1 = (double)total, r1 = (double)((int)p.milli * (int)p.num);
   double s = 0;
@@ -316,7 +318,7 @@ __device__ __forceinline__ int bestfit_score(const NodeV& n, const PodDev& p, in
 
 // calculateDotProductScore with merge/max (dot_product_score.go:64-100,
 // utils.go:1274-1342, resource.go:296-328, utils.go:1220-1248)
-__device__ __forceinline__ int dotprod_score(const NodeV& n, const PodDev& p, int total) {
+KSIM_HD int dotprod_score(const NodeV& n, const PodDev& p, int total) {
   if (n.cpu_left < p.cpu_nz) return 0;
   const double a0 = (double)n.cpu_left / (double)kMaxSpecCpu;
   const double a1 = (double)total / (double)kMaxSpecGpu;
@@ -333,7 +335,7 @@ __device__ __forceinline__ int dotprod_score(const NodeV& n, const PodDev& p, in
 }
 
 // getPackingScore (gpu_packing_score.go:71-117); *err on allocation failure
-__device__ __forceinline__ int packing_score(const NodeV& n, const PodDev& p, bool* err) {
+KSIM_HD int packing_score(const NodeV& n, const PodDev& p, bool* err) {
   *err = false;
   const int cnt = n.gpu_cnt();
   int ff = 0;
@@ -372,7 +374,7 @@ __device__ __forceinline__ int packing_score(const NodeV& n, const PodDev& p, bo
 }
 
 // GpuClusteringScorePlugin.Score (gpu_clustering_score.go:32-56)
-__device__ __forceinline__ int clustering_score(const uint16_t* tags, int pod_tag, int total) {
+KSIM_HD int clustering_score(const uint16_t* tags, int pod_tag, int total) {
   if (pod_tag < 0) return 0;
   int distinct = 0;
 #pragma unroll
@@ -383,7 +385,7 @@ __device__ __forceinline__ int clustering_score(const uint16_t* tags, int pod_ta
 }
 
 // Random contract: splitmix64 finaliser.
-__device__ __host__ __forceinline__ uint64_t mix64(uint64_t x) {
+KSIM_HD uint64_t mix64(uint64_t x) {
   x ^= x >> 30;
   x *= 0xbf58476d1ce4e5b9ULL;
   x ^= x >> 27;
@@ -391,13 +393,13 @@ __device__ __host__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 31;
   return x;
 }
-__device__ __forceinline__ uint64_t rand_node_key(uint64_t seed, int step, uint32_t rank) {
+KSIM_HD uint64_t rand_node_key(uint64_t seed, int step, uint32_t rank) {
   return mix64(mix64(seed ^ 0xA0761D6478BD642FULL) ^ (((uint64_t)(uint32_t)step << 32) | rank));
 }
-__device__ __forceinline__ uint64_t rand_gpu_key(uint64_t node_key, int g) { return mix64(node_key ^ (uint64_t)(0x100 + g)); }
+KSIM_HD uint64_t rand_gpu_key(uint64_t node_key, int g) { return mix64(node_key ^ (uint64_t)(0x100 + g)); }
 
 // Packed argmax key: [63:40] score (24 b) | [39:8] ~name_rank | [7:0] gpu index + 1.
-__device__ __forceinline__ unsigned long long pack_key(unsigned score, uint32_t rank, int gpu) {
+KSIM_HD unsigned long long pack_key(unsigned score, uint32_t rank, int gpu) {
   return ((unsigned long long)(score & 0xFFFFFFu) << 40) | ((unsigned long long)(0xFFFFFFFFu - rank) << 8) |
          (unsigned long long)((gpu + 1) & 0xFF);
 }

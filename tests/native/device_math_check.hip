@@ -1,0 +1,109 @@
+// Host-side harness for the engine's __host__ __device__ math (ksim_device.hpp):
+// the exact functions the gfx950 kernels inline, run on the CPU so the CPU test
+// suite can compare them with the oracle without a GPU.  Test infrastructure only.
+#include <cstring>
+
+#include "ksim_device.hpp"
+
+using namespace ksim;
+
+extern "C" {
+
+double dm_go_exp(double x) { return go_exp(x); }
+
+// F(state) for a node state given as (cpu_left, gl[8], type id) and a typical table
+double dm_frag_F(int cpu_left, const int* gl8, int type_id, int T, const int* tpi4, const double* tpf) {
+  int gl[kMaxGpu];
+  for (int g = 0; g < kMaxGpu; ++g) gl[g] = gl8[g];
+  return frag_F(cpu_left, gl, 1u << type_id, T, reinterpret_cast<const int4*>(tpi4), tpf);
+}
+
+static NodeV mk(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left) {
+  NodeV n;
+  std::memset(&n, 0, sizeof n);
+  n.cpu_left = cpu_left;
+  n.mem_left = mem_left;
+  for (int g = 0; g < 4; ++g) n.g[g] = (uint32_t)gl8[2 * g] | ((uint32_t)gl8[2 * g + 1] << 16);
+  n.meta = ((uint32_t)pods_left & 0xffffu) | ((uint32_t)gpu_cnt << 16) | ((uint32_t)type_id << 24);
+  return n;
+}
+
+static PodDev pod(int cpu, int milli, int num, unsigned mask) {
+  PodDev p;
+  std::memset(&p, 0, sizeof p);
+  p.cpu_req = p.cpu_nz = cpu;
+  p.milli = (int16_t)milli;
+  p.num = (int8_t)num;
+  p.tmask = mask;
+  p.tag = num == 0 ? -1 : (num == 1 && milli < kMilli ? 0 : (milli == kMilli ? num : -2));
+  return p;
+}
+
+// FGD score of one node for one pod, as k_step computes it (current state + candidates)
+int dm_fgd_score(int cpu_left, const int* gl8, int gpu_cnt, int type_id, int cpu, int milli, int num, int T,
+                 const int* tpi4, const double* tpf, int* gpu_out) {
+  const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, type_id, 100);
+  const PodDev p = pod(cpu, milli, num, 0xffffffffu);
+  const int4* tpi = reinterpret_cast<const int4*>(tpi4);
+  int gl[kMaxGpu];
+  unpack_gl(n, gl);
+  const double F0 = frag_F(n.cpu_left, gl, 1u << type_id, T, tpi, tpf);
+  *gpu_out = -1;
+  if (is_share_pod(p)) {
+    int best = -1, bs = 0;
+    for (int g = 0; g < kMaxGpu; ++g) {
+      if (g < gpu_cnt && gl[g] >= milli) {
+        int c[kMaxGpu];
+        for (int k = 0; k < kMaxGpu; ++k) c[k] = gl[k] - (k == g ? milli : 0);
+        const int fs = fgd_frag_score(F0, frag_F(n.cpu_left - cpu, c, 1u << type_id, T, tpi, tpf));
+        if (best < 0 || fs > bs) { bs = fs; best = g; }
+      }
+    }
+    *gpu_out = best;
+    return bs;
+  }
+  bool ok = false;
+  const unsigned sm = sub_gpu_mask(gl, gpu_cnt, n.cpu_left, p, &ok);
+  int c[kMaxGpu];
+  int cl = n.cpu_left;
+  for (int k = 0; k < kMaxGpu; ++k) c[k] = gl[k];
+  if (ok) {
+    cl -= cpu;
+    for (int k = 0; k < kMaxGpu; ++k) c[k] -= ((sm >> k) & 1u) ? milli : 0;
+  }
+  return fgd_frag_score(F0, frag_F(cl, c, 1u << type_id, T, tpi, tpf));
+}
+
+int dm_filter(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left, int cpu, int mem,
+              int milli, int num, unsigned mask) {
+  PodDev p = pod(cpu, milli, num, mask);
+  p.mem = mem;
+  return filter_node(mk(cpu_left, mem_left, gl8, gpu_cnt, type_id, pods_left), p) ? 1 : 0;
+}
+
+int dm_bestfit(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num) {
+  const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, 0, 1);
+  return bestfit_score(n, pod(cpu, milli, num, ~0u), n.total());
+}
+int dm_dotprod(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num) {
+  const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, 0, 1);
+  return dotprod_score(n, pod(cpu, milli, num, ~0u), n.total());
+}
+int dm_packing(const int* gl8, int gpu_cnt, int cpu, int milli, int num, int* err) {
+  bool e = false;
+  const int s = packing_score(mk(64000, 0, gl8, gpu_cnt, 0, 1), pod(cpu, milli, num, ~0u), &e);
+  *err = e ? 1 : 0;
+  return s;
+}
+int dm_clustering(const int* tags9, const int* gl8, int gpu_cnt, int milli, int num) {
+  uint16_t t[16] = {0};
+  for (int k = 0; k < 9; ++k) t[k] = (uint16_t)tags9[k];
+  const NodeV n = mk(64000, 0, gl8, gpu_cnt, 0, 1);
+  const PodDev p = pod(1000, milli, num, ~0u);
+  return clustering_score(t, p.tag, n.total());
+}
+int dm_exclusive(const int* gl8, int gpu_cnt, int milli, int num) {
+  return exclusive_gpu_mask(mk(0, 0, gl8, gpu_cnt, 0, 1), pod(0, milli, num, ~0u));
+}
+
+}  // extern "C"

@@ -1,0 +1,136 @@
+"""The engine's __host__ __device__ math (ksim_device.hpp), compiled for the host, against the oracle.
+
+Fuzzed node states x pods x typical tables: F, FGD score + GPU choice, Filter, BestFit, DotProduct,
+GpuPacking, GpuClustering and AllocateExclusiveGpuId must agree bit for bit.  This is the same source
+the gfx950 kernels inline; tests/test_gpu_parity.py covers the device execution itself.
+"""
+import ctypes as C
+import os
+import random
+import subprocess
+
+import pytest
+
+import helpers
+import ksim
+import pyoracle as O
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+
+
+@pytest.fixture(scope="module")
+def dm():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    L = C.CDLL(os.path.join(HERE, "libdevmath.so"))
+    I8 = C.c_int * 8
+    L.dm_go_exp.argtypes = [C.c_double]
+    L.dm_go_exp.restype = C.c_double
+    L.dm_frag_F.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
+    L.dm_frag_F.restype = C.c_double
+    L.dm_fgd_score.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                               C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    L.dm_filter.argtypes = [C.c_int, C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                            C.c_uint]
+    L.dm_bestfit.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.dm_dotprod.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.dm_packing.argtypes = [I8, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+    L.dm_clustering.argtypes = [C.c_int * 9, I8, C.c_int, C.c_int, C.c_int]
+    L.dm_exclusive.argtypes = [I8, C.c_int, C.c_int, C.c_int]
+    return L
+
+
+TYPES = ["A10", "G2", "G3", "P100", "T4", "V100M16", "V100M32"]
+
+
+def rand_gl(rnd, cnt):
+    gl = [rnd.choice([0, 1000, 1000, 1000, rnd.randint(0, 1000), rnd.randint(0, 1000)]) for _ in range(cnt)]
+    return gl + [0] * (8 - cnt)
+
+
+def rand_pod(rnd):
+    k = rnd.random()
+    if k < 0.15:
+        return rnd.choice([1000, 4000, 12000, 32000]), 0, 0
+    if k < 0.55:
+        return rnd.choice([2000, 4000, 6000, 8000, 11908]), rnd.choice([100, 250, 300, 460, 500, 810, 999]), 1
+    return rnd.choice([4000, 8000, 16000, 64000]), 1000, rnd.choice([1, 1, 1, 2, 4, 8])
+
+
+def table(tlist):
+    tpi = (C.c_int * (4 * len(tlist)))()
+    tpf = (C.c_double * len(tlist))()
+    for i, (cpu, milli, num, spec, f) in enumerate(tlist):
+        mask = 0
+        for x in filter(None, spec.split("|")):
+            mask |= 1 << TYPES.index(x)
+        tpi[4 * i:4 * i + 4] = [cpu, milli, max(num, 1), C.c_int(mask or -1).value]
+        tpf[i] = f
+    return tpi, tpf
+
+
+@pytest.fixture(scope="module")
+def tables():
+    t = ksim.Trace.openb("gpuspec33")
+    d = ksim.Trace.openb("default")
+    return [helpers.oracle_typical(d), helpers.oracle_typical(t)]
+
+
+def test_go_exp_host_equals_oracle(dm):
+    rnd = random.Random(1)
+    for _ in range(20000):
+        x = rnd.uniform(-30, 30) if rnd.random() < 0.9 else rnd.uniform(-1e-6, 1e-6)
+        assert dm.dm_go_exp(x) == O.lib().orc_go_exp(x)
+
+
+def test_frag_F_and_fgd_score_fuzz(dm, tables):
+    rnd = random.Random(2)
+    for tlist in tables:
+        tpi, tpf = table(tlist)
+        otp = O.typical(tlist)
+        for _ in range(1500):
+            cnt = rnd.choice([1, 2, 4, 8])
+            gl = rand_gl(rnd, cnt)
+            cpu_left = rnd.choice([0, 500, 2000, 8000, 32000, 64000, 96000])
+            ty = rnd.randrange(len(TYPES))
+            node = O.node_res(cpu_left, gl[:cnt], cnt, TYPES[ty], 96000)
+            f = dm.dm_frag_F(cpu_left, (C.c_int * 8)(*gl), ty, len(tlist), tpi, tpf)
+            assert f == O.frag_score(node, otp)
+            cpu, milli, num = rand_pod(rnd)
+            pr = O.pod_res(cpu, milli, num, "")
+            # only states that pass Filter are scored by the reference
+            if not dm.dm_filter(cpu_left, 10 ** 6, (C.c_int * 8)(*gl), cnt, ty, 10, cpu, 0, milli, num, 0xFFFFFFFF):
+                continue
+            g = C.c_int(0)
+            s = dm.dm_fgd_score(cpu_left, (C.c_int * 8)(*gl), cnt, ty, cpu, milli, num, len(tlist), tpi, tpf,
+                                C.byref(g))
+            ws, wm = O.fgd_score(node, pr, otp)
+            assert s == ws
+            if num == 1 and milli < 1000:
+                assert wm == (1 << g.value)
+
+
+def test_cheap_scores_and_exclusive_fuzz(dm):
+    rnd = random.Random(3)
+    L = O.lib()
+    for _ in range(20000):
+        cnt = rnd.choice([1, 2, 4, 8])
+        gl = rand_gl(rnd, cnt)
+        cpu_left = rnd.choice([0, 100, 2000, 8000, 32000, 64000, 128000])
+        cpu, milli, num = rand_pod(rnd)
+        node = O.node_res(cpu_left, gl[:cnt], cnt, "G2", 128000)
+        pr = O.pod_res(cpu, milli, num, "")
+        g8 = (C.c_int * 8)(*gl)
+        assert dm.dm_bestfit(cpu_left, g8, cnt, cpu, milli, num) == L.orc_best_fit_score(C.byref(node), C.byref(pr))
+        assert dm.dm_dotprod(cpu_left, g8, cnt, cpu, milli, num) == L.orc_dot_product_score(C.byref(node),
+                                                                                              C.byref(pr))
+        if milli > 0:
+            e1, e2 = C.c_int(0), C.c_int(0)
+            a = dm.dm_packing(g8, cnt, cpu, milli, num, C.byref(e1))
+            b = L.orc_packing_score(C.byref(node), C.byref(pr), C.byref(e2))
+            assert e1.value == e2.value and (e1.value or a == b)
+            assert dm.dm_exclusive(g8, cnt, milli, num) == L.orc_allocate_exclusive_gpu_id(C.byref(node),
+                                                                                            C.byref(pr))
+        tags = [rnd.choice([0, 0, 0, 1, 2]) for _ in range(9)]
+        tag = -1 if num == 0 else (0 if (num == 1 and milli < 1000) else num)
+        want = L.orc_clustering_score(C.byref(node), C.byref(pr), tag, (C.c_int32 * 9)(*tags))
+        assert dm.dm_clustering((C.c_int * 9)(*tags), g8, cnt, milli, num) == want
