@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--nodes-per-block", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | ...")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,7 +75,7 @@ def main():
 
     trace = ksim.Trace.openb("default")
     seeds = [42 + args.replicas * rank + i for i in range(args.replicas)]
-    eng = _engine_on(local, trace, seeds, args.nodes_per_block)
+    eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy)
     total_events = eng.total_events
 
     for _ in range(args.warmup):
@@ -128,6 +129,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_step", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch},
     }
+    if args.policy != "FGD":
+        line["config"]["workload"] = line["config"]["workload"].replace("FGD", args.policy)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(trace, seeds[0], args.cpu_threads)
     if rank == 0:
@@ -137,7 +140,7 @@ def main():
         dist.destroy_process_group()
 
 
-def _engine_on(device, trace, seeds, nodes_per_block):
+def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD"):
     arr, n = trace.typical()
     eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block)
     total = 0
@@ -145,7 +148,7 @@ def _engine_on(device, trace, seeds, nodes_per_block):
         rp = trace.replay(seed=s, tune_ratio=1.3, shuffle=True)
         eng.set_nodes(r, rp.nodes)
         eng.set_typical(r, arr, n)
-        eng.set_policy(r, "FGD")
+        eng.set_policy(r, policy)
         eng.load_events(r, rp.events, rp.n)
         total += rp.n
     eng.total_events = total
