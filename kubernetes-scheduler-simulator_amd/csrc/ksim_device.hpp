@@ -89,15 +89,21 @@ struct __align__(16) PodDev {
 static_assert(sizeof(PodDev) == 32, "PodDev must stay 32 B");
 constexpr uint32_t kPodDelete = 1u;
 
-// Typical-pod table entry, host layout (staged into LDS as int4 + double).
-struct TypDev {
+// Typical-pod table entry: 32 B, read with scalar loads (uniform across the workgroup).
+// Per replica the table is split, order preserved within each part:
+//   [0, ncpu)   typical pods with MilliGpu == 0   (feed only bins XL, XR)
+//   [ncpu, nt)  typical pods with MilliGpu  > 0   (feed only bins Q1, Q2, Q4, NA)
+// Each bin is a sequential sum over its own subsequence, so the split keeps
+// every bin bit-identical to the reference's single pass (frag.go:153-186).
+struct __align__(32) TypDev {
   int32_t cpu;
   int32_t milli;
   int32_t num_eff;  // max(GpuNumber, 1): CanNodeHostPodOnGpuMemory (frag.go:447-458)
   uint32_t tmask;
   double freq;
+  int32_t pad[2];
 };
-static_assert(sizeof(TypDev) == 24, "TypDev must stay 24 B");
+static_assert(sizeof(TypDev) == 32, "TypDev must stay 32 B");
 
 struct ResultDev {  // == ksim_result
   int32_t node;
@@ -113,7 +119,9 @@ struct ReplicaDev {
   int32_t gpusel;
   uint64_t seed;
   int32_t n_events;
-  int32_t nt;
+  int32_t nt;    // typical entries: [0, ncpu) CPU-only, [ncpu, nt) GPU
+  int32_t ncpu;
+  int32_t typed; // some GPU entry names a model (NA bin reachable)
   const TypDev* tp;
   const PodDev* ev;
   ResultDev* res;
@@ -186,40 +194,50 @@ KSIM_HD int fgd_frag_score(double cur, double nw) {
 // Each bin is a sequential fp64 sum in typical-pod order; a bin a typical pod
 // does not touch receives +0.0, which leaves every non-negative sum bit-exact.
 // Bin Q3 (index 2) is not part of F and is not accumulated here.
-// tpi[t] = {MilliCpu, MilliGpu, max(GpuNumber,1), type mask}, tpf[t] = freq.
+// kTyped = some GPU typical pod names a GPU model (else the NA bin stays 0).
 // ---------------------------------------------------------------------------
-KSIM_HD double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, int T,
-                                         const int4* __restrict__ tpi, const double* __restrict__ tpf) {
+template <bool kTyped>
+KSIM_HD double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, const TypDev* __restrict__ tp,
+                      int ncpu, int nt) {
   int total = 0;
 #pragma unroll
   for (int g = 0; g < kMaxGpu; ++g) total += gl[g];  // GetGpuMilliLeftTotal (frag.go:224-229)
   const double dtot = (double)total;
-  double b0 = 0.0, b1 = 0.0, b3 = 0.0, b4 = 0.0, b5 = 0.0, b6 = 0.0;
-  for (int t = 0; t < T; ++t) {
-    const int4 q = tpi[t];
-    const double f = tpf[t];
-    const double x = f * dtot;          // freq * float64(gpuMilliLeftTotal)
-    const bool cpu_ok = cpuL >= q.x;
-    if (q.y == 0) {                     // CPU-only typical pod: XL / XR (frag.go:463-469)
-      b4 += cpu_ok ? x : 0.0;
-      b5 += cpu_ok ? 0.0 : x;
-    } else {
-      const bool acc = (q.w & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
-      int cnt = 0, frag = 0;
+  // CPU-only typical pods: XL / XR (frag.go:463-469)
+  double b4 = 0.0, b5 = 0.0;
+#pragma unroll 2
+  for (int t = 0; t < ncpu; ++t) {
+    const double x = tp[t].freq * dtot;  // freq * float64(gpuMilliLeftTotal)
+    const bool cpu_ok = cpuL >= tp[t].cpu;
+    b4 += cpu_ok ? x : 0.0;
+    b5 += cpu_ok ? 0.0 : x;
+  }
+  double b0 = 0.0, b1 = 0.0, b3 = 0.0, b6 = 0.0;
+#pragma unroll 2
+  for (int t = ncpu; t < nt; ++t) {
+    const int m = tp[t].milli;
+    const double f = tp[t].freq;
+    const double x = f * dtot;
+    const bool cpu_ok = cpuL >= tp[t].cpu;
+    int cnt = 0, frag = 0;
 #pragma unroll
-      for (int g = 0; g < kMaxGpu; ++g) {
-        const bool ge = gl[g] >= q.y;
-        cnt += ge ? 1 : 0;               // CanNodeHostPodOnGpuMemory (frag.go:447-458)
-        frag += ge ? 0 : gl[g];          // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
-      }
-      const bool gpu_ok = cnt >= q.z;
-      const double y = f * (double)frag;  // freq * float64(gpuFragMilli)
-      const bool q3 = acc && gpu_ok && cpu_ok;
-      const bool q2 = acc && !gpu_ok && cpu_ok;
-      b0 += (acc && !gpu_ok && !cpu_ok) ? x : 0.0;  // Q1
-      b1 += q3 ? y : (q2 ? x : 0.0);                 // Q2 (Q3 splits its frag part here)
-      b3 += (acc && gpu_ok && !cpu_ok) ? x : 0.0;   // Q4
-      b6 += acc ? 0.0 : x;                           // NA
+    for (int g = 0; g < kMaxGpu; ++g) {
+      const bool ge = gl[g] >= m;
+      cnt += ge ? 1 : 0;               // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+      frag += ge ? 0 : gl[g];          // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+    }
+    const bool gpu_ok = cnt >= tp[t].num_eff;
+    const double y = f * (double)frag;  // freq * float64(gpuFragMilli)
+    if (kTyped) {
+      const bool acc = (tp[t].tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+      b0 += (acc && !gpu_ok && !cpu_ok) ? x : 0.0;        // Q1
+      b1 += (acc && cpu_ok) ? (gpu_ok ? y : x) : 0.0;     // Q2 (Q3 adds its frag part here)
+      b3 += (acc && gpu_ok && !cpu_ok) ? x : 0.0;         // Q4
+      b6 += acc ? 0.0 : x;                                // NA
+    } else {
+      b0 += (!gpu_ok && !cpu_ok) ? x : 0.0;
+      b1 += cpu_ok ? (gpu_ok ? y : x) : 0.0;
+      b3 += (gpu_ok && !cpu_ok) ? x : 0.0;
     }
   }
   double out = 0.0;
@@ -274,6 +292,18 @@ KSIM_HD unsigned sub_gpu_mask(const int (&gl)[kMaxGpu], int gpu_cnt, int cpuL, c
   *ok = !(cpuL < p.cpu_nz || gpu_cnt < p.num);
   if (!*ok || p.num <= 0) return 0u;
   unsigned taken = 0u;
+  if (p.milli == kMilli) {
+    // whole GPUs: only fully free devices qualify; the stable ascending order keeps them in index order
+    int need = p.num;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      if (need > 0 && g < gpu_cnt && gl[g] == kMilli) {
+        taken |= 1u << g;
+        --need;
+      }
+    }
+    return taken;
+  }
   for (int k = 0; k < p.num; ++k) {
     int best = -1, bv = 0;
 #pragma unroll

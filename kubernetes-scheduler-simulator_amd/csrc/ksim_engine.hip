@@ -145,11 +145,27 @@ __device__ void apply_bind(NodeRec* nr, uint16_t* tags, const PodDev& p, int mas
   if (p.tag >= 0) tags[p.tag] = (uint16_t)((int)tags[p.tag] + sign);
 }
 
-__global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
+// Bit g set iff GPU g fits `milli` and no lower-index fitting GPU has the same milli left.
+__device__ __forceinline__ unsigned first_of_class(const NodeV& n, int milli) {
+  unsigned fm = 0u;
+  const int cnt = n.gpu_cnt();
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) {
+    const int v = n.gl(g);
+    bool first = g < cnt && v >= milli;
+#pragma unroll
+    for (int h = 0; h < g; ++h) first = first && !(n.gl(h) == v);
+    fm |= first ? (1u << g) : 0u;
+  }
+  return fm;
+}
+
+__global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __restrict__ tp_all) {
   const int r = a.rep_first + (int)blockIdx.x / a.bpr;
   const int b = (int)blockIdx.x % a.bpr;
   const int tid = (int)threadIdx.x;
   const ReplicaDev rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int step = (a.base ? *a.base : 0) + a.step_off;
   if (!a.pod_override && step >= rp.n_events) return;
   const PodDev p = a.pod_override ? *a.pod_override : rp.ev[step];
@@ -178,8 +194,6 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
   __shared__ uint8_t s_item_node[kNBMax * kMaxCand];
   __shared__ uint8_t s_item_code[kNBMax * kMaxCand];
   __shared__ double s_F[kNBMax * kMaxCand];
-  __shared__ int4 s_tpi[kMaxTypical];
-  __shared__ double s_tpf[kMaxTypical];
   __shared__ unsigned long long s_rkey[kBlock / 64];
   __shared__ int s_rcnt[kBlock / 64], s_rerr[kBlock / 64], s_rlo[kBlock / 64], s_rhi[kBlock / 64];
 
@@ -187,14 +201,6 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
   const int nb = max(0, min(a.NB, a.N - n0));
   const bool fgd = rp.policy == POL_FGD;
   const bool share = is_share_pod(p);
-
-  if (fgd) {
-    for (int t = tid; t < rp.nt; t += kBlock) {
-      const TypDev q = rp.tp[t];
-      s_tpi[t] = make_int4(q.cpu, q.milli, q.num_eff, (int)q.tmask);
-      s_tpf[t] = q.freq;
-    }
-  }
 
   // ---- phase 1: Filter (+ cheap scores) ----
   bool feas = false, err = false;
@@ -209,10 +215,10 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
       switch (rp.policy) {
         case POL_FGD: {
           if (share) {
-            int c = 1;
-#pragma unroll
-            for (int g = 0; g < kMaxGpu; ++g) c += (g < n.gpu_cnt() && n.gl(g) >= p.milli) ? 1 : 0;
-            nc = c;
+            // one candidate per DISTINCT milli-left value among the fitting GPUs: placing the
+            // pod on any GPU of a value class yields the same multiset of GPU states, hence the
+            // same F (frag.go depends on the multiset only) and the same score.
+            nc = 1 + __builtin_popcount(first_of_class(n, p.milli));
           } else {
             nc = 2;
           }
@@ -262,9 +268,10 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
       s_item_code[o] = 0;  // current state
       ++o;
       if (share) {
+        const unsigned fm = first_of_class(n, p.milli);
 #pragma unroll
         for (int g = 0; g < kMaxGpu; ++g) {
-          if (g < n.gpu_cnt() && n.gl(g) >= p.milli) {
+          if ((fm >> g) & 1u) {
             s_item_node[o] = (uint8_t)tid;
             s_item_code[o] = (uint8_t)(1 + g);  // fgd_score.go:111-118 candidate on GPU g
             ++o;
@@ -297,13 +304,16 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a) {
             if ((sm >> g) & 1u) gl[g] -= p.milli;
         }
       }
-      s_F[j] = frag_F(cpuL, gl, 1u << m.gpu_type(), rp.nt, s_tpi, s_tpf);
+      s_F[j] = rp.typed ? frag_F<true>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt)
+                        : frag_F<false>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt);
     }
     __syncthreads();
     if (tid < nb && feas) {
       const int o = s_off[tid];
       const double F0 = s_F[o];
       if (share) {
+        // candidates are in increasing first-index order: the first max is the
+        // lowest GPU index reaching the max, as fgd_score.go:128 picks it
         int best = -1, bs = 0;
         for (int k = 1; k < nc; ++k) {
           const int fs = fgd_frag_score(F0, s_F[o + k]);
@@ -407,11 +417,10 @@ __global__ void k_advance(int* base, int k) { *base += k; }
 
 // Reserve on an explicit node (ksim_engine_reserve): candidate F values for the
 // FGD selector are evaluated by one workgroup, then thread 0 binds.
-__global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, int r, PodDev p, int node, int step,
-                                                int* out_mask, int sign, int mask_in) {
+__global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* __restrict__ tp_all, int r, PodDev p,
+                                                int node, int step, int* out_mask, int sign, int mask_in) {
   const ReplicaDev rp = reps[r];
-  __shared__ int4 s_tpi[kMaxTypical];
-  __shared__ double s_tpf[kMaxTypical];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   __shared__ double s_F[kMaxCand];
   const int tid = (int)threadIdx.x;
   NodeRec* nr = rp.nodes + node;
@@ -423,12 +432,6 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, int r, PodDev 
   const NodeV n = load_node(nr);
   const bool need_fgd = rp.gpusel == SEL_FGD && is_share_pod(p) && p.milli > 0;
   if (need_fgd) {
-    for (int t = tid; t < rp.nt; t += 64) {
-      const TypDev q = rp.tp[t];
-      s_tpi[t] = make_int4(q.cpu, q.milli, q.num_eff, (int)q.tmask);
-      s_tpf[t] = q.freq;
-    }
-    __syncthreads();
     if (tid < kMaxCand) {
       int gl[kMaxGpu];
       unpack_gl(n, gl);
@@ -444,7 +447,11 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, int r, PodDev 
           }
         }
       }
-      s_F[tid] = valid ? frag_F(cpuL, gl, 1u << n.gpu_type(), rp.nt, s_tpi, s_tpf) : 0.0;
+      double F = 0.0;
+      if (valid)
+        F = rp.typed ? frag_F<true>(cpuL, gl, 1u << n.gpu_type(), tp, rp.ncpu, rp.nt)
+                     : frag_F<false>(cpuL, gl, 1u << n.gpu_type(), tp, rp.ncpu, rp.nt);
+      s_F[tid] = F;
     }
     __syncthreads();
   }
@@ -704,26 +711,37 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
 
 int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp, int n) {
   if (!e || replica < 0 || replica >= e->R || n < 0 || (n > 0 && !tp)) return KSIM_EINVAL;
-  std::vector<TypDev> h;
+  std::vector<TypDev> cpu, gpu;
+  bool typed = false;
   for (int i = 0; i < n; ++i) {
     // frag.go:154-158: entries with freq outside [0,1] are skipped
     if (tp[i].freq < 0 || tp[i].freq > 1 || tp[i].freq != tp[i].freq) continue;
     if (tp[i].gpu_milli < 0 || tp[i].gpu_milli > 0x7fff || tp[i].cpu_milli > 0x3fffffff || tp[i].cpu_milli < -0x3fffffff)
       return KSIM_ERANGE;
     TypDev d;
+    std::memset(&d, 0, sizeof d);
     d.cpu = (int32_t)tp[i].cpu_milli;
     d.milli = tp[i].gpu_milli;
     d.num_eff = std::max(tp[i].gpu_count, 1);
     d.tmask = tp[i].type_mask;
     d.freq = tp[i].freq;
-    h.push_back(d);
+    if (d.milli == 0) {
+      cpu.push_back(d);  // XL/XR bins only (frag.go:463-469)
+    } else {
+      typed |= d.tmask != KSIM_TYPE_ANY;
+      gpu.push_back(d);
+    }
   }
+  std::vector<TypDev> h(cpu);
+  h.insert(h.end(), gpu.begin(), gpu.end());
   if ((int)h.size() > kMaxTypical) return KSIM_ERANGE;
   KSIM_HIP(hipSetDevice(e->device));
   if (!h.empty())
     KSIM_HIP(hipMemcpyAsync(e->d_tp + (size_t)replica * kMaxTypical, h.data(), sizeof(TypDev) * h.size(),
                             hipMemcpyHostToDevice, e->stream));
   e->reps[replica].nt = (int)h.size();
+  e->reps[replica].ncpu = (int)cpu.size();
+  e->reps[replica].typed = typed ? 1 : 0;
   int rc = upload_reps(e);
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
@@ -772,7 +790,7 @@ int ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, i
   a.out_feas = e->d_feas;
   a.out_score = e->d_score;
   a.out_gpu = e->d_gpu;
-  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a);
+  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
   KSIM_HIP(hipGetLastError());
   KSIM_HIP(hipMemcpyAsync(feasible, e->d_feas, e->N, hipMemcpyDeviceToHost, e->stream));
   KSIM_HIP(hipMemcpyAsync(score, e->d_score, sizeof(int32_t) * e->N, hipMemcpyDeviceToHost, e->stream));
@@ -795,7 +813,7 @@ int ksim_engine_schedule(ksim_engine* e, int replica, const ksim_pod* pod, int32
   a.pod_override = e->d_pod;
   a.res_override = e->d_res1;
   a.mode = 0;
-  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a);
+  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
   KSIM_HIP(hipGetLastError());
   ResultDev r;
   KSIM_HIP(hipMemcpyAsync(&r, e->d_res1, sizeof r, hipMemcpyDeviceToHost, e->stream));
@@ -810,7 +828,7 @@ int ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int no
   int rc = to_pod_dev(*pod, &p);
   if (rc) return rc;
   KSIM_HIP(hipSetDevice(e->device));
-  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, replica, p, node, step, e->d_scratch, +1, 0);
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, step, e->d_scratch, +1, 0);
   KSIM_HIP(hipGetLastError());
   int m = 0;
   KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
@@ -825,7 +843,7 @@ int ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int 
   int rc = to_pod_dev(*pod, &p);
   if (rc) return rc;
   KSIM_HIP(hipSetDevice(e->device));
-  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, replica, p, node, 0, e->d_scratch, -1,
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, 0, e->d_scratch, -1,
                      (int)gpu_mask);
   KSIM_HIP(hipGetLastError());
   KSIM_HIP(hipStreamSynchronize(e->stream));
@@ -877,7 +895,7 @@ static int build_graph(ksim_engine* e) {
   a.base = e->d_base;
   for (int i = 0; i < e->K; ++i) {
     a.step_off = i;
-    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
+    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
   }
   hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_base, e->K);
   KSIM_HIP(hipStreamEndCapture(e->stream, &g));
@@ -925,7 +943,7 @@ int ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us) 
   for (int i = 0; i < n_steps; ++i) {
     a.step_off = i;
     KSIM_HIP(hipEventRecord(evs[2 * i], e->stream));
-    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
+    hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
     KSIM_HIP(hipEventRecord(evs[2 * i + 1], e->stream));
   }
   KSIM_HIP(hipStreamSynchronize(e->stream));

@@ -11,11 +11,43 @@ extern "C" {
 
 double dm_go_exp(double x) { return go_exp(x); }
 
-// F(state) for a node state given as (cpu_left, gl[8], type id) and a typical table
+// host copy of the engine's split table: CPU-only entries first, then GPU entries (order kept)
+static int split_table(int T, const int* tpi4, const double* tpf, TypDev* out, int* ncpu, bool* typed) {
+  int k = 0;
+  *typed = false;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int t = 0; t < T; ++t) {
+      const bool cpu = tpi4[4 * t + 1] == 0;
+      if ((pass == 0) != cpu) continue;
+      TypDev d;
+      std::memset(&d, 0, sizeof d);
+      d.cpu = tpi4[4 * t];
+      d.milli = tpi4[4 * t + 1];
+      d.num_eff = tpi4[4 * t + 2];
+      d.tmask = (uint32_t)tpi4[4 * t + 3];
+      d.freq = tpf[t];
+      if (!cpu && d.tmask != 0xFFFFFFFFu) *typed = true;
+      out[k++] = d;
+      if (pass == 0) *ncpu = k;
+    }
+  if (*ncpu > k) *ncpu = 0;
+  return k;
+}
+
+static double F_of(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, const TypDev* tp, int ncpu, int nt,
+                   bool typed) {
+  return typed ? frag_F<true>(cpuL, gl, typebit, tp, ncpu, nt) : frag_F<false>(cpuL, gl, typebit, tp, ncpu, nt);
+}
+
+// F(state) for a node state given as (cpu_left, gl[8], type id) and a typical table {cpu,milli,num_eff,mask},freq
 double dm_frag_F(int cpu_left, const int* gl8, int type_id, int T, const int* tpi4, const double* tpf) {
+  static TypDev tp[kMaxTypical];
+  int ncpu = 0;
+  bool typed = false;
+  const int nt = split_table(T, tpi4, tpf, tp, &ncpu, &typed);
   int gl[kMaxGpu];
   for (int g = 0; g < kMaxGpu; ++g) gl[g] = gl8[g];
-  return frag_F(cpu_left, gl, 1u << type_id, T, reinterpret_cast<const int4*>(tpi4), tpf);
+  return F_of(cpu_left, gl, 1u << type_id, tp, ncpu, nt, typed);
 }
 
 static NodeV mk(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left) {
@@ -39,25 +71,30 @@ static PodDev pod(int cpu, int milli, int num, unsigned mask) {
   return p;
 }
 
-// FGD score of one node for one pod, as k_step computes it (current state + candidates)
+// FGD score of one node for one pod, as k_step computes it (current state + one candidate per
+// distinct fitting milli-left value, or the Sub state)
 int dm_fgd_score(int cpu_left, const int* gl8, int gpu_cnt, int type_id, int cpu, int milli, int num, int T,
                  const int* tpi4, const double* tpf, int* gpu_out) {
+  static TypDev tp[kMaxTypical];
+  int ncpu = 0;
+  bool typed = false;
+  const int nt = split_table(T, tpi4, tpf, tp, &ncpu, &typed);
   const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, type_id, 100);
   const PodDev p = pod(cpu, milli, num, 0xffffffffu);
-  const int4* tpi = reinterpret_cast<const int4*>(tpi4);
   int gl[kMaxGpu];
   unpack_gl(n, gl);
-  const double F0 = frag_F(n.cpu_left, gl, 1u << type_id, T, tpi, tpf);
+  const double F0 = F_of(n.cpu_left, gl, 1u << type_id, tp, ncpu, nt, typed);
   *gpu_out = -1;
   if (is_share_pod(p)) {
     int best = -1, bs = 0;
     for (int g = 0; g < kMaxGpu; ++g) {
-      if (g < gpu_cnt && gl[g] >= milli) {
-        int c[kMaxGpu];
-        for (int k = 0; k < kMaxGpu; ++k) c[k] = gl[k] - (k == g ? milli : 0);
-        const int fs = fgd_frag_score(F0, frag_F(n.cpu_left - cpu, c, 1u << type_id, T, tpi, tpf));
-        if (best < 0 || fs > bs) { bs = fs; best = g; }
-      }
+      bool first = g < gpu_cnt && gl[g] >= milli;
+      for (int h = 0; h < g; ++h) first = first && !(gl[h] == gl[g]);
+      if (!first) continue;
+      int c[kMaxGpu];
+      for (int k = 0; k < kMaxGpu; ++k) c[k] = gl[k] - (k == g ? milli : 0);
+      const int fs = fgd_frag_score(F0, F_of(n.cpu_left - cpu, c, 1u << type_id, tp, ncpu, nt, typed));
+      if (best < 0 || fs > bs) { bs = fs; best = g; }
     }
     *gpu_out = best;
     return bs;
@@ -71,7 +108,7 @@ int dm_fgd_score(int cpu_left, const int* gl8, int gpu_cnt, int type_id, int cpu
     cl -= cpu;
     for (int k = 0; k < kMaxGpu; ++k) c[k] -= ((sm >> k) & 1u) ? milli : 0;
   }
-  return fgd_frag_score(F0, frag_F(cl, c, 1u << type_id, T, tpi, tpf));
+  return fgd_frag_score(F0, F_of(cl, c, 1u << type_id, tp, ncpu, nt, typed));
 }
 
 int dm_filter(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left, int cpu, int mem,
