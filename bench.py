@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--replicas", type=int, default=10, help="seeds per GPU (C2: 10)")
     ap.add_argument("--nodes-per-block", type=int, default=0)
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per replica (0 = auto)")
+    ap.add_argument("--run-mode", type=int, default=0, help="0 persistent k_replay, 1 k_step per pod")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | ...")
@@ -75,7 +77,7 @@ def main():
 
     trace = ksim.Trace.openb("default")
     seeds = [42 + args.replicas * rank + i for i in range(args.replicas)]
-    eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy)
+    eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode)
     total_events = eng.total_events
 
     for _ in range(args.warmup):
@@ -99,9 +101,10 @@ def main():
         dt = float(t.item())
 
     steps_per_run = eng.last_run_steps()
-    # roofline: mean k_step duration over every step of one replay, hipEvent-timed on the engine stream
-    kern_us = eng.time_steps(steps_per_run)
-    bytes_per_launch = total_events / steps_per_run * (BYTES_PER_NODE_EVAL * trace.num_nodes + BYTES_PER_POD)
+    # roofline: the dominant kernel is k_replay, one launch per replay of all replicas; its duration is
+    # the hipEvent pair around the launch on the engine stream (mean over the timed runs)
+    kern_us = dev_ms / args.steps * 1000.0
+    bytes_per_launch = total_events * (BYTES_PER_NODE_EVAL * trace.num_nodes + BYTES_PER_POD)
     achieved = bytes_per_launch / (kern_us * 1e-6) / 1e9
 
     pods_total = total_events * args.steps * world
@@ -127,7 +130,8 @@ def main():
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_step", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch},
+                     "kernel": "k_replay", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
+                     "wgs_per_replica": eng.last_run_wgs()},
     }
     if args.policy != "FGD":
         line["config"]["workload"] = line["config"]["workload"].replace("FGD", args.policy)
@@ -140,9 +144,10 @@ def main():
         dist.destroy_process_group()
 
 
-def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD"):
+def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_mode=0):
     arr, n = trace.typical()
-    eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block)
+    eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block,
+                      wgs_per_replica=wgs, run_mode=run_mode)
     total = 0
     for r, s in enumerate(seeds):
         rp = trace.replay(seed=s, tune_ratio=1.3, shuffle=True)

@@ -136,9 +136,11 @@ typedef struct ksim_engine ksim_engine;
 /* Engine configuration (0 = default). */
 typedef struct {
     int32_t device;                /* HIP device ordinal */
-    int32_t nodes_per_block;       /* nodes per workgroup in the step kernel (default 32) */
-    int32_t steps_per_graph;       /* pod steps captured per hipGraph (default 256) */
-    int32_t reserved;
+    int32_t nodes_per_block;       /* k_step: nodes per workgroup (default 64) */
+    int32_t steps_per_graph;       /* k_step: pod steps captured per hipGraph (default 256) */
+    int32_t wgs_per_replica;       /* k_replay: workgroups per replica (0 = CUs / replicas, <= 64) */
+    int32_t run_mode;              /* ksim_engine_run: 0 = persistent k_replay, 1 = k_step per pod (hipGraph) */
+    int32_t reserved[3];
 } ksim_config;
 
 const char* ksim_strerror(int code);
@@ -187,6 +189,8 @@ int  ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us)
 int  ksim_engine_last_run_ms(ksim_engine* e, double* ms);
 /* Steps executed by the last run (max events over replicas). */
 int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
+/* Workgroups per replica used by the last run. */
+int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 
 #ifdef __cplusplus
 }

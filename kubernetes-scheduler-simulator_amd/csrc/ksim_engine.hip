@@ -160,6 +160,130 @@ __device__ __forceinline__ unsigned first_of_class(const NodeV& n, int milli) {
   return fm;
 }
 
+// ---------------------------------------------------------------------------
+// Per-node pieces shared by k_step (one launch per pod) and k_replay (persistent).
+// ---------------------------------------------------------------------------
+
+// Filter, then the cheap scores; for FGD only the candidate count.  `tags` may
+// point at global memory (k_step) or LDS (k_replay).
+__device__ __forceinline__ bool node_phase1(const NodeV& n, const PodDev& p, const ReplicaDev& rp,
+                                            const uint16_t* tags, int step, bool share, int* raw, int* nc,
+                                            bool* err) {
+  *raw = 0;
+  *nc = 0;
+  *err = false;
+  if (!filter_node(n, p)) return false;
+  const int total = n.total();
+  switch (rp.policy) {
+    case POL_FGD:
+      // one candidate per DISTINCT milli-left value among the fitting GPUs: placing the pod on
+      // any GPU of a value class yields the same multiset of GPU states, hence the same F
+      // (frag.go depends on the multiset only) and the same score.
+      *nc = share ? 1 + __builtin_popcount(first_of_class(n, p.milli)) : 2;
+      break;
+    case POL_BESTFIT:
+      *raw = bestfit_score(n, p, total);
+      if (*raw < 0) { *err = true; *raw = 0; }
+      break;
+    case POL_DOTPROD:
+      *raw = dotprod_score(n, p, total);
+      break;
+    case POL_PACKING: {
+      bool perr = false;
+      *raw = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
+      *err = perr;
+      break;
+    }
+    case POL_CLUSTERING:
+      if (p.tag == -2) *err = true;
+      else *raw = clustering_score(tags, p.tag, total);
+      break;
+    default:  // POL_RANDOM: RandomScorePlugin.PreScore pick, as a 24-bit hash key
+      *raw = (int)(rand_node_key(rp.seed, step, n.name_rank) >> 40);
+      break;
+  }
+  return true;
+}
+
+// FGD work list of one node: current state, then one candidate per GPU value class
+// (share pod) or the NodeResource.Sub state.
+__device__ __forceinline__ void emit_fgd_items(const NodeV& n, const PodDev& p, bool share, int local, int o,
+                                               uint8_t* item_node, uint8_t* item_code) {
+  item_node[o] = (uint8_t)local;
+  item_code[o] = 0;  // current state
+  ++o;
+  if (share) {
+    const unsigned fm = first_of_class(n, p.milli);
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      if ((fm >> g) & 1u) {
+        item_node[o] = (uint8_t)local;
+        item_code[o] = (uint8_t)(1 + g);  // fgd_score.go:111-118 candidate on GPU g
+        ++o;
+      }
+    }
+  } else {
+    item_node[o] = (uint8_t)local;
+    item_code[o] = 9;  // fgd_score.go:137-141 NodeResource.Sub
+  }
+}
+
+// F of one candidate state.
+__device__ __forceinline__ double eval_fgd_item(const NodeV& m, int code, const PodDev& p, const ReplicaDev& rp,
+                                                const TypDev* __restrict__ tp) {
+  int gl[kMaxGpu];
+  unpack_gl(m, gl);
+  int cpuL = m.cpu_left;
+  if (code >= 1 && code <= 8) {
+    cpuL -= p.cpu_nz;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) gl[g] -= (g == code - 1) ? (int)p.milli : 0;
+  } else if (code == 9) {
+    bool ok = false;
+    const unsigned sm = sub_gpu_mask(gl, m.gpu_cnt(), cpuL, p, &ok);
+    if (ok) {
+      cpuL -= p.cpu_nz;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g)
+        if ((sm >> g) & 1u) gl[g] -= p.milli;
+    }
+  }
+  return rp.typed ? frag_F<true>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt)
+                  : frag_F<false>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt);
+}
+
+// Node score from its candidates' F values; *gpu = lowest GPU index reaching the max (share pods).
+__device__ __forceinline__ void finalize_fgd(const double* F, const uint8_t* code, int o, int nc, bool share,
+                                             int* raw, int* gpu) {
+  const double F0 = F[o];
+  *gpu = -1;
+  if (share) {
+    // candidates are in increasing first-index order: the first max is the lowest GPU index
+    // reaching the max, as fgd_score.go:128 picks it
+    int best = -1, bs = 0;
+    for (int k = 1; k < nc; ++k) {
+      const int fs = fgd_frag_score(F0, F[o + k]);
+      if (best < 0 || fs > bs) { bs = fs; best = code[o + k] - 1; }
+    }
+    *raw = bs;
+    *gpu = best;
+  } else {
+    *raw = fgd_frag_score(F0, F[o + 1]);
+  }
+}
+
+// Winning total weighted score as the reference reports it (0 on the single-feasible shortcut).
+__device__ __forceinline__ long long result_score(const ReplicaDev& rp, int nfeas, int wscore, int lo, int hi) {
+  if (nfeas <= 1) return 0;
+  if (rp.policy == POL_BESTFIT) return (hi > lo ? 100 : 0) * 1000LL;  // NormalizeScore (plugin_utils.go:48-74)
+  if (rp.policy == POL_RANDOM) return 100 * 1000LL;
+  return (long long)wscore * 1000LL;
+}
+
+__device__ __forceinline__ uint32_t key_rank(unsigned long long key) {
+  return 0xFFFFFFFFu - (uint32_t)((key >> 8) & 0xFFFFFFFFull);
+}
+
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __restrict__ tp_all) {
   const int r = a.rep_first + (int)blockIdx.x / a.bpr;
   const int b = (int)blockIdx.x % a.bpr;
@@ -209,43 +333,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
   if (tid < nb) {
     n = load_node(rp.nodes + n0 + tid);
     store_node(&s_node[tid], n);
-    feas = filter_node(n, p);
-    if (feas) {
-      const int total = n.total();
-      switch (rp.policy) {
-        case POL_FGD: {
-          if (share) {
-            // one candidate per DISTINCT milli-left value among the fitting GPUs: placing the
-            // pod on any GPU of a value class yields the same multiset of GPU states, hence the
-            // same F (frag.go depends on the multiset only) and the same score.
-            nc = 1 + __builtin_popcount(first_of_class(n, p.milli));
-          } else {
-            nc = 2;
-          }
-          break;
-        }
-        case POL_BESTFIT:
-          raw = bestfit_score(n, p, total);
-          if (raw < 0) { err = true; raw = 0; }
-          break;
-        case POL_DOTPROD:
-          raw = dotprod_score(n, p, total);
-          break;
-        case POL_PACKING: {
-          bool perr = false;
-          raw = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
-          err = perr;
-          break;
-        }
-        case POL_CLUSTERING:
-          if (p.tag == -2) err = true;
-          else raw = clustering_score(rp.tags + (size_t)(n0 + tid) * kTagStride, p.tag, total);
-          break;
-        default:  // POL_RANDOM: RandomScorePlugin.PreScore pick, as a 24-bit hash key
-          raw = (int)(rand_node_key(rp.seed, step, n.name_rank) >> 40);
-          break;
-      }
-    }
+    feas = node_phase1(n, p, rp, rp.tags + (size_t)(n0 + tid) * kTagStride, step, share, &raw, &nc, &err);
   }
 
   // ---- phase 2: FGD candidate evaluation over a compacted work list ----
@@ -262,69 +350,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
       if (tid == 63) s_off[64] = incl;
     }
     __syncthreads();
-    if (tid < nb && nc > 0) {
-      int o = s_off[tid];
-      s_item_node[o] = (uint8_t)tid;
-      s_item_code[o] = 0;  // current state
-      ++o;
-      if (share) {
-        const unsigned fm = first_of_class(n, p.milli);
-#pragma unroll
-        for (int g = 0; g < kMaxGpu; ++g) {
-          if ((fm >> g) & 1u) {
-            s_item_node[o] = (uint8_t)tid;
-            s_item_code[o] = (uint8_t)(1 + g);  // fgd_score.go:111-118 candidate on GPU g
-            ++o;
-          }
-        }
-      } else {
-        s_item_node[o] = (uint8_t)tid;
-        s_item_code[o] = 9;  // fgd_score.go:137-141 NodeResource.Sub
-      }
-    }
+    if (tid < nb && nc > 0) emit_fgd_items(n, p, share, tid, s_off[tid], s_item_node, s_item_code);
     __syncthreads();
     const int items = s_off[64];
-    for (int j = tid; j < items; j += kBlock) {
-      const NodeV m = load_node(&s_node[s_item_node[j]]);
-      const int code = s_item_code[j];
-      int gl[kMaxGpu];
-      unpack_gl(m, gl);
-      int cpuL = m.cpu_left;
-      if (code >= 1 && code <= 8) {
-        cpuL -= p.cpu_nz;
-#pragma unroll
-        for (int g = 0; g < kMaxGpu; ++g) gl[g] -= (g == code - 1) ? (int)p.milli : 0;
-      } else if (code == 9) {
-        bool ok = false;
-        const unsigned sm = sub_gpu_mask(gl, m.gpu_cnt(), cpuL, p, &ok);
-        if (ok) {
-          cpuL -= p.cpu_nz;
-#pragma unroll
-          for (int g = 0; g < kMaxGpu; ++g)
-            if ((sm >> g) & 1u) gl[g] -= p.milli;
-        }
-      }
-      s_F[j] = rp.typed ? frag_F<true>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt)
-                        : frag_F<false>(cpuL, gl, 1u << m.gpu_type(), tp, rp.ncpu, rp.nt);
-    }
+    for (int j = tid; j < items; j += kBlock)
+      s_F[j] = eval_fgd_item(load_node(&s_node[s_item_node[j]]), s_item_code[j], p, rp, tp);
     __syncthreads();
-    if (tid < nb && feas) {
-      const int o = s_off[tid];
-      const double F0 = s_F[o];
-      if (share) {
-        // candidates are in increasing first-index order: the first max is the
-        // lowest GPU index reaching the max, as fgd_score.go:128 picks it
-        int best = -1, bs = 0;
-        for (int k = 1; k < nc; ++k) {
-          const int fs = fgd_frag_score(F0, s_F[o + k]);
-          if (best < 0 || fs > bs) { bs = fs; best = s_item_code[o + k] - 1; }
-        }
-        raw = bs;
-        gpu = best;
-      } else {
-        raw = fgd_frag_score(F0, s_F[o + 1]);
-      }
-    }
+    if (tid < nb && feas) finalize_fgd(s_F, s_item_code, s_off[tid], nc, share, &raw, &gpu);
   }
 
   if (a.mode == 1) {
@@ -379,27 +411,15 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
 
   ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
   if (nfeas > 0) {
-    const uint32_t wrank = 0xFFFFFFFFu - (uint32_t)((best >> 8) & 0xFFFFFFFFull);
-    const int wscore = (int)(best >> 40);
-    const int wgpu = (int)(best & 0xFF) - 1;
-    // find the winner's index: ranks are unique, the key carries ~rank; the
-    // node index is recovered from the rank->index table built on the host.
-    (void)wrank;
-    out.status = ST_OK;
-    if (nfeas > 1) {
-      if (anyerr) out.status = ST_ERROR;  // framework.go:650-656: a Score error aborts the cycle
-      else if (rp.policy == POL_BESTFIT) out.score = (ghi > glo ? 100 : 0) * 1000LL;  // NormalizeScore
-      else if (rp.policy == POL_RANDOM) out.score = 100 * 1000LL;
-      else out.score = (long long)wscore * 1000LL;
-    }
-    (void)glo;
+    out.status = (nfeas > 1 && anyerr) ? ST_ERROR : ST_OK;  // framework.go:650-656: a Score error aborts
     if (out.status == ST_OK) {
+      out.score = result_score(rp, nfeas, (int)(best >> 40), glo, ghi);
       // the rank -> node index map lives right after the replica's tags (see host)
       const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
-      const int node = rank2idx[wrank];
+      const int node = rank2idx[key_rank(best)];
       NodeRec* nr = rp.nodes + node;
       const NodeV wn = load_node(nr);
-      const int mask = select_gpus(wn, p, rp.gpusel, wgpu, rp.seed, step);
+      const int mask = select_gpus(wn, p, rp.gpusel, (int)(best & 0xFF) - 1, rp.seed, step);
       if (mask < 0) {
         out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
         out.score = 0;
@@ -411,6 +431,218 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
     }
   }
   *res_slot = out;
+}
+
+#include "ksim_replay.hpp"
+
+// ---------------------------------------------------------------------------
+// k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
+// Dynamic LDS: NodeRec nodes[S] | u16 tags[S][16].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
+                                                                 const TypDev* __restrict__ tp_all) {
+  using namespace ksim_replay;
+  // all LDS is dynamic (no static __shared__ in front of it), carved 16-byte aligned
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  ReplayShared& sh = *reinterpret_cast<ReplayShared*>(smem);
+  int* s_tmp = sh.tmp;
+  uint8_t* s_item_node = sh.item_node;
+  uint8_t* s_item_code = sh.item_code;
+  double* s_F = sh.F;
+  unsigned long long* s_rkey = sh.rkey;
+  int *s_rcnt = sh.rcnt, *s_rerr = sh.rerr, *s_rlo = sh.rlo, *s_rhi = sh.rhi;
+  unsigned long long& s_win = sh.win;
+  int* s_wstat = sh.wstat;
+  int& s_stop = sh.stop;
+  const int r = (int)blockIdx.x / a.K;
+  const int w = (int)blockIdx.x % a.K;
+  const int tid = (int)threadIdx.x;
+  const ReplicaDev rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
+  const int n_lo = w * a.S;
+  const int ns = max(0, min(a.S, a.N - n_lo));
+  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(ReplayShared));
+  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)a.S * sizeof(NodeRec));
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
+  int2* hist = a.hist + (size_t)(r * a.K + w) * a.hist_stride;
+  unsigned long long* gr = a.gran + (size_t)r * 2 * a.K * 4;
+
+  for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
+  for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
+  if (tid == 0) s_stop = 0;
+  __syncthreads();
+
+  const bool fgd = rp.policy == POL_FGD;
+  for (int step = 0; step < rp.n_events; ++step) {
+    const PodDev p = rp.ev[step];
+    if (p.flags & kPodDelete) {
+      // removePod on the owner of the creation (every workgroup recorded the winner)
+      if (tid == 0) {
+        const int2 h = (p.ref >= 0 && p.ref < step) ? hist[p.ref] : make_int2(-1, 0);
+        if (h.x >= 0 && h.y != 0) {
+          const PodDev cp = rp.ev[p.ref];
+          const int loc = h.x - n_lo;
+          apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
+          rp.res[step] = ResultDev{h.x, h.y - 1, 0, 0, ST_DELETED};
+        } else if (h.x < 0 && w == 0) {
+          rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
+        }
+        hist[step] = make_int2(-1, 0);
+      }
+      __syncthreads();
+      continue;
+    }
+    const bool share = is_share_pod(p);
+    unsigned long long key = 0ull;
+    int cnt = 0, lo = 0x7fffffff, hi = -1;
+    bool err = false;
+    for (int c0 = 0; c0 < ns; c0 += kChunk) {
+      const int cn = min(kChunk, ns - c0);
+      bool feas = false, e1 = false;
+      int raw = 0, nc = 0, gpu = -1;
+      NodeV n{};
+      if (tid < cn) {
+        n = load_node(&s_nodes[c0 + tid]);
+        feas = node_phase1(n, p, rp, &s_tags[(size_t)(c0 + tid) * kTagStride], step, share, &raw, &nc, &e1);
+      }
+      if (fgd) {
+        int tot = 0;
+        const int off = block_excl_scan(tid < cn ? nc : 0, s_tmp, &tot);
+        if (tid < cn && nc > 0) emit_fgd_items(n, p, share, tid, off, s_item_node, s_item_code);
+        __syncthreads();
+        for (int j = tid; j < tot; j += kRBlock)
+          s_F[j] = eval_fgd_item(load_node(&s_nodes[c0 + s_item_node[j]]), s_item_code[j], p, rp, tp);
+        __syncthreads();
+        if (tid < cn && feas) finalize_fgd(s_F, s_item_code, off, nc, share, &raw, &gpu);
+        __syncthreads();  // s_F / items are reused by the next chunk
+      }
+      if (feas) {
+        const unsigned long long k = pack_key((unsigned)raw, n.name_rank, gpu);
+        key = k > key ? k : key;
+        ++cnt;
+        lo = min(lo, raw);
+        hi = max(hi, raw);
+        err |= e1;
+      }
+    }
+    // workgroup reduction
+    key = wave_max_u64(key);
+    cnt = wave_sum_i(cnt);
+    const int ew = wave_max_i(err ? 1 : 0);
+    lo = wave_min_i(lo);
+    hi = wave_max_i(hi);
+    const int wv = tid >> 6;
+    if ((tid & 63) == 0) { s_rkey[wv] = key; s_rcnt[wv] = cnt; s_rerr[wv] = ew; s_rlo[wv] = lo; s_rhi[wv] = hi; }
+    __syncthreads();
+    if (tid < 64) {
+      if (a.K == 1) {
+        if (tid == 0) {
+          unsigned long long kk = s_rkey[0];
+          int c = s_rcnt[0], e = s_rerr[0], l = s_rlo[0], h = s_rhi[0];
+          for (int i = 1; i < kRBlock / 64; ++i) {
+            kk = s_rkey[i] > kk ? s_rkey[i] : kk;
+            c += s_rcnt[i]; e |= s_rerr[i]; l = min(l, s_rlo[i]); h = max(h, s_rhi[i]);
+          }
+          s_win = kk;
+          s_wstat[0] = c; s_wstat[1] = e; s_wstat[2] = l; s_wstat[3] = h;
+        }
+      } else {
+        unsigned long long* slot = gr + (size_t)(step & 1) * a.K * 4;
+        const unsigned long long tag = (unsigned long long)(unsigned)(step + 1) << 32;
+        if (tid == 0) {
+          unsigned long long kk = s_rkey[0];
+          int c = s_rcnt[0], e = s_rerr[0], l = s_rlo[0], h = s_rhi[0];
+          for (int i = 1; i < kRBlock / 64; ++i) {
+            kk = s_rkey[i] > kk ? s_rkey[i] : kk;
+            c += s_rcnt[i]; e |= s_rerr[i]; l = min(l, s_rlo[i]); h = max(h, s_rhi[i]);
+          }
+          // granules: {tag, key lo32}, {tag, key hi32}, {tag, err|hi|lo|cnt}
+          const unsigned stat = ((unsigned)e << 31) | ((unsigned)(h < 0 ? 0 : h) & 0x7f) << 24 |
+                                ((unsigned)(l > 127 ? 127 : l) & 0x7f) << 17 | ((unsigned)c & 0x1ffff);
+          gstore(slot + (size_t)w * 4 + 0, tag | (kk & 0xffffffffull));
+          gstore(slot + (size_t)w * 4 + 1, tag | (kk >> 32));
+          gstore(slot + (size_t)w * 4 + 2, tag | stat);
+        }
+        // one wave polls every workgroup's granules of this step (lane k <-> workgroup k)
+        unsigned long long g0 = 0, g1 = 0, g2 = 0;
+        bool ok = false;
+        unsigned spins = 0;
+        for (;;) {
+          if (tid < a.K) {
+            g0 = gload(slot + (size_t)tid * 4 + 0);
+            g1 = gload(slot + (size_t)tid * 4 + 1);
+            g2 = gload(slot + (size_t)tid * 4 + 2);
+            ok = (g0 & ~0xffffffffull) == tag && (g1 & ~0xffffffffull) == tag && (g2 & ~0xffffffffull) == tag;
+          } else {
+            ok = true;
+          }
+          if (__all(ok)) break;
+          if (++spins > kSpinLimit) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const bool timed_out = !__all(ok);
+        unsigned long long kk = tid < a.K ? ((g1 & 0xffffffffull) << 32) | (g0 & 0xffffffffull) : 0ull;
+        const unsigned st = tid < a.K ? (unsigned)(g2 & 0xffffffffull) : 0u;
+        int c = (int)(st & 0x1ffff), e = (int)(st >> 31);
+        int l = tid < a.K && c > 0 ? (int)((st >> 17) & 0x7f) : 0x7fffffff;
+        int h = tid < a.K && c > 0 ? (int)((st >> 24) & 0x7f) : -1;
+        kk = wave_max_u64(kk);
+        c = wave_sum_i(c);
+        e = wave_max_i(e);
+        l = wave_min_i(l);
+        h = wave_max_i(h);
+        if (tid == 0) {
+          s_win = kk;
+          s_wstat[0] = c; s_wstat[1] = e; s_wstat[2] = l; s_wstat[3] = h;
+          if (timed_out) {
+            s_stop = 1;
+            atomicOr(a.fail, 1);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s_stop) break;
+    if (tid == 0) {
+      const unsigned long long best = s_win;
+      const int nfeas = s_wstat[0];
+      ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+      int2 hrec = make_int2(-1, 0);
+      bool writer = w == 0;
+      if (nfeas > 0) {
+        out.status = (nfeas > 1 && s_wstat[1]) ? ST_ERROR : ST_OK;
+        if (out.status == ST_OK) {
+          const int node = rank2idx[key_rank(best)];
+          hrec.x = node;
+          out.score = result_score(rp, nfeas, (int)(best >> 40), s_wstat[2], s_wstat[3]);
+          if (node >= n_lo && node < n_lo + ns) {
+            // this workgroup owns the winner: Reserve's GPU selector + Bind on the LDS record
+            writer = true;
+            const int loc = node - n_lo;
+            const NodeV wn = load_node(&s_nodes[loc]);
+            const int mask = select_gpus(wn, p, rp.gpusel, (int)(best & 0xFF) - 1, rp.seed, step);
+            if (mask < 0) {
+              out.status = ST_ERROR;
+              out.score = 0;
+            } else {
+              apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], p, mask, +1);
+              out.node = node;
+              out.gpu_mask = mask;
+              hrec.y = mask + 1;
+            }
+          } else {
+            writer = false;  // the owner reports
+          }
+        }
+      }
+      hist[step] = hrec;
+      if (writer) rp.res[step] = out;
+    }
+    __syncthreads();
+  }
+  // write the slice back (final cluster state)
+  for (int i = tid; i < ns; i += kRBlock) store_node(rp.nodes + n_lo + i, load_node(&s_nodes[i]));
+  for (int i = tid; i < ns * kTagStride; i += kRBlock) rp.tags[(size_t)n_lo * kTagStride + i] = s_tags[i];
 }
 
 __global__ void k_advance(int* base, int k) { *base += k; }
@@ -488,7 +720,15 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
 // ---------------------------------------------------------------------------
 struct ksim_engine {
   int device = 0;
-  int N = 0, R = 0, NB = 32, bpr = 0, K = 256;
+  int N = 0, R = 0, NB = 64, bpr = 0, K = 256;
+  int run_mode = 0;        // 0: persistent k_replay, 1: one k_step launch per pod (hipGraph)
+  int wgs_req = 0;         // requested workgroups per replica (0 = auto)
+  int cus = 256;
+  unsigned long long* d_gran = nullptr;
+  int2* d_hist = nullptr;
+  size_t hist_cap = 0;
+  int* d_fail = nullptr;
+  int last_K = 0;
   hipStream_t stream = nullptr;
   NodeRec* d_nodes = nullptr;
   NodeRec* d_nodes_init = nullptr;  // cluster state given to set_nodes (run() restarts from it)
@@ -573,6 +813,15 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->R = n_replicas;
   if (cfg && cfg->nodes_per_block > 0) e->NB = std::min(cfg->nodes_per_block, kNBMax);
   if (cfg && cfg->steps_per_graph > 0) e->K = cfg->steps_per_graph;
+  if (cfg) {
+    e->run_mode = cfg->run_mode;
+    e->wgs_req = cfg->wgs_per_replica;
+  }
+  {
+    hipDeviceProp_t prop;
+    KSIM_HIP(hipGetDeviceProperties(&prop, dev));
+    e->cus = prop.multiProcessorCount;
+  }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
   KSIM_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
@@ -593,6 +842,8 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_feas, (size_t)n_nodes));
   KSIM_HIP(hipMalloc(&e->d_score, sizeof(int32_t) * n_nodes));
   KSIM_HIP(hipMalloc(&e->d_gpu, sizeof(int32_t) * n_nodes));
+  KSIM_HIP(hipMalloc(&e->d_gran, sizeof(unsigned long long) * (size_t)n_replicas * 2 * ksim_replay::kMaxK * 4));
+  KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
   KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
   std::vector<Accum> acc(n_replicas);
   for (auto& a : acc) {
@@ -632,7 +883,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (auto p : e->d_ev) (void)hipFree(p);
   for (auto p : e->d_res) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
-                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu};
+                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -905,6 +1156,65 @@ static int build_graph(ksim_engine* e) {
   return KSIM_OK;
 }
 
+// Workgroups per replica for k_replay: every workgroup of a replica must be
+// co-resident (they exchange granules every step), so R*K never exceeds one
+// workgroup per CU; K = 1 needs no co-residency at all.
+static int choose_wgs(const ksim_engine* e) {
+  int K = e->wgs_req > 0 ? e->wgs_req : e->cus / e->R;
+  K = std::max(1, std::min(K, ksim_replay::kMaxK));
+  K = std::min(K, e->N);
+  if (e->R * K > e->cus) K = 1;
+  return K;
+}
+
+static size_t replay_lds(int S) {
+  return sizeof(ksim_replay::ReplayShared) + (size_t)S * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t));
+}
+
+static int run_persistent(ksim_engine* e, int max_ev) {
+  int K = choose_wgs(e);
+  int S = (e->N + K - 1) / K;
+  while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && e->R * (K + 1) <= e->cus) {
+    ++K;
+    S = (e->N + K - 1) / K;
+  }
+  if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
+  const size_t need = (size_t)e->R * K * std::max(max_ev, 1);
+  if (need > e->hist_cap) {
+    if (e->d_hist) KSIM_HIP(hipFree(e->d_hist));
+    KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
+    e->hist_cap = need;
+  }
+  const size_t lds = replay_lds(S);
+  KSIM_HIP(hipFuncSetAttribute((const void*)k_replay, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  ksim_replay::ReplayArgs ra;
+  ra.reps = e->d_reps;
+  ra.N = e->N;
+  ra.K = K;
+  ra.S = S;
+  ra.gran = e->d_gran;
+  ra.hist = e->d_hist;
+  ra.hist_stride = std::max(max_ev, 1);
+  ra.fail = e->d_fail;
+  // re-initialise every polled word before the launch (granule tags restart at step 1)
+  KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
+                          e->stream));
+  KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
+  hipLaunchKernelGGL(k_replay, dim3(e->R * K), dim3(ksim_replay::kRBlock), lds, e->stream, ra, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  e->last_K = K;
+  return KSIM_OK;
+}
+
+static int run_graph(ksim_engine* e, int max_ev) {
+  int rc = build_graph(e);
+  if (rc) return rc;
+  KSIM_HIP(hipMemsetAsync(e->d_base, 0, sizeof(int), e->stream));
+  const int reps = (max_ev + e->K - 1) / e->K;
+  for (int i = 0; i < reps; ++i) KSIM_HIP(hipGraphLaunch(e->graph, e->stream));
+  return KSIM_OK;
+}
+
 int ksim_engine_run(ksim_engine* e) {
   if (!e) return KSIM_EINVAL;
   int max_ev = 0;
@@ -913,20 +1223,28 @@ int ksim_engine_run(ksim_engine* e) {
     max_ev = std::max(max_ev, e->n_events[r]);
   }
   KSIM_HIP(hipSetDevice(e->device));
-  int rc = build_graph(e);
-  if (rc) return rc;
-  const int reps = (max_ev + e->K - 1) / e->K;
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
-  rc = reset_state(e);
+  int rc = reset_state(e);
   if (rc) return rc;
-  KSIM_HIP(hipMemsetAsync(e->d_base, 0, sizeof(int), e->stream));
-  for (int i = 0; i < reps; ++i) KSIM_HIP(hipGraphLaunch(e->graph, e->stream));
+  rc = e->run_mode == 1 ? run_graph(e, max_ev) : run_persistent(e, max_ev);
+  if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev1, e->stream));
   KSIM_HIP(hipStreamSynchronize(e->stream));
   float ms = 0;
   KSIM_HIP(hipEventElapsedTime(&ms, e->ev0, e->ev1));
   e->last_ms = ms;
   e->last_steps = max_ev;
+  if (e->run_mode != 1) {
+    int fail = 0;
+    KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
+    if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
+  }
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica) {
+  if (!e || !wgs_per_replica) return KSIM_EINVAL;
+  *wgs_per_replica = e->run_mode == 1 ? e->bpr : e->last_K;
   return KSIM_OK;
 }
 

@@ -68,7 +68,7 @@ class Result(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("nodes_per_block", C.c_int32), ("steps_per_graph", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("wgs_per_replica", C.c_int32), ("run_mode", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class TraceNode(C.Structure):
@@ -119,6 +119,7 @@ SIGNATURES = {
     "ksim_engine_time_steps": (C.c_int, [_VP, C.c_int, _P(C.c_double)]),
     "ksim_engine_last_run_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
+    "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
     "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
     "ksim_trace_free": (None, [_VP]),
@@ -267,9 +268,11 @@ class Replay:
 class Engine:
     """R independent simulated clusters of N nodes on one MI355X."""
 
-    def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0):
+    def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0, wgs_per_replica=0,
+                 run_mode=0):
+        """run_mode 0: persistent k_replay (default); 1: one k_step launch per pod step (hipGraph)."""
         self.N, self.R = n_nodes, n_replicas
-        cfg = Config(device, nodes_per_block, steps_per_graph, 0)
+        cfg = Config(device, nodes_per_block, steps_per_graph, wgs_per_replica, run_mode)
         h = _VP()
         check(lib().ksim_engine_create(C.byref(cfg), n_nodes, n_replicas, C.byref(h)), "ksim_engine_create")
         self.h = h
@@ -330,6 +333,11 @@ class Engine:
         s = C.c_int64(0)
         check(lib().ksim_engine_last_run_steps(self.h, C.byref(s)), "last_run_steps")
         return s.value
+
+    def last_run_wgs(self):
+        k = C.c_int(0)
+        check(lib().ksim_engine_last_run_wgs(self.h, C.byref(k)), "last_run_wgs")
+        return k.value
 
     def time_steps(self, n_steps):
         us = C.c_double(0)

@@ -25,11 +25,11 @@ def default_trace():
     return ksim.Trace.openb("default")
 
 
-def engine_run(trace, replay, keep, n_ev, policy, seed=0, nodes_per_block=0, typical=None):
+def engine_run(trace, replay, keep, n_ev, policy, seed=0, nodes_per_block=0, typical=None, run_mode=0, wgs=0):
     nodes = helpers.subset_nodes(replay, keep) if keep is not None else replay.nodes
     nn = len(keep) if keep is not None else trace.num_nodes
     arr, n = typical if typical is not None else trace.typical()
-    eng = ksim.Engine(nn, 1, nodes_per_block=nodes_per_block)
+    eng = ksim.Engine(nn, 1, nodes_per_block=nodes_per_block, run_mode=run_mode, wgs_per_replica=wgs)
     eng.set_nodes(0, nodes)
     eng.set_typical(0, arr, n)
     eng.set_policy(0, policy, seed=seed)
@@ -74,11 +74,31 @@ def test_subset_replay_all_policies(default_trace, name, pol, sel):
 
 @pytest.mark.parametrize("nb", [8, 32, 64])
 def test_nodes_per_block_invariance(default_trace, nb):
+    # k_step path (one launch per pod, hipGraph), any workgroup size
     rp = default_trace.replay(seed=5)
     keep = list(range(0, default_trace.num_nodes, 5))
-    res, _ = engine_run(default_trace, rp, keep, 800, "FGD", nodes_per_block=nb)
+    res, _ = engine_run(default_trace, rp, keep, 800, "FGD", nodes_per_block=nb, run_mode=1)
     want, _, _ = oracle_run(default_trace, rp, keep, 800, O.POL_FGD, O.SEL_FGD)
     assert res == want
+
+
+@pytest.mark.parametrize("wgs", [1, 2, 7, 16, 64])
+def test_replay_workgroups_invariance(default_trace, wgs):
+    # k_replay path: the granule all-gather gives the same decisions for any split of the nodes
+    rp = default_trace.replay(seed=6)
+    keep = list(range(0, default_trace.num_nodes, 3))
+    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", wgs=wgs)
+    want, want_state, _ = oracle_run(default_trace, rp, keep, 1500, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, keep)
+
+
+@pytest.mark.parametrize("name,pol,sel", POLICIES, ids=[p[0] for p in POLICIES])
+def test_step_kernel_path_all_policies(default_trace, name, pol, sel):
+    rp = default_trace.replay(seed=8)
+    keep = list(range(2, default_trace.num_nodes, 9))
+    res, state = engine_run(default_trace, rp, keep, 1000, name, seed=5, run_mode=1)
+    want, want_state, _ = oracle_run(default_trace, rp, keep, 1000, pol, sel, seed=5)
+    assert_same(res, want, state, want_state, keep)
 
 
 def test_full_openb_fgd_bit_exact(default_trace):
