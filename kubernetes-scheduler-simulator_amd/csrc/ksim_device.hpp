@@ -428,10 +428,18 @@ KSIM_HD uint64_t rand_node_key(uint64_t seed, int step, uint32_t rank) {
 }
 KSIM_HD uint64_t rand_gpu_key(uint64_t node_key, int g) { return mix64(node_key ^ (uint64_t)(0x100 + g)); }
 
-// Packed argmax key: [63:40] score (24 b) | [39:8] ~name_rank | [7:0] gpu index + 1.
-KSIM_HD unsigned long long pack_key(unsigned score, uint32_t rank, int gpu) {
-  return ((unsigned long long)(score & 0xFFFFFFu) << 40) | ((unsigned long long)(0xFFFFFFFFu - rank) << 8) |
-         (unsigned long long)((gpu + 1) & 0xFF);
+// Packed argmax key: [63:40] score (24 b) | [39:16] ~name_rank (24 b) | [15:12] gpu index + 1 |
+// [11:0] the node's slot in its workgroup slice (k_replay; 0 elsewhere).  Ranks are unique,
+// so max over keys = max score, ties to the byte-wise smallest name (selectHost).
+KSIM_HD unsigned long long pack_key(unsigned score, uint32_t rank, int gpu, int loc = 0) {
+  return ((unsigned long long)(score & 0xFFFFFFu) << 40) | ((unsigned long long)((0xFFFFFFu - rank) & 0xFFFFFFu) << 16) |
+         ((unsigned long long)((gpu + 1) & 0xF) << 12) | (unsigned long long)(loc & 0xFFF);
 }
+KSIM_HD int key_score(unsigned long long k) { return (int)(k >> 40); }
+KSIM_HD uint32_t key_rank(unsigned long long k) { return 0xFFFFFFu - (uint32_t)((k >> 16) & 0xFFFFFFu); }
+KSIM_HD int key_gpu(unsigned long long k) { return (int)((k >> 12) & 0xFu) - 1; }
+KSIM_HD int key_loc(unsigned long long k) { return (int)(k & 0xFFFu); }
+constexpr int kMaxRank = 0xFFFFFF;  // name ranks must stay below (N < 2^24)
+constexpr int kMaxSlice = 0xFFF;    // slots per k_replay workgroup
 
 }  // namespace ksim

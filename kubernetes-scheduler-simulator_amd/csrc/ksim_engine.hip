@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -127,6 +128,20 @@ __device__ int select_gpus(const NodeV& n, const PodDev& p, int gpusel, int fgd_
   }
 }
 
+// Bind on a register image (see apply_bind).
+__device__ __forceinline__ void bind_node(NodeV& n, const PodDev& p, int mask, int sign) {
+  n.cpu_left -= sign * p.cpu_req;
+  n.mem_left -= sign * p.mem;
+  const int pods = n.pods_left() - sign;
+  n.meta = (n.meta & 0xffff0000u) | ((uint32_t)pods & 0xffffu);
+  const uint32_t d = (uint32_t)(sign * (int)p.milli) & 0xffffu;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) {
+    // u16 lanes never borrow across halves: 0 <= left - milli and left + milli <= 1000
+    if ((mask >> g) & 1) n.g[g >> 1] = (g & 1) ? n.g[g >> 1] - (d << 16) : ((n.g[g >> 1] & 0xffff0000u) | ((n.g[g >> 1] - d) & 0xffffu));
+  }
+}
+
 // Bind: scheduler cache assume (Requested += pod), open-gpu-share cache
 // AddOrUpdatePod (devices += milli), NodeInfo.Pods += pod (affinity tags).
 __device__ void apply_bind(NodeRec* nr, uint16_t* tags, const PodDev& p, int mask, int sign) {
@@ -163,6 +178,31 @@ __device__ __forceinline__ unsigned first_of_class(const NodeV& n, int milli) {
 // ---------------------------------------------------------------------------
 // Per-node pieces shared by k_step (one launch per pod) and k_replay (persistent).
 // ---------------------------------------------------------------------------
+
+// Raw score of a feasible node under a non-FGD policy (compile-time policy, used by
+// k_replay); *err on a Score error.  Same functions and semantics as node_phase1.
+template <int kPol>
+__device__ __forceinline__ int cheap_score(const NodeV& n, const PodDev& p, uint64_t seed, const uint16_t* tags,
+                                           int step, bool* err) {
+  *err = false;
+  if constexpr (kPol == POL_BESTFIT) {
+    const int r = bestfit_score(n, p, n.total());
+    if (r < 0) { *err = true; return 0; }
+    return r;
+  } else if constexpr (kPol == POL_DOTPROD) {
+    return dotprod_score(n, p, n.total());
+  } else if constexpr (kPol == POL_PACKING) {
+    bool perr = false;
+    const int r = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
+    *err = perr;
+    return r;
+  } else if constexpr (kPol == POL_CLUSTERING) {
+    if (p.tag == -2) { *err = true; return 0; }
+    return clustering_score(tags, p.tag, n.total());
+  } else {
+    return (int)(rand_node_key(seed, step, n.name_rank) >> 40);
+  }
+}
 
 // Filter, then the cheap scores; for FGD only the candidate count.  `tags` may
 // point at global memory (k_step) or LDS (k_replay).
@@ -280,9 +320,6 @@ __device__ __forceinline__ long long result_score(const ReplicaDev& rp, int nfea
   return (long long)wscore * 1000LL;
 }
 
-__device__ __forceinline__ uint32_t key_rank(unsigned long long key) {
-  return 0xFFFFFFFFu - (uint32_t)((key >> 8) & 0xFFFFFFFFull);
-}
 
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __restrict__ tp_all) {
   const int r = a.rep_first + (int)blockIdx.x / a.bpr;
@@ -413,13 +450,13 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
   if (nfeas > 0) {
     out.status = (nfeas > 1 && anyerr) ? ST_ERROR : ST_OK;  // framework.go:650-656: a Score error aborts
     if (out.status == ST_OK) {
-      out.score = result_score(rp, nfeas, (int)(best >> 40), glo, ghi);
+      out.score = result_score(rp, nfeas, key_score(best), glo, ghi);
       // the rank -> node index map lives right after the replica's tags (see host)
       const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
       const int node = rank2idx[key_rank(best)];
       NodeRec* nr = rp.nodes + node;
       const NodeV wn = load_node(nr);
-      const int mask = select_gpus(wn, p, rp.gpusel, (int)(best & 0xFF) - 1, rp.seed, step);
+      const int mask = select_gpus(wn, p, rp.gpusel, key_gpu(best), rp.seed, step);
       if (mask < 0) {
         out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
         out.score = 0;
@@ -439,207 +476,410 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
 // Dynamic LDS: NodeRec nodes[S] | u16 tags[S][16].
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+template <int kPol>
 __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
                                                                  const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
+  constexpr bool kFgd = kPol == POL_FGD;
+  constexpr bool kMinMax = kPol == POL_BESTFIT;  // NormalizeScore needs the raw min / max
+  constexpr bool kErr = kPol == POL_BESTFIT || kPol == POL_PACKING || kPol == POL_CLUSTERING;
   // all LDS is dynamic (no static __shared__ in front of it), carved 16-byte aligned
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ReplayShared& sh = *reinterpret_cast<ReplayShared*>(smem);
-  int* s_tmp = sh.tmp;
-  uint8_t* s_item_node = sh.item_node;
-  uint8_t* s_item_code = sh.item_code;
-  double* s_F = sh.F;
-  unsigned long long* s_rkey = sh.rkey;
-  int *s_rcnt = sh.rcnt, *s_rerr = sh.rerr, *s_rlo = sh.rlo, *s_rhi = sh.rhi;
-  unsigned long long& s_win = sh.win;
-  int* s_wstat = sh.wstat;
-  int& s_stop = sh.stop;
-  const int r = (int)blockIdx.x / a.K;
+  const int r = a.rep_list[(int)blockIdx.x / a.K];
   const int w = (int)blockIdx.x % a.K;
-  const int tid = (int)threadIdx.x;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const ReplicaDev rp = a.reps[r];
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int n_lo = w * a.S;
   const int ns = max(0, min(a.S, a.N - n_lo));
+  const int S1 = a.S + 1;  // slots incl. the virtual node
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(ReplayShared));
-  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)a.S * sizeof(NodeRec));
-  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
+  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)S1 * sizeof(NodeRec));
+  double* s_F0 = reinterpret_cast<double*>(smem + sizeof(ReplayShared) +
+                                           (size_t)S1 * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t)));
+  // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   int2* hist = a.hist + (size_t)(r * a.K + w) * a.hist_stride;
-  unsigned long long* gr = a.gran + (size_t)r * 2 * a.K * 4;
+  unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * 4;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
   for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
-  if (tid == 0) s_stop = 0;
-  __syncthreads();
+  if (kFgd) {
+    for (int i = tid; i <= ns; i += kRBlock) s_F0[i] = -1.0;  // every cached F stale
+    for (int i = tid; i < rp.nt * 2; i += kRBlock)
+      reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
+  }
+  auto reset_agg = [&]() {
+    sh.agg_key = 0ull;
+    sh.agg_cnt = 0;
+    sh.agg_err = 0;
+    sh.agg_lo = 0x7fffffff;
+    sh.agg_hi = -1;
+  };
+  if (tid == 0) { sh.stop = 0; sh.nitems = 0; sh.pend_valid = 0; sh.pend_b = -1; reset_agg(); }
 
-  const bool fgd = rp.policy == POL_FGD;
+  // wave 0's copy of the pending exchange (the previous pod step, published, not committed)
+  int p_step = 0, p_seq = 0, p_b = -1, p_mask = -1, seq = 0;
+  unsigned long long p_key = 0ull;
+  int p_st0 = 0, p_st1 = 0, p_st2 = 0, p_st3 = 0;  // K == 1: the step's own totals
+
+  // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
+  const bool prof = a.prof != nullptr;
+  if (prof && tid < kProfPhases) sh.prof[tid] = 0ull;
+  unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto mark = [&](int ph) {
+    if (prof && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - t_last;
+      t_last = t;
+    }
+  };
+
+  // Wave 0, lane k < K: workgroup k's granules of the pending exchange (relaxed agent-scope loads).
+  auto poll_once = [&](unsigned long long* g0, unsigned long long* g1, unsigned long long* g2) {
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * 4 + (size_t)lane * 4;
+    if (lane < a.K) {
+      *g0 = gload(slot + 0);
+      *g1 = gload(slot + 1);
+      *g2 = gload(slot + 2);
+    }
+  };
+  // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
+  // this workgroup's own totals (K == 1); g* hold an earlier poll.  Returns the winning key.
+  auto exchange = [&](unsigned long long g0, unsigned long long g1, unsigned long long g2, int* gc, int* ge,
+                      int* gl, int* gh, bool* ok) -> unsigned long long {
+    *ok = true;
+    if (a.K == 1) {
+      *gc = p_st0; *ge = p_st1; *gl = p_st2; *gh = p_st3;
+      return p_key;
+    }
+    const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
+    auto ready = [&]() {
+      return lane >= a.K ||
+             ((g0 & ~0xffffffffull) == tag && (g1 & ~0xffffffffull) == tag && (g2 & ~0xffffffffull) == tag);
+    };
+    unsigned spins = 0;
+    while (!__all(ready())) {
+      if (++spins > kSpinLimit) { *ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+      poll_once(&g0, &g1, &g2);
+    }
+    if (prof && lane == 0) sh.prof[8] += spins;
+    const bool in = lane < a.K;
+    const unsigned st = in ? (unsigned)(g2 & 0xffffffffull) : 0u;
+    const int c = (int)(st & 0x1ffff);
+    *gc = wave_sum_dpp(c);
+    *ge = __any(st >> 31) ? 1 : 0;
+    *gl = 0x7fffffff;
+    *gh = -1;
+    if (kMinMax) {
+      *gl = wave_min_dpp(c > 0 ? (int)((st >> 17) & 0x7f) : 0x7fffffff);
+      *gh = wave_max_dpp(c > 0 ? (int)((st >> 24) & 0x7f) : -1);
+    }
+    return wave_max_u64_dpp(in ? ((g1 & 0xffffffffull) << 32) | (g0 & 0xffffffffull) : 0ull);
+  };
+
+  // Wave 0: commit the pending step -- the owner of the winning node turns the virtual slot
+  // into that node (Reserve + Bind were applied to it when it was prepared).  Lanes 0-6 copy.
+  auto commit = [&](unsigned long long W, int nfeas, int gerr, int glo, int ghi) {
+    const bool owner = W != 0ull && W == p_key;
+    ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+    int2 hrec = make_int2(-1, 0);
+    bool writer = w == 0;
+    if (nfeas > 0) {
+      out.status = (nfeas > 1 && gerr) ? ST_ERROR : ST_OK;
+      if (out.status == ST_OK) {
+        out.score = result_score(rp, nfeas, key_score(W), glo, ghi);
+        writer = owner;  // the owner of the winning node reports
+        hrec.x = -2;
+        if (owner) {
+          if (p_mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+            out.score = 0;
+            hrec.x = -3;
+          } else {
+            if (lane < 2) reinterpret_cast<uint4*>(&s_nodes[p_b])[lane] = reinterpret_cast<const uint4*>(&s_nodes[ns])[lane];
+            else if (lane < 6)
+              reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
+                  reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
+            else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
+            out.node = n_lo + p_b;
+            out.gpu_mask = p_mask;
+            hrec = make_int2(n_lo + p_b, p_mask + 1);
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      hist[p_step] = hrec;
+      if (writer) rp.res[p_step] = out;
+    }
+  };
+
+  // Finish the pending step with nothing to overlap (before a delete / at the end).
+  auto finish_pending = [&]() {
+    if (wv == 0) {
+      unsigned long long g0 = 0, g1 = 0, g2 = 0;
+      if (a.K > 1) poll_once(&g0, &g1, &g2);
+      int gc, ge, gl, gh;
+      bool ok;
+      const unsigned long long W = exchange(g0, g1, g2, &gc, &ge, &gl, &gh, &ok);
+      if (ok) commit(W, gc, ge, gl, gh);
+      if (lane == 0) {
+        if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
+        sh.pend_valid = 0;
+        sh.pend_b = -1;
+      }
+    }
+    __syncthreads();
+  };
+
+  __syncthreads();
   for (int step = 0; step < rp.n_events; ++step) {
-    const PodDev p = rp.ev[step];
+    const int eb = step & (kEvBuf - 1);
+    if (eb == 0) {
+      // refill the LDS event window (every thread passed the previous step's final barrier)
+      const int nl = min(kEvBuf, rp.n_events - step) * 2;
+      const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+      for (int i = tid; i < nl; i += kRBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
+      __syncthreads();
+    }
+    const PodDev p = uniform_pod(&sh.ev[eb]);
+    const int2 pvb = *reinterpret_cast<const int2*>(&sh.pend_valid);
+    const bool pend = __builtin_amdgcn_readfirstlane(pvb.x) != 0;
     if (p.flags & kPodDelete) {
-      // removePod on the owner of the creation (every workgroup recorded the winner)
+      if (pend) finish_pending();
+      if (sh.stop) break;
+      // removePod on the owner of the creation (every workgroup recorded its view of it)
       if (tid == 0) {
         const int2 h = (p.ref >= 0 && p.ref < step) ? hist[p.ref] : make_int2(-1, 0);
-        if (h.x >= 0 && h.y != 0) {
+        if (h.x >= 0) {
           const PodDev cp = rp.ev[p.ref];
           const int loc = h.x - n_lo;
           apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
+          if (kFgd) s_F0[loc] = -1.0;
           rp.res[step] = ResultDev{h.x, h.y - 1, 0, 0, ST_DELETED};
-        } else if (h.x < 0 && w == 0) {
+        } else if ((h.x == -1 && w == 0) || h.x == -3) {
           rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
         }
         hist[step] = make_int2(-1, 0);
       }
       __syncthreads();
+      mark(0);
       continue;
     }
+    mark(0);
+    // ---- Filter + Score of the slice, the pending best node b excluded, plus the virtual node
     const bool share = is_share_pod(p);
-    unsigned long long key = 0ull;
-    int cnt = 0, lo = 0x7fffffff, hi = -1;
-    bool err = false;
-    for (int c0 = 0; c0 < ns; c0 += kChunk) {
-      const int cn = min(kChunk, ns - c0);
-      bool feas = false, e1 = false;
-      int raw = 0, nc = 0, gpu = -1;
-      NodeV n{};
-      if (tid < cn) {
-        n = load_node(&s_nodes[c0 + tid]);
-        feas = node_phase1(n, p, rp, &s_tags[(size_t)(c0 + tid) * kTagStride], step, share, &raw, &nc, &e1);
+    const int vb = pend ? __builtin_amdgcn_readfirstlane(pvb.y) : -1;
+    const int nsv = ns + (vb >= 0 ? 1 : 0);
+    // early poll of the pending exchange by wave 0 (consumed after the evaluation)
+    unsigned long long pg0 = 0, pg1 = 0, pg2 = 0;
+    // one node's packed key into the workgroup aggregate (LDS atomics), or the excluded pair
+    auto route = [&](bool leader, int i, bool feas, bool e1, int raw, unsigned long long k) {
+      const bool excl = leader && (i == vb || i == ns);
+      if (excl) {
+        // the pending best node as it is / as it would be after the pending Bind
+        if (i == ns) { sh.post_key = k; sh.post_feas = feas ? 1 : 0; sh.post_err = (feas && e1) ? 1 : 0; }
+        else { sh.pre_key = k; sh.pre_feas = feas ? 1 : 0; sh.pre_err = (feas && e1) ? 1 : 0; }
       }
-      if (fgd) {
-        int tot = 0;
-        const int off = block_excl_scan(tid < cn ? nc : 0, s_tmp, &tot);
-        if (tid < cn && nc > 0) emit_fgd_items(n, p, share, tid, off, s_item_node, s_item_code);
-        __syncthreads();
-        for (int j = tid; j < tot; j += kRBlock)
-          s_F[j] = eval_fgd_item(load_node(&s_nodes[c0 + s_item_node[j]]), s_item_code[j], p, rp, tp);
-        __syncthreads();
-        if (tid < cn && feas) finalize_fgd(s_F, s_item_code, off, nc, share, &raw, &gpu);
-        __syncthreads();  // s_F / items are reused by the next chunk
-      }
-      if (feas) {
-        const unsigned long long k = pack_key((unsigned)raw, n.name_rank, gpu);
-        key = k > key ? k : key;
-        ++cnt;
-        lo = min(lo, raw);
-        hi = max(hi, raw);
-        err |= e1;
-      }
-    }
-    // workgroup reduction
-    key = wave_max_u64(key);
-    cnt = wave_sum_i(cnt);
-    const int ew = wave_max_i(err ? 1 : 0);
-    lo = wave_min_i(lo);
-    hi = wave_max_i(hi);
-    const int wv = tid >> 6;
-    if ((tid & 63) == 0) { s_rkey[wv] = key; s_rcnt[wv] = cnt; s_rerr[wv] = ew; s_rlo[wv] = lo; s_rhi[wv] = hi; }
-    __syncthreads();
-    if (tid < 64) {
-      if (a.K == 1) {
-        if (tid == 0) {
-          unsigned long long kk = s_rkey[0];
-          int c = s_rcnt[0], e = s_rerr[0], l = s_rlo[0], h = s_rhi[0];
-          for (int i = 1; i < kRBlock / 64; ++i) {
-            kk = s_rkey[i] > kk ? s_rkey[i] : kk;
-            c += s_rcnt[i]; e |= s_rerr[i]; l = min(l, s_rlo[i]); h = max(h, s_rhi[i]);
-          }
-          s_win = kk;
-          s_wstat[0] = c; s_wstat[1] = e; s_wstat[2] = l; s_wstat[3] = h;
+      const bool agg = leader && feas && !excl;
+      const unsigned long long am = __ballot(agg);
+      if (am) {
+        if (agg) {
+          atomicMax(&sh.agg_key, k);
+          if (kMinMax) { atomicMin(&sh.agg_lo, raw); atomicMax(&sh.agg_hi, raw); }
         }
-      } else {
-        unsigned long long* slot = gr + (size_t)(step & 1) * a.K * 4;
-        const unsigned long long tag = (unsigned long long)(unsigned)(step + 1) << 32;
-        if (tid == 0) {
-          unsigned long long kk = s_rkey[0];
-          int c = s_rcnt[0], e = s_rerr[0], l = s_rlo[0], h = s_rhi[0];
-          for (int i = 1; i < kRBlock / 64; ++i) {
-            kk = s_rkey[i] > kk ? s_rkey[i] : kk;
-            c += s_rcnt[i]; e |= s_rerr[i]; l = min(l, s_rlo[i]); h = max(h, s_rhi[i]);
-          }
-          // granules: {tag, key lo32}, {tag, key hi32}, {tag, err|hi|lo|cnt}
-          const unsigned stat = ((unsigned)e << 31) | ((unsigned)(h < 0 ? 0 : h) & 0x7f) << 24 |
-                                ((unsigned)(l > 127 ? 127 : l) & 0x7f) << 17 | ((unsigned)c & 0x1ffff);
-          gstore(slot + (size_t)w * 4 + 0, tag | (kk & 0xffffffffull));
-          gstore(slot + (size_t)w * 4 + 1, tag | (kk >> 32));
-          gstore(slot + (size_t)w * 4 + 2, tag | stat);
+        if (lane == 0) atomicAdd(&sh.agg_cnt, (int)__popcll(am));
+        if (kErr) {
+          if (__any(agg && e1) && lane == 0) atomicOr(&sh.agg_err, 1);
         }
-        // one wave polls every workgroup's granules of this step (lane k <-> workgroup k)
-        unsigned long long g0 = 0, g1 = 0, g2 = 0;
-        bool ok = false;
-        unsigned spins = 0;
-        for (;;) {
-          if (tid < a.K) {
-            g0 = gload(slot + (size_t)tid * 4 + 0);
-            g1 = gload(slot + (size_t)tid * 4 + 1);
-            g2 = gload(slot + (size_t)tid * 4 + 2);
-            ok = (g0 & ~0xffffffffull) == tag && (g1 & ~0xffffffffull) == tag && (g2 & ~0xffffffffull) == tag;
+      }
+    };
+    if constexpr (kFgd) {
+      for (int c0 = 0; c0 < nsv; c0 += kFChunk) {
+        const int cn = min(kFChunk, nsv - c0);
+        const int i = c0 + (tid >> 3), g = tid & 7;
+        const bool valid = (tid >> 3) < cn;
+        NodeV n{};
+        bool feas = false;
+        if (valid) {
+          n = load_node(&s_nodes[i]);
+          feas = filter_node(n, p);
+        }
+        // lane g's candidate: share pod -> GPU g if it fits and no lower GPU has the same milli
+        // left (equal values give the same GPU multiset, hence the same F); else the Sub state
+        bool cand = false;
+        if (feas) {
+          if (share) {
+            const int v = gl_dyn(n, g);
+            cand = g < n.gpu_cnt() && v >= p.milli && (gl_equal_mask(n, v) & ((1u << g) - 1u)) == 0u;
           } else {
-            ok = true;
-          }
-          if (__all(ok)) break;
-          if (++spins > kSpinLimit) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        const bool timed_out = !__all(ok);
-        unsigned long long kk = tid < a.K ? ((g1 & 0xffffffffull) << 32) | (g0 & 0xffffffffull) : 0ull;
-        const unsigned st = tid < a.K ? (unsigned)(g2 & 0xffffffffull) : 0u;
-        int c = (int)(st & 0x1ffff), e = (int)(st >> 31);
-        int l = tid < a.K && c > 0 ? (int)((st >> 17) & 0x7f) : 0x7fffffff;
-        int h = tid < a.K && c > 0 ? (int)((st >> 24) & 0x7f) : -1;
-        kk = wave_max_u64(kk);
-        c = wave_sum_i(c);
-        e = wave_max_i(e);
-        l = wave_min_i(l);
-        h = wave_max_i(h);
-        if (tid == 0) {
-          s_win = kk;
-          s_wstat[0] = c; s_wstat[1] = e; s_wstat[2] = l; s_wstat[3] = h;
-          if (timed_out) {
-            s_stop = 1;
-            atomicOr(a.fail, 1);
+            cand = g == 0;
           }
         }
+        const bool cur = feas && g == 0 && s_F0[i] < 0.0;  // cached F of the current state stale
+        const unsigned long long cm = __ballot(cand), um = __ballot(cur);
+        const int nw = __popcll(cm) + __popcll(um);
+        int base = 0;
+        if (nw > 0) {
+          if (lane == 0) base = atomicAdd(&sh.nitems, nw);
+          base = __builtin_amdgcn_readfirstlane(base);
+        }
+        int my_item = -1;
+        if (cand) {
+          my_item = base + lanes_below(cm);
+          sh.item_node[my_item] = (uint16_t)i;
+          sh.item_code[my_item] = (uint8_t)(share ? 1 + g : 9);
+        }
+        if (cur) {
+          const int o = base + __popcll(cm) + lanes_below(um);
+          sh.item_node[o] = (uint16_t)i;
+          sh.item_code[o] = 0;
+        }
+        __syncthreads();
+        mark(1);
+        const int tot = sh.nitems;
+        const int q = tid & 3;
+        for (int j = tid >> 2; j < tot; j += kRBlock / 4) {  // one quad per item
+          const int loc = sh.item_node[j], code = sh.item_code[j];
+          const NodeV m = load_node(&s_nodes[loc]);
+          int cpuL, total;
+          uint32_t gs[4];
+          fgd_candidate(m, code, p, &cpuL, gs, &total);
+          const uint32_t tb = 1u << m.gpu_type();
+          const double F = rp.typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
+                                    : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          if (q == 0) {
+            if (code == 0) s_F0[loc] = F;
+            else sh.F[j] = F;
+          }
+        }
+        __syncthreads();
+        mark(2);
+        if (pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(&pg0, &pg1, &pg2);
+        if (tid == 0) sh.nitems = 0;  // every thread has read tot; the next writer is past a barrier
+        // fgd_score.go:100-141: every candidate lane scores itself; the node keeps the max,
+        // ties to the lowest GPU index (fgd_score.go:128 keeps the first max)
+        int v = -1;
+        if (cand) v = fgd_frag_score(s_F0[i], sh.F[my_item]) * 16 + (15 - g);
+        v = group8_max(v);
+        // a feasible node with no candidate (share pod with milli 0 on a GPU-less node) scores 0
+        const int raw = v < 0 ? 0 : v >> 4;
+        const int gpu = (share && v >= 0) ? 15 - (v & 15) : -1;
+        const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, gpu, i == ns ? vb : i) : 0ull;
+        route(valid && g == 0, i, feas, false, raw, k);
+        if (c0 + kFChunk < nsv) __syncthreads();  // F / items are reused by the next chunk
+        mark(3);
+      }
+    } else {
+      if (pend && a.K > 1 && wv == 0) poll_once(&pg0, &pg1, &pg2);
+      for (int c0 = 0; c0 < nsv; c0 += kChunk) {
+        const int cn = min(kChunk, nsv - c0);
+        const int i = c0 + tid;
+        bool feas = false, e1 = false;
+        int raw = 0;
+        NodeV n{};
+        if (tid < cn) {
+          n = load_node(&s_nodes[i]);
+          feas = filter_node(n, p);
+          if (feas) raw = cheap_score<kPol>(n, p, rp.seed, &s_tags[(size_t)i * kTagStride], step, &e1);
+        }
+        const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, -1, i == ns ? vb : i) : 0ull;
+        route(tid < cn, i, feas, e1, raw, k);
       }
     }
     __syncthreads();
-    if (s_stop) break;
-    if (tid == 0) {
-      const unsigned long long best = s_win;
-      const int nfeas = s_wstat[0];
-      ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
-      int2 hrec = make_int2(-1, 0);
-      bool writer = w == 0;
-      if (nfeas > 0) {
-        out.status = (nfeas > 1 && s_wstat[1]) ? ST_ERROR : ST_OK;
-        if (out.status == ST_OK) {
-          const int node = rank2idx[key_rank(best)];
-          hrec.x = node;
-          out.score = result_score(rp, nfeas, (int)(best >> 40), s_wstat[2], s_wstat[3]);
-          if (node >= n_lo && node < n_lo + ns) {
-            // this workgroup owns the winner: Reserve's GPU selector + Bind on the LDS record
-            writer = true;
-            const int loc = node - n_lo;
-            const NodeV wn = load_node(&s_nodes[loc]);
-            const int mask = select_gpus(wn, p, rp.gpusel, (int)(best & 0xFF) - 1, rp.seed, step);
-            if (mask < 0) {
-              out.status = ST_ERROR;
-              out.score = 0;
-            } else {
-              apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], p, mask, +1);
-              out.node = node;
-              out.gpu_mask = mask;
-              hrec.y = mask + 1;
+    mark(4);
+    if (wv == 0) {
+      // the slice's aggregate without b (LDS atomics above), then b's two versions
+      unsigned long long mk = sh.agg_key;
+      int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
+      const unsigned long long k_pre = sh.pre_key, k_post = sh.post_key;
+      const int f_pre = sh.pre_feas, f_post = sh.post_feas, e_pre = sh.pre_err, e_post = sh.post_err;
+      // finish the pending exchange (its latency overlapped the evaluation above)
+      bool owner = false, ok = true;
+      unsigned long long W = 0ull;
+      int gc = 0, ge = 0, gl = 0, gh = 0;
+      if (pend) {
+        W = exchange(pg0, pg1, pg2, &gc, &ge, &gl, &gh, &ok);
+        owner = W != 0ull && W == p_key;
+      }
+      mark(5);
+      // add b back: post-Bind if this workgroup owned the pending winner, else as it was
+      if (vb >= 0 && (owner ? f_post : f_pre)) {
+        const unsigned long long vk = owner ? k_post : k_pre;
+        mk = vk > mk ? vk : mk;
+        ++c;
+        e |= owner ? e_post : e_pre;
+        if (kMinMax) { l = min(l, key_score(vk)); h = max(h, key_score(vk)); }
+      }
+      if (ok) {
+        if (lane == 0) {
+          // publish this step first: granules {tag, key lo32}, {tag, key hi32}, {tag, err|hi|lo|cnt}
+          if (a.K > 1) {
+            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * 4;
+            const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
+            const unsigned stat = ((unsigned)e << 31) | ((unsigned)(h < 0 ? 0 : h) & 0x7f) << 24 |
+                                  ((unsigned)(l > 127 ? 127 : l) & 0x7f) << 17 | ((unsigned)c & 0x1ffff);
+            gstore(slot + (size_t)w * 4 + 0, tag | (mk & 0xffffffffull));
+            gstore(slot + (size_t)w * 4 + 1, tag | (mk >> 32));
+            gstore(slot + (size_t)w * 4 + 2, tag | stat);
+          }
+          reset_agg();
+        }
+        if (pend) commit(W, gc, ge, gl, gh);
+        // prepare the virtual node: this step's best node with this step's Reserve + Bind applied
+        const int mloc = key_loc(mk);
+        int mask = -1;
+        if (mk != 0ull) {
+          NodeV bn = load_node(&s_nodes[mloc]);
+          mask = select_gpus(bn, p, rp.gpusel, key_gpu(mk), rp.seed, step);
+          if (mask >= 0) bind_node(bn, p, mask, +1);
+          if (lane == 0) store_node(&s_nodes[ns], bn);
+          else if (lane >= 2 && lane < 6) {
+            uint2 t = reinterpret_cast<const uint2*>(&s_tags[(size_t)mloc * kTagStride])[lane - 2];
+            if (mask >= 0 && p.tag >= 0 && (p.tag >> 2) == lane - 2) {
+              // +1 on u16 tag p.tag (counts stay far below 2^16, no carry across halves)
+              const uint32_t inc = 1u << (16 * (p.tag & 1));
+              t.x += (p.tag & 2) ? 0u : inc;
+              t.y += (p.tag & 2) ? inc : 0u;
             }
-          } else {
-            writer = false;  // the owner reports
+            reinterpret_cast<uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2] = t;
+          } else if (lane == 6 && kFgd) {
+            s_F0[ns] = mask >= 0 ? -1.0 : s_F0[mloc];
           }
         }
+        p_step = step;
+        p_seq = seq;
+        p_b = mk != 0ull ? mloc : -1;
+        p_key = mk;
+        p_mask = mask;
+        p_st0 = c; p_st1 = e; p_st2 = l; p_st3 = h;
+        ++seq;
+        if (lane == 0) { sh.pend_valid = 1; sh.pend_b = p_b; }
+      } else if (lane == 0) {
+        sh.stop = 1;
+        atomicOr(a.fail, 1);
       }
-      hist[step] = hrec;
-      if (writer) rp.res[step] = out;
     }
+    mark(6);
     __syncthreads();
+    mark(7);
+    if (sh.stop) break;
   }
+  if (!sh.stop && __builtin_amdgcn_readfirstlane(sh.pend_valid)) finish_pending();
+  if (prof && tid == 0) {
+    sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
+    sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;
+  }
+  __syncthreads();
+  if (prof && tid < kProfPhases) a.prof[(size_t)blockIdx.x * kProfPhases + tid] = sh.prof[tid];
   // write the slice back (final cluster state)
   for (int i = tid; i < ns; i += kRBlock) store_node(rp.nodes + n_lo + i, load_node(&s_nodes[i]));
   for (int i = tid; i < ns * kTagStride; i += kRBlock) rp.tags[(size_t)n_lo * kTagStride + i] = s_tags[i];
@@ -728,6 +968,10 @@ struct ksim_engine {
   int2* d_hist = nullptr;
   size_t hist_cap = 0;
   int* d_fail = nullptr;
+  int* d_replist = nullptr;              // replicas ordered by policy (k_replay groups)
+  int last_groups = 0;
+  unsigned long long* d_prof = nullptr;  // KSIM_PROFILE=1: k_replay phase timers
+  size_t prof_cap = 0;
   int last_K = 0;
   hipStream_t stream = nullptr;
   NodeRec* d_nodes = nullptr;
@@ -772,6 +1016,12 @@ static int upload_reps(ksim_engine* e) {
   return KSIM_OK;
 }
 
+template <int P>
+static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp) {
+  (void)hipFuncSetAttribute((const void*)k_replay<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_replay<P>, dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+}
+
 extern "C" {
 
 const char* ksim_strerror(int code) {
@@ -803,6 +1053,7 @@ int ksim_device_count(void) {
 int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim_engine** out) {
   if (!out || n_nodes <= 0 || n_replicas <= 0) return KSIM_EINVAL;
   *out = nullptr;
+  if (n_nodes > kMaxRank) return KSIM_ERANGE;  // name ranks are 24-bit fields of the argmax key
   const int dev = cfg ? cfg->device : 0;
   int rc = check_gfx950(dev);
   if (rc) return rc;
@@ -844,6 +1095,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_gpu, sizeof(int32_t) * n_nodes));
   KSIM_HIP(hipMalloc(&e->d_gran, sizeof(unsigned long long) * (size_t)n_replicas * 2 * ksim_replay::kMaxK * 4));
   KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
+  KSIM_HIP(hipMalloc(&e->d_replist, sizeof(int) * (size_t)n_replicas));
   KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
   std::vector<Accum> acc(n_replicas);
   for (auto& a : acc) {
@@ -883,7 +1135,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (auto p : e->d_ev) (void)hipFree(p);
   for (auto p : e->d_res) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
-                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail};
+                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -1156,53 +1408,123 @@ static int build_graph(ksim_engine* e) {
   return KSIM_OK;
 }
 
-// Workgroups per replica for k_replay: every workgroup of a replica must be
+// KSIM_PROFILE=1: per-phase k_replay time (us per step, mean and max over workgroups) on stderr.
+static void print_replay_profile(ksim_engine* e, int R, int K, int steps) {
+  const int nb = R * K, P = ksim_replay::kProfPhases;
+  std::vector<unsigned long long> h((size_t)nb * P);
+  if (hipMemcpy(h.data(), e->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+  static const char* names[] = {"pod", "filter(+emit)", "fgd-eval", "fgd-final", "agg-sync", "poll", "commit+publish", "end-sync"};
+  std::fprintf(stderr, "ksim profile: %d workgroups (K=%d), %d steps, us/step mean [max]:", nb, K, steps);
+  for (int ph = 0; ph < 8; ++ph) {
+    double sum = 0, mx = 0;
+    for (int b = 0; b < nb; ++b) {
+      const double us = (double)h[(size_t)b * P + ph] / 100.0 / steps;  // 100 MHz ticks
+      sum += us;
+      mx = std::max(mx, us);
+    }
+    std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / nb, mx);
+  }
+  double spins = 0;
+  for (int b = 0; b < nb; ++b) spins += (double)h[(size_t)b * P + 8];
+  std::fprintf(stderr, " poll spins/step %.2f", spins / nb / steps);
+  double cyc = 0, tick = 0;
+  for (int b = 0; b < nb; ++b) { cyc += (double)h[(size_t)b * P + 10]; tick += (double)h[(size_t)b * P + 11]; }
+  if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz", cyc / tick * 100.0);
+  std::fprintf(stderr, "\n");
+}
+
+// Workgroups per replica for k_replay: every workgroup of a launch must be
 // co-resident (they exchange granules every step), so R*K never exceeds one
 // workgroup per CU; K = 1 needs no co-residency at all.
-static int choose_wgs(const ksim_engine* e) {
-  int K = e->wgs_req > 0 ? e->wgs_req : e->cus / e->R;
+static int choose_wgs(const ksim_engine* e, int R) {
+  int K = e->wgs_req > 0 ? e->wgs_req : e->cus / R;
   K = std::max(1, std::min(K, ksim_replay::kMaxK));
   K = std::min(K, e->N);
-  if (e->R * K > e->cus) K = 1;
+  if (R * K > e->cus) K = 1;
   return K;
 }
 
-static size_t replay_lds(int S) {
-  return sizeof(ksim_replay::ReplayShared) + (size_t)S * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t));
+static size_t replay_lds(int S) {  // S real slots + the virtual node
+  return sizeof(ksim_replay::ReplayShared) +
+         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double));
 }
 
+// One k_replay launch per policy present (the kernel is specialised on the policy);
+// launches of different policies run back to back on the engine stream.
 static int run_persistent(ksim_engine* e, int max_ev) {
-  int K = choose_wgs(e);
-  int S = (e->N + K - 1) / K;
-  while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && e->R * (K + 1) <= e->cus) {
-    ++K;
-    S = (e->N + K - 1) / K;
+  std::vector<int> order;
+  std::vector<std::pair<int, int>> groups;  // (policy, count) in `order`
+  for (int pol = POL_FGD; pol <= POL_RANDOM; ++pol) {
+    int c = 0;
+    for (int r = 0; r < e->R; ++r)
+      if (e->reps[r].policy == pol) { order.push_back(r); ++c; }
+    if (c) groups.push_back({pol, c});
   }
-  if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
-  const size_t need = (size_t)e->R * K * std::max(max_ev, 1);
-  if (need > e->hist_cap) {
-    if (e->d_hist) KSIM_HIP(hipFree(e->d_hist));
-    KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
-    e->hist_cap = need;
-  }
-  const size_t lds = replay_lds(S);
-  KSIM_HIP(hipFuncSetAttribute((const void*)k_replay, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  ksim_replay::ReplayArgs ra;
-  ra.reps = e->d_reps;
-  ra.N = e->N;
-  ra.K = K;
-  ra.S = S;
-  ra.gran = e->d_gran;
-  ra.hist = e->d_hist;
-  ra.hist_stride = std::max(max_ev, 1);
-  ra.fail = e->d_fail;
-  // re-initialise every polled word before the launch (granule tags restart at step 1)
-  KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
-                          e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_replist, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
-  hipLaunchKernelGGL(k_replay, dim3(e->R * K), dim3(ksim_replay::kRBlock), lds, e->stream, ra, (const TypDev*)e->d_tp);
-  KSIM_HIP(hipGetLastError());
-  e->last_K = K;
+  const char* pe = std::getenv("KSIM_PROFILE");
+  const bool profile = pe && pe[0] == '1';
+  int first = 0;
+  for (const auto& gp : groups) {
+    const int Rg = gp.second;
+    int K = choose_wgs(e, Rg);
+    int S = (e->N + K - 1) / K;
+    while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && Rg * (K + 1) <= e->cus) {
+      ++K;
+      S = (e->N + K - 1) / K;
+    }
+    if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
+    const size_t need = (size_t)e->R * K * std::max(max_ev, 1);
+    if (need > e->hist_cap) {
+      if (e->d_hist) KSIM_HIP(hipFree(e->d_hist));
+      KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
+      e->hist_cap = need;
+    }
+    const size_t lds = replay_lds(S);
+    ksim_replay::ReplayArgs ra;
+    ra.reps = e->d_reps;
+    ra.rep_list = e->d_replist + first;
+    ra.N = e->N;
+    ra.K = K;
+    ra.S = S;
+    ra.gran = e->d_gran;
+    ra.hist = e->d_hist;
+    ra.hist_stride = std::max(max_ev, 1);
+    ra.fail = e->d_fail;
+    ra.prof = nullptr;
+    if (profile) {
+      const size_t words = (size_t)Rg * K * ksim_replay::kProfPhases;
+      if (words > e->prof_cap) {
+        if (e->d_prof) KSIM_HIP(hipFree(e->d_prof));
+        KSIM_HIP(hipMalloc(&e->d_prof, sizeof(unsigned long long) * words));
+        e->prof_cap = words;
+      }
+      KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * words, e->stream));
+      ra.prof = e->d_prof;
+    }
+    // re-initialise every polled word before the launch (granule tags restart at step 1)
+    KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
+                            e->stream));
+    const int grid = Rg * K;
+    const TypDev* tp = e->d_tp;
+    switch (gp.first) {
+      case POL_FGD: launch_replay<POL_FGD>(grid, lds, e->stream, ra, tp); break;
+      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, e->stream, ra, tp); break;
+      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, e->stream, ra, tp); break;
+      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, e->stream, ra, tp); break;
+      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, e->stream, ra, tp); break;
+      default: launch_replay<POL_RANDOM>(grid, lds, e->stream, ra, tp); break;
+    }
+    KSIM_HIP(hipGetLastError());
+    e->last_K = K;
+    e->last_groups = (int)groups.size();
+    first += Rg;
+    if (profile) {
+      // phase timers of this group (the stream is in order; read back before the next group reuses them)
+      KSIM_HIP(hipStreamSynchronize(e->stream));
+      print_replay_profile(e, Rg, K, max_ev);
+    }
+  }
   return KSIM_OK;
 }
 

@@ -1,10 +1,26 @@
 // ksim_replay.hpp -- persistent whole-trace replay kernel (k_replay).
 //
-// One launch replays every replica to completion.  Replica r is owned by K
+// One launch replays every replica to completion (1024-thread workgroups).  Replica r is owned by K
 // co-resident workgroups; workgroup w keeps the node records of its slice
 // [w*S, min(N,(w+1)*S)) in LDS for the whole run, so the per-pod loop touches
 // no node record in HBM.  Per pod step:
-//   1. Filter + Score of the slice (the k_step phases, on LDS records);
+// Pipelining: a Bind changes ONE node, and the only node of a slice that can win a
+// step is the slice's own best.  So right after publishing step s a workgroup
+// evaluates pod s+1 on its slice with its step-s best node b excluded from the
+// aggregate, evaluating b twice: as it is (pre) and in the virtual slot with step
+// s's Bind applied (post).  When step s's exchange completes it commits (owner ->
+// the virtual slot becomes b) and combines the aggregate with post (owner) or pre
+// (everyone else) -- the exchange latency overlaps the next step's Filter+Score.
+// Per pod step:
+//   1. Filter + Score of the slice on LDS records.  FGD: eight lanes per node,
+//      lane g owning GPU g -- Filter, the candidate placements (one per distinct
+//      milli-left value among the fitting GPUs) and the final sigmoid scores are
+//      per-lane; the work list is compacted with ballot + mbcnt.  F of the node's current
+//      state is cached per node in LDS (it does not depend on the pod; a Bind or a
+//      delete invalidates it), and every candidate state is evaluated by a QUAD of
+//      lanes -- lane q classifies typical pod tb+q, then the quad folds the four
+//      (bin, value) pairs in typical-pod order with lane q owning bin q, so every
+//      bin stays the reference's sequential fp64 sum;
 //   2. the workgroup publishes its best packed key and its counters as three
 //      8-byte {tag = step+1, value} granules (agent-scope relaxed stores);
 //   3. one wave polls the replica's 3K granules (agent-scope relaxed loads)
@@ -23,38 +39,53 @@ namespace ksim_replay {
 
 using namespace ksim;
 
-constexpr int kRBlock = 256;
-constexpr int kChunk = 128;        // nodes per evaluation chunk
-constexpr int kRMaxCand = 9;
+constexpr int kRBlock = 1024;
+constexpr int kRWaves = kRBlock / 64;
+constexpr int kChunk = kRBlock;      // nodes per chunk, one lane per node (non-FGD policies)
+constexpr int kFChunk = kRBlock / 8; // nodes per chunk, 8 lanes per node -- lane g <-> GPU g (FGD)
+constexpr int kRMaxCand = 9;         // FGD items per node: stale current state + up to 8 candidates
 constexpr int kMaxK = 64;          // workgroups per replica
 constexpr int kGran = 3;           // granules per workgroup per step
 constexpr unsigned kSpinLimit = 1u << 22;  // ~seconds: only a non-resident workgroup can stall a poll
+constexpr int kEvBuf = 128;        // events staged in LDS per refill (4 KB)
 
 struct ReplayArgs {
   ReplicaDev* reps;
+  const int* rep_list;  // replica of each group of K workgroups (one policy per launch)
   int N;
   int K;            // workgroups per replica
   int S;            // slice size (nodes per workgroup)
-  unsigned long long* gran;  // [R][2][K][4]
+  unsigned long long* gran;  // [launch replica][2][K][4]
   int2* hist;       // [R][K][hist_stride]: (node, mask+1) of pods this workgroup bound
   int hist_stride;
   int* fail;
+  unsigned long long* prof;  // optional [R*K][8] s_memrealtime phase sums (KSIM_PROFILE=1), else null
 };
+constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 
-// Small per-workgroup state at the start of the dynamic LDS region (16-B aligned);
-// NodeRec nodes[S] and u16 tags[S][16] follow it.
+// Per-workgroup state at the start of the dynamic LDS region (16-B aligned).  After it:
+// NodeRec nodes[S+1], u16 tags[S+1][16], double F0[S+1] (cached F of the current state,
+// < 0 = stale).  Slot ns (one past the slice) is the VIRTUAL node: the pending step's
+// local best node with that step's Bind already applied (see the pipelining note).
 struct __align__(16) ReplayShared {
-  unsigned long long rkey[kRBlock / 64];
-  unsigned long long win;
-  int rcnt[kRBlock / 64], rerr[kRBlock / 64], rlo[kRBlock / 64], rhi[kRBlock / 64];
-  int wstat[4];
-  int tmp[kRBlock / 64];
+  PodDev ev[kEvBuf];
+  TypDev tp[kMaxTypical];  // the replica's typical table (per-lane reads in the quad evaluator)
+  // the step's local aggregate (LDS atomics), the pending best node b and the virtual node excluded
+  unsigned long long agg_key;
+  int agg_cnt, agg_err, agg_lo, agg_hi;
+  // the excluded real node (pre-Bind) and the virtual node (post-Bind) of the current step
+  unsigned long long pre_key, post_key;
+  int pre_feas, pre_err, post_feas, post_err;
+  // the pending exchange as the other waves need it (wave 0 keeps the rest in registers)
+  int pend_valid, pend_b;
   int stop;
+  int nitems;                   // FGD work-list length of the current chunk
   int pad0[3];
-  int off[kChunk + 4];
-  double F[kChunk * kRMaxCand];
-  uint8_t item_node[kChunk * kRMaxCand];
-  uint8_t item_code[kChunk * kRMaxCand];
+  unsigned long long prof[kProfPhases];  // KSIM_PROFILE phase sums (thread 0)
+  unsigned long long prof_pad[4];
+  double F[kFChunk * kRMaxCand];
+  uint16_t item_node[kFChunk * kRMaxCand];
+  uint8_t item_code[kFChunk * kRMaxCand];
 };
 static_assert(sizeof(ReplayShared) % 16 == 0, "keep the node records 16-B aligned");
 
@@ -65,7 +96,209 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Workgroup-wide exclusive scan of one int per thread (256 threads), total in *tot.
+// ---- wave reductions over all 64 lanes with DPP row ops + 4 readlanes (call with every lane active) ----
+template <int kCtrl>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const int lo = dpp_i<kCtrl>((int)(unsigned)v), hi = dpp_i<kCtrl>((int)(unsigned)(v >> 32));
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror: every lane of a
+// 16-lane row ends with the row's reduction; the four rows are then combined uniformly.
+__device__ __forceinline__ unsigned long long wave_max_u64_dpp(unsigned long long v) {
+  unsigned long long w;
+  w = dpp_u64<0xB1>(v); v = w > v ? w : v;
+  w = dpp_u64<0x4E>(v); v = w > v ? w : v;
+  w = dpp_u64<0x141>(v); v = w > v ? w : v;
+  w = dpp_u64<0x140>(v); v = w > v ? w : v;
+  const unsigned long long a = readlane_u64(v, 0), b = readlane_u64(v, 16), c = readlane_u64(v, 32),
+                           d = readlane_u64(v, 48);
+  const unsigned long long x = a > b ? a : b, y = c > d ? c : d;
+  return x > y ? x : y;
+}
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+  v += dpp_i<0xB1>(v);
+  v += dpp_i<0x4E>(v);
+  v += dpp_i<0x141>(v);
+  v += dpp_i<0x140>(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ int wave_min_dpp(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  v = min(v, dpp_i<0x140>(v));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ int wave_max_dpp(int v) {
+  v = max(v, dpp_i<0xB1>(v));
+  v = max(v, dpp_i<0x4E>(v));
+  v = max(v, dpp_i<0x141>(v));
+  v = max(v, dpp_i<0x140>(v));
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+// Max over each group of 8 lanes (8k .. 8k+7): xor 1, xor 2, then row_half_mirror.
+__device__ __forceinline__ int group8_max(int v) {
+  v = max(v, dpp_i<0xB1>(v));
+  v = max(v, dpp_i<0x4E>(v));
+  v = max(v, dpp_i<0x141>(v));
+  return v;
+}
+
+// milli left on GPU g (0..7, lane-varying) without dynamic register indexing.
+__device__ __forceinline__ int gl_dyn(const NodeV& n, int g) {
+  const uint32_t w01 = (g & 2) ? n.g[1] : n.g[0];
+  const uint32_t w23 = (g & 2) ? n.g[3] : n.g[2];
+  const uint32_t w = (g & 4) ? w23 : w01;
+  return (int)((g & 1) ? (w >> 16) : (w & 0xffffu));
+}
+
+// Bit h set iff GPU h has exactly v milli left.
+__device__ __forceinline__ unsigned gl_equal_mask(const NodeV& n, int v) {
+  const uint32_t vv = (uint32_t)v * 0x10001u;
+  unsigned m = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = n.g[i] ^ vv;
+    m |= ((x & 0xffffu) == 0u ? 1u : 0u) << (2 * i);
+    m |= ((x >> 16) == 0u ? 1u : 0u) << (2 * i + 1);
+  }
+  return m;
+}
+
+// An LDS-staged event as wave-uniform values (readfirstlane keeps it in SGPRs).
+__device__ __forceinline__ PodDev uniform_pod(const PodDev* s) {
+  const uint4* q = reinterpret_cast<const uint4*>(s);
+  uint4 x = q[0], y = q[1];
+  x.x = __builtin_amdgcn_readfirstlane(x.x); x.y = __builtin_amdgcn_readfirstlane(x.y);
+  x.z = __builtin_amdgcn_readfirstlane(x.z); x.w = __builtin_amdgcn_readfirstlane(x.w);
+  y.x = __builtin_amdgcn_readfirstlane(y.x); y.y = __builtin_amdgcn_readfirstlane(y.y);
+  y.z = __builtin_amdgcn_readfirstlane(y.z); y.w = __builtin_amdgcn_readfirstlane(y.w);
+  PodDev p;
+  uint4* o = reinterpret_cast<uint4*>(&p);
+  o[0] = x;
+  o[1] = y;
+  return p;
+}
+
+// ---- quad (4-lane) broadcasts: every lane of a quad gets lane J's value ----
+template <int J>
+__device__ __forceinline__ int qbc(int v) {
+  return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xF, 0xF, true);
+}
+template <int J>
+__device__ __forceinline__ double qbc_d(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)qbc<J>((int)(unsigned)u), hi = (unsigned)qbc<J>((int)(unsigned)(u >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Candidate state of `code` on node m: 0 current, 1..8 share pod on GPU code-1
+// (fgd_score.go:111-118), 9 NodeResource.Sub (fgd_score.go:137-141, resource.go:454-480).
+// g: packed u16 milli-left per GPU; *total: GetGpuMilliLeftTotal of the state.
+__device__ __forceinline__ void fgd_candidate(const NodeV& m, int code, const PodDev& p, int* cpuL,
+                                              uint32_t (&g)[4], int* total) {
+  *cpuL = m.cpu_left;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = m.g[i];
+  unsigned mask = 0u;
+  if (code >= 1 && code <= 8) {
+    mask = 1u << (code - 1);
+  } else if (code == 9) {
+    int gl[kMaxGpu];
+    unpack_gl(m, gl);
+    bool ok = false;
+    mask = sub_gpu_mask(gl, m.gpu_cnt(), *cpuL, p, &ok);
+    if (!ok) mask = 0u;
+    if (ok) *cpuL -= p.cpu_nz;
+  }
+  if (code >= 1 && code <= 8) *cpuL -= p.cpu_nz;
+  const uint32_t d = (uint32_t)(uint16_t)p.milli;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)  // u16 lanes never borrow: a selected GPU has left >= milli
+    g[i] -= (((mask >> (2 * i)) & 1u) ? d : 0u) + (((mask >> (2 * i + 1)) & 1u) ? (d << 16) : 0u);
+  uint32_t t = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, g[i]), (u16x2){1, 1}, t, false);
+  *total = (int)t;
+}
+
+// F = NodeGpuShareFragAmountScore of one state (frag.go:148-203, 411-418, 460-493),
+// evaluated by the 4 lanes of a quad (q = lane & 3); every lane returns the same F.
+//   CPU-only typical pods [0, ncpu): scalar table loads; lane 0 folds XL, lane 1 XR.
+//   GPU typical pods [ncpu, nt): lane q classifies t = tb+q from the LDS table --
+//     cnt / frag over the 8 packed GPUs with v_pk_sub_i16 + v_pk_lshrrev_b16 +
+//     v_dot2_u32_u16 -- into (bin, value); the quad then folds t = tb..tb+3 in order
+//     and lane q keeps bin q (0 = Q1, 1 = Q2 + Q3's frag part, 2 = Q4, 3 = NA).
+// Every bin is the same sequence of fp64 adds as frag_F's (adding +0.0 for the
+// typical pods that do not touch it), so F is bit-identical.
+template <bool kTyped>
+__device__ __forceinline__ double frag_F_quad(int cpuL, const uint32_t (&g)[4], int total, uint32_t typebit,
+                                              const TypDev* __restrict__ tp, const TypDev* ltp, int ncpu, int nt,
+                                              int q) {
+  const double dtot = (double)total;
+  double bc = 0.0;
+  for (int t = 0; t < ncpu; ++t) {
+    const double x = tp[t].freq * dtot;  // freq * float64(gpuMilliLeftTotal)
+    const bool cpu_ok = cpuL >= tp[t].cpu;
+    bc += (cpu_ok == (q == 0)) ? x : 0.0;
+  }
+  double bg = 0.0;
+  TypDev en = ltp[min(ncpu + q, nt - 1)];
+  for (int tb = ncpu; tb < nt; tb += 4) {
+    const TypDev e = en;
+    en = ltp[min(tb + 4 + q, nt - 1)];  // prefetch the next round's entry
+    const uint32_t mp = (uint32_t)e.milli * 0x10001u;
+    uint32_t frag = 0u, nlt = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
+      const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
+      frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+      nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
+    }
+    const bool gpu_ok = kMaxGpu - (int)nlt >= e.num_eff;  // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+    const bool cpu_ok = cpuL >= e.cpu;
+    const bool acc = !kTyped || (e.tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+    const double x = e.freq * dtot;
+    const double y = e.freq * (double)(int)frag;           // freq * float64(gpuFragMilli)
+    int code = acc ? (cpu_ok ? 1 : (gpu_ok ? 2 : 0)) : 3;
+    code = tb + q < nt ? code : 4;
+    const double v = (acc && cpu_ok && gpu_ok) ? y : x;
+    double vj;
+    int cj;
+    cj = qbc<0>(code); vj = qbc_d<0>(v); bg += (cj == q) ? vj : 0.0;
+    cj = qbc<1>(code); vj = qbc_d<1>(v); bg += (cj == q) ? vj : 0.0;
+    cj = qbc<2>(code); vj = qbc_d<2>(v); bg += (cj == q) ? vj : 0.0;
+    cj = qbc<3>(code); vj = qbc_d<3>(v); bg += (cj == q) ? vj : 0.0;
+  }
+  const double b0 = qbc_d<0>(bg), b1 = qbc_d<1>(bg), b3 = qbc_d<2>(bg), b6 = qbc_d<3>(bg);
+  const double b4 = qbc_d<0>(bc), b5 = qbc_d<1>(bc);
+  double out = 0.0;
+  out += b0;
+  out += b1;
+  out += b3;
+  out += b4;
+  out += b5;
+  out += b6;
+  return out;
+}
+
+// Workgroup-wide exclusive scan of one int per thread (kRBlock threads), total in *tot.
 __device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* tot) {
   const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
   int incl = v;
@@ -78,7 +311,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* tot) {
   __syncthreads();
   int base = 0, t = 0;
 #pragma unroll
-  for (int i = 0; i < kRBlock / 64; ++i) {
+  for (int i = 0; i < kRWaves; ++i) {
     base += i < w ? s_tmp[i] : 0;
     t += s_tmp[i];
   }
