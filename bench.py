@@ -8,8 +8,13 @@ fixed (rank k replays seeds 42+10k .. 51+10k): weak scaling, replicas only, no
 collective on the data path.
 
 One JSON line on rank 0.  Extra keys: node_evals_per_s, roofline (dominant
-kernel k_step, HBM-bound by SURVEY §8(d)'s 32 B per node-evaluation), and
-cpu_baseline (the C oracle -- a restatement of the Go path -- on the host cores).
+kernel k_replay -- one persistent launch replays every replica -- priced against
+HBM with SURVEY §8(d)'s 32 B per node-evaluation + 56 B per pod), and cpu_baseline
+(the C oracle -- a restatement of the Go path -- on the host cores).
+
+Multi-GPU (torchrun, one rank per GPU): each rank replays its own seeds on its own
+GPU; the only collectives are the timing barrier and the job reduction (max time,
+summed events) -- see seeds_for_rank / reduce_job, tested with gloo on CPU.
 """
 import argparse
 import json
@@ -25,6 +30,9 @@ import ksim  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
+# HBM bytes per k_replay launch of this default workload from the PMC passes of
+# scripts/profile_round.sh (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "round_end", "pmc.json")
 
 
 def cpu_baseline(trace, seed, threads):
@@ -45,6 +53,23 @@ def cpu_baseline(trace, seed, threads):
                 sample="openb default, seed %d, full replay (%d events x %d nodes), FGD, %d worker threads "
                        "(parallelize.Until fan-out); host nproc=%d" % (seed, len(ev), trace.num_nodes, threads,
                                                                         os.cpu_count()))
+
+
+def seeds_for_rank(rank, replicas, base=42):
+    """C2 seeds of one rank: rank k replays base + replicas*k .. base + replicas*(k+1) - 1."""
+    return [base + replicas * rank + i for i in range(replicas)]
+
+
+def reduce_job(dt, events, dist=None, device="cpu"):
+    """Whole-job time (max over ranks) and events (sum over ranks)."""
+    if dist is None:
+        return dt, events
+    import torch
+    t = torch.tensor([dt], device=device, dtype=torch.float64)
+    n = torch.tensor([events], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(n.item())
 
 
 def main():
@@ -76,7 +101,7 @@ def main():
         torch.cuda.set_device(0)
 
     trace = ksim.Trace.openb("default")
-    seeds = [42 + args.replicas * rank + i for i in range(args.replicas)]
+    seeds = seeds_for_rank(rank, args.replicas)
     eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode)
     total_events = eng.total_events
 
@@ -95,10 +120,7 @@ def main():
         dev_ms += eng.run()
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt, job_events = reduce_job(dt, total_events * args.steps, dist, "cuda")
 
     steps_per_run = eng.last_run_steps()
     # roofline: the dominant kernel is k_replay, one launch per replay of all replicas; its duration is
@@ -107,8 +129,14 @@ def main():
     bytes_per_launch = total_events * (BYTES_PER_NODE_EVAL * trace.num_nodes + BYTES_PER_POD)
     achieved = bytes_per_launch / (kern_us * 1e-6) / 1e9
 
-    pods_total = total_events * args.steps * world
-    value = pods_total / dt
+    value = job_events / dt
+    traffic, traffic_src = None, None
+    default_cfg = (args.policy == "FGD" and args.replicas == 10 and args.run_mode == 0 and args.wgs == 0)
+    if default_cfg and os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("hbm_bytes_per_dispatch")
+        traffic_src = os.path.relpath(PMC_FILE, ROOT)
     line = {
         "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
         "value": value,
@@ -129,7 +157,7 @@ def main():
         "node_evals_per_s": value * trace.num_nodes,
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_replay", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
                      "wgs_per_replica": eng.last_run_wgs()},
     }

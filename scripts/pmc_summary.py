@@ -1,0 +1,45 @@
+"""Summarise a profile_round.sh run: k_replay duration (kernel trace) and HBM bytes per
+k_replay dispatch from the FETCH_SIZE / WRITE_SIZE passes.  FETCH_SIZE is doubled
+(MI355X_MICROARCH.md, HBM section: on gfx950 it reports half the bytes of wide
+coalesced reads); WRITE_SIZE is taken as is.  FETCH/WRITE_SIZE are in KiB."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def main(d):
+    kt = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_trace.csv")) if "k_replay" in r.get("Kernel_Name", "")]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt]
+
+    def counter(sub, name):
+        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
+                if "k_replay" in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+        return vals
+
+    fetch = counter("fetch", "FETCH_SIZE")
+    write = counter("write", "WRITE_SIZE")
+    res = {
+        "kernel": "k_replay",
+        "dispatches": len(durs),
+        "mean_duration_ns": sum(durs) / len(durs) if durs else None,
+        "fetch_kib_per_dispatch_raw": (sum(fetch) / len(fetch)) if fetch else None,
+        "write_kib_per_dispatch": (sum(write) / len(write)) if write else None,
+    }
+    if fetch and write:
+        res["hbm_bytes_per_dispatch"] = (2 * res["fetch_kib_per_dispatch_raw"] + res["write_kib_per_dispatch"]) * 1024
+        res["note"] = "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, mean over dispatches"
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
