@@ -127,7 +127,24 @@ struct ReplicaDev {
   ResultDev* res;
   NodeRec* nodes;
   uint16_t* tags;  // [N][16]
+  // cluster report (null when disabled): the state a Bind / delete left on the node it changed,
+  // the previous event that changed the same node (-1: none since the run started), the
+  // per-event exact report, the static allocatable CPU per node and the run's initial state
+  NodeRec* snap;         // [E]
+  int32_t* prev;         // [E]
+  struct RepAcc* rep;    // [E]
+  const int32_t* cap;    // [N] MilliCpuCapacity (utils.go:1101)
+  const NodeRec* init;   // [N]
+  int32_t* last;         // [N] k_step: last event that changed each node
 };
+
+// Per-event cluster report, exact (fixed point 2^-80 for the fp64 bins; see fix80).
+// cnt: used nodes, used GPUs, used GPU milli, used CPU milli, arrived GPU milli, arrived CPU milli.
+struct __align__(16) RepAcc {
+  __int128 bins[7];
+  long long cnt[6];
+};
+static_assert(sizeof(RepAcc) == 160, "RepAcc layout");
 
 // Per-replica cross-workgroup accumulators for one step (reset by the last block).
 struct __align__(64) Accum {
@@ -248,6 +265,63 @@ KSIM_HD double frag_F(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, cons
   out += b5;
   out += b6;
   return out;
+}
+
+// NodeGpuShareFragAmount (frag.go:148-188): all 7 bins of one node state (Q1, Q2, Q3, Q4, XL,
+// XR, NA; frag.go:27-35), the per-node term of the cluster report (analysis.go:81-85).  Every
+// bin is a sequential fp64 sum in typical-pod order: the table split of TypDev keeps the
+// order of each bin, since CPU-only pods only touch XL/XR and GPU pods only Q1-Q4/NA.
+KSIM_HD void frag_bins7(int cpuL, const int (&gl)[kMaxGpu], uint32_t typebit, const TypDev* __restrict__ tp,
+                        int ncpu, int nt, double (&b)[7]) {
+  int total = 0;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) total += gl[g];  // GetGpuMilliLeftTotal (frag.go:224-229)
+  const double dtot = (double)total;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) b[k] = 0.0;
+  for (int t = 0; t < ncpu; ++t) {  // GetNodePodFrag case 1 (frag.go:463-469)
+    const double x = tp[t].freq * dtot;
+    if (cpuL >= tp[t].cpu) b[4] += x;
+    else b[5] += x;
+  }
+  for (int t = ncpu; t < nt; ++t) {
+    const double f = tp[t].freq;
+    const int m = tp[t].milli;
+    int cnt = 0, frag = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      cnt += gl[g] >= m ? 1 : 0;   // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+      frag += gl[g] < m ? gl[g] : 0;  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+    }
+    const bool cpu_ok = cpuL >= tp[t].cpu;
+    const bool gpu_ok = cnt >= tp[t].num_eff;
+    if ((tp[t].tmask & typebit) == 0u) {
+      b[6] += f * dtot;                      // NA (frag.go:472-474)
+    } else if (gpu_ok && cpu_ok) {           // Q3: frag part to Q2, the rest to Q3 (frag.go:174-181)
+      b[1] += f * (double)frag;
+      b[2] += f * (double)(total - frag);
+    } else if (gpu_ok) {
+      b[3] += f * dtot;                      // Q4
+    } else if (cpu_ok) {
+      b[1] += f * dtot;                      // Q2
+    } else {
+      b[0] += f * dtot;                      // Q1
+    }
+  }
+}
+
+// Exact fixed-point image of a non-negative fp64 value: x * 2^80 as a 128-bit integer
+// (truncated below 2^-80).  Cluster sums of these are exact and order independent, so the
+// report's cluster bins are the correctly rounded exact sum of the per-node fp64 bins
+// (DESIGN.md "Cluster report"); the reference sums them in Go map order (analysis.go:80-98).
+KSIM_HD __int128 fix80(double x) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const int ex = (int)((b >> 52) & 0x7ff);
+  if (ex == 0) return 0;  // zero / subnormal (< 2^-1022): far below 2^-80
+  const unsigned long long m = (b & ((1ull << 52) - 1)) | (1ull << 52);
+  const int sh = ex - 1075 + 80;  // x = m * 2^(ex-1075)
+  __int128 v = sh >= 0 ? ((__int128)m << sh) : (sh > -64 ? (__int128)(m >> (-sh)) : (__int128)0);
+  return (b >> 63) ? -v : v;
 }
 
 KSIM_HD void unpack_gl(const NodeV& n, int (&gl)[kMaxGpu]) {

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -158,6 +159,14 @@ __device__ void apply_bind(NodeRec* nr, uint16_t* tags, const PodDev& p, int mas
   }
   store_node(nr, n);
   if (p.tag >= 0) tags[p.tag] = (uint16_t)((int)tags[p.tag] + sign);
+}
+
+// Cluster report bookkeeping of k_step: the state event `step` left on `node` and the previous
+// event that changed it (k_replay keeps the same per-node record in LDS).
+__device__ __forceinline__ void note_change(const ReplicaDev& rp, int node, int step) {
+  store_node(rp.snap + step, load_node(rp.nodes + node));
+  rp.prev[step] = rp.last[node];
+  rp.last[node] = step;
 }
 
 // Bit g set iff GPU g fits `milli` and no lower-index fitting GPU has the same milli left.
@@ -341,6 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
         if (c.node >= 0) {
           const PodDev cp = rp.ev[p.ref];
           apply_bind(rp.nodes + c.node, rp.tags + (size_t)c.node * kTagStride, cp, c.gpu_mask, -1);
+          if (rp.snap && !a.pod_override) note_change(rp, c.node, step);
           out.node = c.node;
           out.gpu_mask = c.gpu_mask;
         }
@@ -462,6 +472,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
         out.score = 0;
       } else {
         apply_bind(nr, rp.tags + (size_t)node * kTagStride, p, mask, +1);
+        if (rp.snap && !a.pod_override) note_change(rp, node, step);
         out.node = node;
         out.gpu_mask = mask;
       }
@@ -471,10 +482,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
 }
 
 #include "ksim_replay.hpp"
+#include "ksim_report.hpp"
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
-// Dynamic LDS: NodeRec nodes[S] | u16 tags[S][16].
+// Dynamic LDS: ReplayShared | NodeRec nodes[S+1] | u16 tags[S+1][16] | f64 F0[S+1] | i32 last[S+1].
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -502,12 +514,15 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)S1 * sizeof(NodeRec));
   double* s_F0 = reinterpret_cast<double*>(smem + sizeof(ReplayShared) +
                                            (size_t)S1 * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t)));
+  // cluster report: the last event that changed each slot (-1: none yet)
+  int* s_last = reinterpret_cast<int*>(s_F0 + S1);
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   int2* hist = a.hist + (size_t)(r * a.K + w) * a.hist_stride;
   unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * 4;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
   for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
+  for (int i = tid; i <= ns; i += kRBlock) s_last[i] = -1;
   if (kFgd) {
     for (int i = tid; i <= ns; i += kRBlock) s_F0[i] = -1.0;  // every cached F stale
     for (int i = tid; i < rp.nt * 2; i += kRBlock)
@@ -608,6 +623,11 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
               reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
                   reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
+            else if (lane == 7 && rp.snap) {  // cluster report: the post-Bind record (the virtual slot)
+              store_node(rp.snap + p_step, load_node(&s_nodes[ns]));
+              rp.prev[p_step] = s_last[p_b];
+              s_last[p_b] = p_step;
+            }
             out.node = n_lo + p_b;
             out.gpu_mask = p_mask;
             hrec = make_int2(n_lo + p_b, p_mask + 1);
@@ -663,6 +683,11 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
           const int loc = h.x - n_lo;
           apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
+          if (rp.snap) {
+            store_node(rp.snap + step, load_node(&s_nodes[loc]));
+            rp.prev[step] = s_last[loc];
+            s_last[loc] = step;
+          }
           rp.res[step] = ResultDev{h.x, h.y - 1, 0, 0, ST_DELETED};
         } else if ((h.x == -1 && w == 0) || h.x == -3) {
           rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
@@ -997,8 +1022,16 @@ struct ksim_engine {
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
   int graph_R = -1;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double last_ms = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+  double last_ms = 0, last_report_ms = 0;
+  // cluster report (ksim_engine_set_report)
+  bool report = false;
+  int32_t* d_cap = nullptr;   // [R][N] allocatable milli-CPU
+  int32_t* d_last = nullptr;  // [R][N] k_step: last event that changed each node
+  std::vector<NodeRec*> d_snap;
+  std::vector<int32_t*> d_prev;
+  std::vector<RepAcc*> d_rep;
+  std::vector<int64_t> total_gpus;
   int64_t last_steps = 0;
 };
 
@@ -1010,6 +1043,8 @@ static int check_gfx950(int dev) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KSIM_ENODEV;
   return KSIM_OK;
 }
+
+static int alloc_report(ksim_engine* e, int r);
 
 static int upload_reps(ksim_engine* e) {
   KSIM_HIP(hipMemcpyAsync(e->d_reps, e->reps.data(), sizeof(ReplicaDev) * e->R, hipMemcpyHostToDevice, e->stream));
@@ -1096,6 +1131,9 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_gran, sizeof(unsigned long long) * (size_t)n_replicas * 2 * ksim_replay::kMaxK * 4));
   KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
   KSIM_HIP(hipMalloc(&e->d_replist, sizeof(int) * (size_t)n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_cap, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_last, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMemset(e->d_cap, 0, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
   std::vector<Accum> acc(n_replicas);
   for (auto& a : acc) {
@@ -1110,6 +1148,10 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
   e->nt.assign(n_replicas, 0);
+  e->d_snap.assign(n_replicas, nullptr);
+  e->d_prev.assign(n_replicas, nullptr);
+  e->d_rep.assign(n_replicas, nullptr);
+  e->total_gpus.assign(n_replicas, 0);
   for (int r = 0; r < n_replicas; ++r) {
     ReplicaDev& rp = e->reps[r];
     std::memset(&rp, 0, sizeof rp);
@@ -1118,9 +1160,13 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     rp.tp = e->d_tp + (size_t)r * kMaxTypical;
     rp.nodes = e->d_nodes + (size_t)r * n_nodes;
     rp.tags = e->d_tags + (size_t)r * e->tags_stride;
+    rp.cap = e->d_cap + (size_t)r * n_nodes;
+    rp.init = e->d_nodes_init + (size_t)r * n_nodes;
+    rp.last = e->d_last + (size_t)r * n_nodes;
   }
   KSIM_HIP(hipEventCreate(&e->ev0));
   KSIM_HIP(hipEventCreate(&e->ev1));
+  KSIM_HIP(hipEventCreate(&e->ev_mid));
   rc = upload_reps(e);
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
@@ -1134,11 +1180,16 @@ void ksim_engine_destroy(ksim_engine* e) {
   if (e->graph) (void)hipGraphExecDestroy(e->graph);
   for (auto p : e->d_ev) (void)hipFree(p);
   for (auto p : e->d_res) (void)hipFree(p);
+  for (auto p : e->d_snap) (void)hipFree(p);
+  for (auto p : e->d_prev) (void)hipFree(p);
+  for (auto p : e->d_rep) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
-                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist};
+                  e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
+                  e->d_cap, e->d_last};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1168,6 +1219,8 @@ static int to_pod_dev(const ksim_pod& s, PodDev* d) {
 int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
   if (!e || !nodes || replica < 0 || replica >= e->R) return KSIM_EINVAL;
   std::vector<NodeRec> h(e->N);
+  std::vector<int32_t> cap(e->N);
+  int64_t gpus = 0;
   std::vector<uint16_t> tags(e->tags_stride, 0);
   int* rank2idx = reinterpret_cast<int*>(tags.data() + (size_t)e->N * kTagStride);
   std::vector<char> seen(e->N, 0);
@@ -1176,6 +1229,9 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     if (s.gpu_count < 0 || s.gpu_count > kMaxGpu || s.gpu_type < 0 || s.gpu_type >= KSIM_MAX_TYPES)
       return KSIM_ERANGE;
     if (s.name_rank >= (uint32_t)e->N || seen[s.name_rank]) return KSIM_EINVAL;
+    if (s.cpu_alloc_milli < 0 || s.cpu_alloc_milli > 0x3fffffff) return KSIM_ERANGE;
+    cap[i] = (int32_t)s.cpu_alloc_milli;
+    gpus += s.gpu_count;
     seen[s.name_rank] = 1;
     const int64_t cpu_left = s.cpu_alloc_milli - s.cpu_used_milli;
     const int64_t mem_left = s.mem_alloc_mib - s.mem_used_mib;
@@ -1200,7 +1256,10 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     rank2idx[s.name_rank] = i;
   }
   e->h_nodes[replica].assign(nodes, nodes + e->N);
+  e->total_gpus[replica] = gpus;
   KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(e->d_cap + (size_t)replica * e->N, cap.data(), sizeof(int32_t) * e->N, hipMemcpyHostToDevice,
+                          e->stream));
   KSIM_HIP(hipMemcpyAsync(e->reps[replica].nodes, h.data(), sizeof(NodeRec) * e->N, hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemcpyAsync(e->d_tags + (size_t)replica * e->tags_stride, tags.data(), sizeof(uint16_t) * e->tags_stride,
                           hipMemcpyHostToDevice, e->stream));
@@ -1373,7 +1432,9 @@ int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events,
   e->reps[replica].ev = e->d_ev[replica];
   e->reps[replica].res = e->d_res[replica];
   e->reps[replica].n_events = n;
-  int rc = upload_reps(e);
+  int rc = alloc_report(e, replica);
+  if (rc) return rc;
+  rc = upload_reps(e);
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
   return KSIM_OK;
@@ -1385,6 +1446,39 @@ static int reset_state(ksim_engine* e) {
                           e->stream));
   KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride * e->R, hipMemcpyDeviceToDevice,
                           e->stream));
+  return KSIM_OK;
+}
+
+// Per-event report buffers of one replica (allocated while the report is enabled).
+static int alloc_report(ksim_engine* e, int r) {
+  ReplicaDev& rp = e->reps[r];
+  if (e->d_snap[r]) { KSIM_HIP(hipFree(e->d_snap[r])); e->d_snap[r] = nullptr; }
+  if (e->d_prev[r]) { KSIM_HIP(hipFree(e->d_prev[r])); e->d_prev[r] = nullptr; }
+  if (e->d_rep[r]) { KSIM_HIP(hipFree(e->d_rep[r])); e->d_rep[r] = nullptr; }
+  rp.snap = nullptr;
+  rp.prev = nullptr;
+  rp.rep = nullptr;
+  if (!e->report || !e->d_ev[r]) return KSIM_OK;
+  const size_t ne = (size_t)std::max(e->n_events[r], 1);
+  KSIM_HIP(hipMalloc(&e->d_snap[r], sizeof(NodeRec) * ne));
+  KSIM_HIP(hipMalloc(&e->d_prev[r], sizeof(int32_t) * ne));
+  KSIM_HIP(hipMalloc(&e->d_rep[r], sizeof(RepAcc) * ne));
+  rp.snap = e->d_snap[r];
+  rp.prev = e->d_prev[r];
+  rp.rep = e->d_rep[r];
+  return KSIM_OK;
+}
+
+// The per-event cluster report of every replica from the run's snapshots (ksim_report.hpp).
+static int run_report(ksim_engine* e, int max_ev) {
+  if (max_ev <= 0) return KSIM_OK;
+  const dim3 grid((unsigned)((max_ev + ksim_rep::kDeltaBlock - 1) / ksim_rep::kDeltaBlock), (unsigned)e->R);
+  hipLaunchKernelGGL(ksim_rep::k_report_delta, grid, dim3(ksim_rep::kDeltaBlock), 0, e->stream,
+                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ksim_rep::k_report_scan, dim3(e->R), dim3(ksim_rep::kScanBlock), 0, e->stream,
+                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N);
+  KSIM_HIP(hipGetLastError());
   return KSIM_OK;
 }
 
@@ -1446,7 +1540,7 @@ static int choose_wgs(const ksim_engine* e, int R) {
 
 static size_t replay_lds(int S) {  // S real slots + the virtual node
   return sizeof(ksim_replay::ReplayShared) +
-         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double));
+         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double) + sizeof(int));
 }
 
 // One k_replay launch per policy present (the kernel is specialised on the policy);
@@ -1548,19 +1642,71 @@ int ksim_engine_run(ksim_engine* e) {
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
   int rc = reset_state(e);
   if (rc) return rc;
+  if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N * e->R, e->stream));
   rc = e->run_mode == 1 ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
+  KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
+  if (e->report) {
+    rc = run_report(e, max_ev);
+    if (rc) return rc;
+  }
   KSIM_HIP(hipEventRecord(e->ev1, e->stream));
   KSIM_HIP(hipStreamSynchronize(e->stream));
-  float ms = 0;
+  float ms = 0, rms = 0;
   KSIM_HIP(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  KSIM_HIP(hipEventElapsedTime(&rms, e->ev_mid, e->ev1));
   e->last_ms = ms;
+  e->last_report_ms = e->report ? rms : 0.0;
   e->last_steps = max_ev;
   if (e->run_mode != 1) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
     if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
   }
+  return KSIM_OK;
+}
+
+int ksim_engine_set_report(ksim_engine* e, int enable) {
+  if (!e) return KSIM_EINVAL;
+  e->report = enable != 0;
+  KSIM_HIP(hipSetDevice(e->device));
+  for (int r = 0; r < e->R; ++r) {
+    int rc = alloc_report(e, r);
+    if (rc) return rc;
+  }
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int n) {
+  if (!e || !out || replica < 0 || replica >= e->R || n < 0 || n > e->n_events[replica]) return KSIM_EINVAL;
+  if (!e->report || !e->d_rep[replica]) return KSIM_ESTATE;
+  if (n == 0) return KSIM_OK;
+  std::vector<RepAcc> h((size_t)n);
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(h.data(), e->d_rep[replica], sizeof(RepAcc) * n, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  for (int i = 0; i < n; ++i) {
+    ksim_report& o = out[i];
+    // exact fixed-point sum -> nearest double (the int128 -> double conversion rounds to nearest
+    // even; the 2^-80 scaling is exact)
+    for (int k = 0; k < 7; ++k) o.frag_bins[k] = std::ldexp((double)h[i].bins[k], -80);
+    o.used_nodes = h[i].cnt[0];
+    o.used_gpus = h[i].cnt[1];
+    o.used_gpu_milli = h[i].cnt[2];
+    o.total_gpus = e->total_gpus[replica];
+    o.arrived_gpu_milli = h[i].cnt[4];
+    o.used_cpu_milli = h[i].cnt[3];
+    o.arrived_cpu_milli = h[i].cnt[5];
+  }
+  return KSIM_OK;
+}
+
+int ksim_engine_last_report_ms(ksim_engine* e, double* ms) {
+  if (!e || !ms) return KSIM_EINVAL;
+  *ms = e->last_report_ms;
   return KSIM_OK;
 }
 

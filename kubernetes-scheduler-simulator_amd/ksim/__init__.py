@@ -66,6 +66,12 @@ class Result(C.Structure):
                 ("status", C.c_int32)]
 
 
+class Report(C.Structure):
+    _fields_ = [("frag_bins", C.c_double * 7), ("used_nodes", C.c_int64), ("used_gpus", C.c_int64),
+                ("used_gpu_milli", C.c_int64), ("total_gpus", C.c_int64), ("arrived_gpu_milli", C.c_int64),
+                ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64)]
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("nodes_per_block", C.c_int32), ("steps_per_graph", C.c_int32),
                 ("wgs_per_replica", C.c_int32), ("run_mode", C.c_int32), ("reserved", C.c_int32 * 3)]
@@ -92,6 +98,7 @@ class ReplayCfg(C.Structure):
 
 
 assert C.sizeof(Node) == 128 and C.sizeof(Pod) == 48 and C.sizeof(Typical) == 32 and C.sizeof(Result) == 24
+assert C.sizeof(Report) == 112
 
 _LIB = None
 
@@ -120,6 +127,9 @@ SIGNATURES = {
     "ksim_engine_last_run_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
     "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
+    "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
+    "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
+    "ksim_engine_last_report_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
     "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
     "ksim_trace_free": (None, [_VP]),
@@ -327,6 +337,25 @@ class Engine:
         check(lib().ksim_engine_run(self.h), "run")
         ms = C.c_double(0)
         check(lib().ksim_engine_last_run_ms(self.h, C.byref(ms)), "last_run_ms")
+        return ms.value
+
+    def set_report(self, enable=True):
+        """Per-event cluster report (analysis.go:59-119) computed on the device by run()."""
+        check(lib().ksim_engine_set_report(self.h, 1 if enable else 0), "set_report")
+
+    def reports(self, r):
+        """The report after every event of replica r: list of dicts (ksim_report fields)."""
+        n = self.n_events[r]
+        out = (Report * max(1, n))()
+        check(lib().ksim_engine_get_reports(self.h, r, out, n), "get_reports")
+        return [dict(frag_bins=list(out[i].frag_bins), used_nodes=out[i].used_nodes, used_gpus=out[i].used_gpus,
+                     used_gpu_milli=out[i].used_gpu_milli, total_gpus=out[i].total_gpus,
+                     arrived_gpu_milli=out[i].arrived_gpu_milli, used_cpu_milli=out[i].used_cpu_milli,
+                     arrived_cpu_milli=out[i].arrived_cpu_milli) for i in range(n)]
+
+    def last_report_ms(self):
+        ms = C.c_double(0)
+        check(lib().ksim_engine_last_report_ms(self.h, C.byref(ms)), "last_report_ms")
         return ms.value
 
     def last_run_steps(self):

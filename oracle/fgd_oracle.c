@@ -666,6 +666,21 @@ static void* work_fn(void* arg) {
     return NULL;
 }
 
+/* Exact accumulation for the cluster report: x * 2^80 as a 128-bit integer (x >= 0, finite),
+ * via frexp/ldexp.  The reference sums the per-node bins in Go map order, which is not
+ * reproducible (client-go/testing/fixture.go:201); the exact sum rounded once is order free and
+ * within a few ulps of any ordered sum of these non-negative terms. */
+static __int128 orc_fix80(double x) {
+    if (x == 0.0) return 0;
+    int ex = 0;
+    double m = frexp(x, &ex);                 /* x = m * 2^ex, 0.5 <= |m| < 1 */
+    int64_t mant = (int64_t)ldexp(m, 53);     /* exact: 53 significant bits */
+    int sh = ex - 53 + 80;
+    if (sh >= 0) return (__int128)mant << sh;
+    if (sh <= -64) return 0;
+    return (__int128)(mant >> (-sh));
+}
+
 static const orc_node_spec* g_sort_nodes;
 static int cmp_name_idx(const void* a, const void* b) {
     int i = *(const int*)a, j = *(const int*)b;
@@ -835,12 +850,16 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
             /* analysis.go:59-119 ClusterGpuFragReport (node order: input order) */
             orc_report* P = &rep[s];
             memset(P, 0, sizeof *P);
+            __int128 ex[ORC_NBINS] = {0};
             for (int i = 0; i < n_nodes; i++) {
                 orc_node_resource nr;
                 node_res_of(&nodes[i], &dyn[i], &nr);
                 double b[ORC_NBINS];
                 orc_node_gpu_share_frag_amount(&nr, tp, nt, b);
-                for (int k = 0; k < ORC_NBINS; k++) P->frag_bins[k] += 1.0 * b[k];
+                for (int k = 0; k < ORC_NBINS; k++) {
+                    P->frag_bins[k] += 1.0 * b[k];
+                    ex[k] += orc_fix80(b[k]);
+                }
                 P->total_gpus += nr.gpu_number;
                 int ff = 0;
                 for (int g = 0; g < nr.n_gpu_left; g++)
@@ -852,6 +871,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                     P->used_cpu_milli += nr.milli_cpu_capacity - nr.milli_cpu_left;
                 }
             }
+            for (int k = 0; k < ORC_NBINS; k++) P->frag_bins_exact[k] = ldexp((double)ex[k], -80);
             P->arrived_gpu_milli = arrived_gpu;
             P->arrived_cpu_milli = arrived_cpu;
         }

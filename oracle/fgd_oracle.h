@@ -162,6 +162,8 @@ typedef struct {
     double  frag_bins[ORC_NBINS];  /* cluster sum of NodeGpuShareFragAmount (analysis.go:81-85) */
     int64_t used_nodes, used_gpus, used_gpu_milli, total_gpus, arrived_gpu_milli;
     int64_t used_cpu_milli, arrived_cpu_milli;
+    double  frag_bins_exact[ORC_NBINS]; /* the same sums, exact, rounded once to nearest (see
+                                           orc_fix80 in fgd_oracle.c; the product's contract) */
 } orc_report;
 
 typedef struct {

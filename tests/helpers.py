@@ -48,3 +48,29 @@ def subset_nodes(replay, keep):
         C.memmove(C.byref(sub[j]), C.byref(replay.nodes[i]), C.sizeof(ksim.Node))
         sub[j].name_rank = rank_of[j]
     return sub
+
+
+def delete_stream(trace, replay, n_create, p_delete=0.3, seed=0):
+    """A create/delete event stream (simulator.go:416-422): after each creation, with probability
+    p_delete, a deletion of a random live earlier creation.  Returns (engine events, oracle events)."""
+    import ctypes as C
+    import random
+    rnd = random.Random(seed)
+    evs, oev, live = [], [], []
+    base = oracle_events(trace, replay, n_create)
+    for k in range(n_create):
+        e = ksim.Pod()
+        C.memmove(C.byref(e), C.byref(replay.events[k]), C.sizeof(ksim.Pod))
+        evs.append(e)
+        oev.append(dict(base[k]))
+        live.append(len(evs) - 1)
+        if rnd.random() < p_delete and live:
+            ref = live.pop(rnd.randrange(len(live)))
+            d = ksim.Pod()
+            C.memmove(C.byref(d), C.byref(evs[ref]), C.sizeof(ksim.Pod))
+            d.is_delete, d.ref = 1, ref
+            evs.append(d)
+            od = dict(oev[ref])
+            od.update(delete=1, ref=ref)
+            oev.append(od)
+    return (ksim.Pod * len(evs))(*evs), oev

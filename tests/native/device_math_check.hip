@@ -50,6 +50,26 @@ double dm_frag_F(int cpu_left, const int* gl8, int type_id, int T, const int* tp
   return F_of(cpu_left, gl, 1u << type_id, tp, ncpu, nt, typed);
 }
 
+// all 7 NodeGpuShareFragAmount bins (the report's per-node term)
+void dm_frag_bins7(int cpu_left, const int* gl8, int type_id, int T, const int* tpi4, const double* tpf, double* out7) {
+  static TypDev tp[kMaxTypical];
+  int ncpu = 0;
+  bool typed = false;
+  const int nt = split_table(T, tpi4, tpf, tp, &ncpu, &typed);
+  int gl[kMaxGpu];
+  for (int g = 0; g < kMaxGpu; ++g) gl[g] = gl8[g];
+  double b[7];
+  frag_bins7(cpu_left, gl, 1u << type_id, tp, ncpu, nt, b);
+  for (int k = 0; k < 7; ++k) out7[k] = b[k];
+}
+
+// fix80 as two 64-bit halves (lo, hi)
+void dm_fix80(double x, unsigned long long* lo, long long* hi) {
+  const __int128 v = fix80(x);
+  *lo = (unsigned long long)v;
+  *hi = (long long)(v >> 64);
+}
+
 static NodeV mk(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left) {
   NodeV n;
   std::memset(&n, 0, sizeof n);

@@ -36,6 +36,9 @@ def dm():
     L.dm_packing.argtypes = [I8, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
     L.dm_clustering.argtypes = [C.c_int * 9, I8, C.c_int, C.c_int, C.c_int]
     L.dm_exclusive.argtypes = [I8, C.c_int, C.c_int, C.c_int]
+    L.dm_frag_bins7.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                C.c_double * 7]
+    L.dm_fix80.argtypes = [C.c_double, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
     return L
 
 
@@ -134,3 +137,32 @@ def test_cheap_scores_and_exclusive_fuzz(dm):
         tag = -1 if num == 0 else (0 if (num == 1 and milli < 1000) else num)
         want = L.orc_clustering_score(C.byref(node), C.byref(pr), tag, (C.c_int32 * 9)(*tags))
         assert dm.dm_clustering((C.c_int * 9)(*tags), g8, cnt, milli, num) == want
+
+
+def test_frag_bins7_fuzz(dm, tables):
+    # the report's per-node term: every NodeGpuShareFragAmount bin bit-identical to the oracle
+    rnd = random.Random(4)
+    for tlist in tables:
+        tpi, tpf = table(tlist)
+        otp = O.typical(tlist)
+        for _ in range(1500):
+            cnt = rnd.choice([1, 2, 4, 8])
+            gl = rand_gl(rnd, cnt)
+            cpu_left = rnd.choice([0, 500, 2000, 8000, 32000, 64000, 96000])
+            ty = rnd.randrange(len(TYPES))
+            out = (C.c_double * 7)()
+            dm.dm_frag_bins7(cpu_left, (C.c_int * 8)(*gl), ty, len(tlist), tpi, tpf, out)
+            assert list(out) == O.frag_bins(O.node_res(cpu_left, gl[:cnt], cnt, TYPES[ty], 96000), otp)
+
+
+def test_fix80_exact_scaling(dm):
+    # x * 2^80 as an integer, exactly, for report-sized values (and truncation below 2^-80)
+    from fractions import Fraction
+    rnd = random.Random(5)
+    vals = [0.0, 1.0, 0.5, 2.0 ** -80, 2.0 ** -81, 1e-30, 123456.789, 8e8, 2.0 ** 45]
+    vals += [rnd.uniform(0, 1e6) for _ in range(2000)] + [rnd.random() * 10 ** rnd.randint(-20, 8) for _ in range(2000)]
+    for x in vals:
+        lo, hi = C.c_uint64(0), C.c_int64(0)
+        dm.dm_fix80(x, C.byref(lo), C.byref(hi))
+        got = (hi.value << 64) | lo.value
+        assert got == int(Fraction(x) * 2 ** 80), x

@@ -3,9 +3,6 @@
 Bar: bit-exact (node, GPU set, score, feasible count, status) for every event,
 and identical final cluster state.  Every test here needs a gfx950 device.
 """
-import ctypes as C
-import random
-
 import numpy as np
 import pytest
 
@@ -149,25 +146,8 @@ def test_deletion_events(default_trace):
     # creation + deletion events (simulator.go:416-422): removePod restores the node
     rp = default_trace.replay(seed=9)
     keep = list(range(0, default_trace.num_nodes, 9))
-    rnd = random.Random(0)
-    evs, oev, live = [], [], []
-    base = helpers.oracle_events(default_trace, rp, 900)
-    for k in range(900):
-        e = ksim.Pod()
-        C.memmove(C.byref(e), C.byref(rp.events[k]), C.sizeof(ksim.Pod))
-        evs.append(e)
-        oev.append(dict(base[k]))
-        live.append(len(evs) - 1)
-        if rnd.random() < 0.3 and live:
-            ref = live.pop(rnd.randrange(len(live)))
-            d = ksim.Pod()
-            C.memmove(C.byref(d), C.byref(evs[ref]), C.sizeof(ksim.Pod))
-            d.is_delete, d.ref = 1, ref
-            evs.append(d)
-            od = dict(oev[ref])
-            od.update(delete=1, ref=ref)
-            oev.append(od)
-    arr_ev = (ksim.Pod * len(evs))(*evs)
+    arr_ev, oev = helpers.delete_stream(default_trace, rp, 900, 0.3, seed=0)
+    evs = arr_ev
     arr, n = default_trace.typical()
     eng = ksim.Engine(len(keep), 1)
     eng.set_nodes(0, helpers.subset_nodes(rp, keep))

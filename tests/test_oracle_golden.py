@@ -120,3 +120,28 @@ def test_typical_pods_threshold_and_renorm():
     wl2 = [(1000, 0, 0, "")] * 10 + [(3000, 0, 0, "")] * 10
     tp2 = O.get_typical_pods(wl2, threshold=100, step=1)
     assert [x[0] for x in tp2] == [3000, 1000]
+
+
+def test_report_exact_sum_is_fsum():
+    # The oracle's exact cluster bins (fixed point 2^-80, orc_fix80) equal math.fsum of the
+    # per-node NodeGpuShareFragAmount bins (correctly rounded sum), at several prefixes of a run.
+    import math
+    import ksim
+    import helpers
+    t = ksim.Trace.openb("default")
+    rp = t.replay(seed=42)
+    keep = list(range(0, t.num_nodes, 5))
+    onodes = [helpers.oracle_nodes(t, rp)[i] for i in keep]
+    tl = helpers.oracle_typical(t)
+    tp = O.typical(tl)
+    for n_ev in (1, 200, 900):
+        res, state, reps = O.run_events(onodes, tl, helpers.oracle_events(t, rp, n_ev), threads=8,
+                                        with_report=True)
+        per_node = []
+        for d, (cpu_left, _, _, gl) in zip(onodes, state):
+            nr = O.node_res(cpu_left, gl[:d["gpu"]], d["gpu"], d["model"], d["cpu"])
+            per_node.append(O.frag_bins(nr, tp))
+        exact = [math.fsum(b[k] for b in per_node) for k in range(7)]
+        assert reps[-1]["frag_bins_exact"] == exact
+        for a, b in zip(reps[-1]["frag_bins"], exact):
+            assert abs(a - b) <= 1e-12 * max(b, 1.0)
