@@ -84,6 +84,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | ...")
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2: openb x 10 seeds per GPU (headline); c4: the paper sweep, 17 traces x 6 policies "
+                         "x 10 seeds split over the GPUs; c5: synthetic 100k nodes x 1M pods, one replica per GPU")
+    ap.add_argument("--report", action="store_true", help="also compute the per-event cluster report")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,8 +105,25 @@ def main():
         torch.cuda.set_device(0)
 
     trace = ksim.Trace.openb("default")
-    seeds = seeds_for_rank(rank, args.replicas)
-    eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode)
+    if args.config == "c4":
+        import ksim.sweep as SW
+        exps = SW.shard(SW.plan(), rank, world)
+        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs)
+        eng = sweep.eng
+        eng.total_events = sweep.total_events
+        args.replicas = len(exps)
+    elif args.config == "c5":
+        # nodes i.i.d. from the openb node specs (seed 0), 1M pods i.i.d. from the
+        # default-trace rows; rank k replays its own draw (seed 2k+1), no tuning, trace order
+        trace = trace.synthetic(100_000, 1_000_000, seed=0)
+        args.replicas = 1
+        seeds = [2 * rank + 1]
+        eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
+                         tune=0.0, shuffle=False, report=args.report)
+    else:
+        seeds = seeds_for_rank(rank, args.replicas)
+        eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
+                         report=args.report)
     total_events = eng.total_events
 
     for _ in range(args.warmup):
@@ -131,7 +152,8 @@ def main():
 
     value = job_events / dt
     traffic, traffic_src = None, None
-    default_cfg = (args.policy == "FGD" and args.replicas == 10 and args.run_mode == 0 and args.wgs == 0)
+    default_cfg = (args.config == "c2" and args.policy == "FGD" and args.replicas == 10 and args.run_mode == 0
+                   and args.wgs == 0 and not args.report)
     if default_cfg and os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
@@ -161,9 +183,24 @@ def main():
                      "kernel": "k_replay", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
                      "wgs_per_replica": eng.last_run_wgs()},
     }
+    if args.config == "c4":
+        line["data"] = "Alibaba openb traces (data/openb: 17 pod lists), documented event order"
+        line["config"] = {"workload": "C4: paper sweep, 17 traces x 6 policies x seeds 42-51, tune 1.3, "
+                                      "per-event cluster report", "replicas_per_gpu": args.replicas,
+                          "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
+        # whole job: every rank's experiments per timed step (the reference: 1020 in ~10 h on 256 vCPU)
+        line["experiments_per_s"] = args.replicas * world / (dt / args.steps)
+    if args.config == "c5":
+        line["data"] = "synthetic (SURVEY §8(d) C5): nodes and pods drawn i.i.d. from the openb default trace"
+        line["config"] = {"workload": "C5: synthetic 100000 nodes x 1000000 pods, FGD, one replica per GPU",
+                          "replicas_per_gpu": 1, "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
     if args.policy != "FGD":
         line["config"]["workload"] = line["config"]["workload"].replace("FGD", args.policy)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.report:
+        line["config"]["report"] = True
+    if args.config == "c4" or args.report:
+        line["report_ms_per_step"] = eng.last_report_ms()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         line["cpu_baseline"] = cpu_baseline(trace, seeds[0], args.cpu_threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -172,13 +209,16 @@ def main():
         dist.destroy_process_group()
 
 
-def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_mode=0):
+def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_mode=0, tune=1.3, shuffle=True,
+               report=False):
     arr, n = trace.typical()
     eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block,
                       wgs_per_replica=wgs, run_mode=run_mode)
+    if report:
+        eng.set_report(True)
     total = 0
     for r, s in enumerate(seeds):
-        rp = trace.replay(seed=s, tune_ratio=1.3, shuffle=True)
+        rp = trace.replay(seed=s, tune_ratio=tune, shuffle=shuffle)
         eng.set_nodes(r, rp.nodes)
         eng.set_typical(r, arr, n)
         eng.set_policy(r, policy)

@@ -492,7 +492,14 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-template <int kPol>
+// Polled granules of the pending exchange, per wave-0 lane: workgroups lane + 64 j, j < kSub.
+template <int kSub>
+struct GranV {
+  unsigned long long g0[kSub], g1[kSub], g2[kSub];
+};
+
+// kSub = ceil(K / 64): 1 for K <= 64, 4 for K <= 256 (one wave-0 lane polls kSub workgroups).
+template <int kPol, int kSub>
 __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
                                                                  const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
@@ -517,7 +524,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   // cluster report: the last event that changed each slot (-1: none yet)
   int* s_last = reinterpret_cast<int*>(s_F0 + S1);
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
-  int2* hist = a.hist + (size_t)(r * a.K + w) * a.hist_stride;
+  // (null when no replica of the launch has a delete event: nothing ever reads it)
+  int2* hist = a.hist ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
   unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * 4;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
@@ -555,19 +563,23 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     }
   };
 
-  // Wave 0, lane k < K: workgroup k's granules of the pending exchange (relaxed agent-scope loads).
-  auto poll_once = [&](unsigned long long* g0, unsigned long long* g1, unsigned long long* g2) {
-    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * 4 + (size_t)lane * 4;
-    if (lane < a.K) {
-      *g0 = gload(slot + 0);
-      *g1 = gload(slot + 1);
-      *g2 = gload(slot + 2);
+  // Wave 0, lane k: the granules of workgroups k, k+64, .. (< K) of the pending exchange
+  // (relaxed agent-scope loads).
+  auto poll_once = [&](GranV<kSub>& g) {
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * 4;
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) {
+      const int k = lane + 64 * j;
+      if (k < a.K) {
+        g.g0[j] = gload(slot + (size_t)k * 4 + 0);
+        g.g1[j] = gload(slot + (size_t)k * 4 + 1);
+        g.g2[j] = gload(slot + (size_t)k * 4 + 2);
+      }
     }
   };
   // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
-  // this workgroup's own totals (K == 1); g* hold an earlier poll.  Returns the winning key.
-  auto exchange = [&](unsigned long long g0, unsigned long long g1, unsigned long long g2, int* gc, int* ge,
-                      int* gl, int* gh, bool* ok) -> unsigned long long {
+  // this workgroup's own totals (K == 1); g holds an earlier poll.  Returns the winning key.
+  auto exchange = [&](GranV<kSub> g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
     *ok = true;
     if (a.K == 1) {
       *gc = p_st0; *ge = p_st1; *gl = p_st2; *gh = p_st3;
@@ -575,28 +587,46 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     }
     const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
     auto ready = [&]() {
-      return lane >= a.K ||
-             ((g0 & ~0xffffffffull) == tag && (g1 & ~0xffffffffull) == tag && (g2 & ~0xffffffffull) == tag);
+      bool r = true;
+#pragma unroll
+      for (int j = 0; j < kSub; ++j)
+        r = r && (lane + 64 * j >= a.K || ((g.g0[j] & ~0xffffffffull) == tag && (g.g1[j] & ~0xffffffffull) == tag &&
+                                          (g.g2[j] & ~0xffffffffull) == tag));
+      return r;
     };
     unsigned spins = 0;
     while (!__all(ready())) {
       if (++spins > kSpinLimit) { *ok = false; break; }
       __builtin_amdgcn_s_sleep(1);
-      poll_once(&g0, &g1, &g2);
+      poll_once(g);
     }
     if (prof && lane == 0) sh.prof[8] += spins;
-    const bool in = lane < a.K;
-    const unsigned st = in ? (unsigned)(g2 & 0xffffffffull) : 0u;
-    const int c = (int)(st & 0x1ffff);
+    int c = 0, lo = 0x7fffffff, hi = -1;
+    bool e1 = false;
+    unsigned long long best = 0ull;
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) {
+      const bool in = lane + 64 * j < a.K;
+      const unsigned st = in ? (unsigned)(g.g2[j] & 0xffffffffull) : 0u;
+      const int cj = (int)(st & 0x1ffff);
+      c += cj;
+      e1 = e1 || (st >> 31) != 0u;
+      if (kMinMax && cj > 0) {
+        lo = min(lo, (int)((st >> 17) & 0x7f));
+        hi = max(hi, (int)((st >> 24) & 0x7f));
+      }
+      const unsigned long long kj = in ? ((g.g1[j] & 0xffffffffull) << 32) | (g.g0[j] & 0xffffffffull) : 0ull;
+      best = kj > best ? kj : best;
+    }
     *gc = wave_sum_dpp(c);
-    *ge = __any(st >> 31) ? 1 : 0;
+    *ge = __any(e1) ? 1 : 0;
     *gl = 0x7fffffff;
     *gh = -1;
     if (kMinMax) {
-      *gl = wave_min_dpp(c > 0 ? (int)((st >> 17) & 0x7f) : 0x7fffffff);
-      *gh = wave_max_dpp(c > 0 ? (int)((st >> 24) & 0x7f) : -1);
+      *gl = wave_min_dpp(lo);
+      *gh = wave_max_dpp(hi);
     }
-    return wave_max_u64_dpp(in ? ((g1 & 0xffffffffull) << 32) | (g0 & 0xffffffffull) : 0ull);
+    return wave_max_u64_dpp(best);
   };
 
   // Wave 0: commit the pending step -- the owner of the winning node turns the virtual slot
@@ -636,7 +666,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
       }
     }
     if (lane == 0) {
-      hist[p_step] = hrec;
+      if (hist) hist[p_step] = hrec;
       if (writer) rp.res[p_step] = out;
     }
   };
@@ -644,11 +674,11 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   // Finish the pending step with nothing to overlap (before a delete / at the end).
   auto finish_pending = [&]() {
     if (wv == 0) {
-      unsigned long long g0 = 0, g1 = 0, g2 = 0;
-      if (a.K > 1) poll_once(&g0, &g1, &g2);
+      GranV<kSub> g{};
+      if (a.K > 1) poll_once(g);
       int gc, ge, gl, gh;
       bool ok;
-      const unsigned long long W = exchange(g0, g1, g2, &gc, &ge, &gl, &gh, &ok);
+      const unsigned long long W = exchange(g, &gc, &ge, &gl, &gh, &ok);
       if (ok) commit(W, gc, ge, gl, gh);
       if (lane == 0) {
         if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
@@ -692,7 +722,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         } else if ((h.x == -1 && w == 0) || h.x == -3) {
           rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
         }
-        hist[step] = make_int2(-1, 0);
+        if (hist) hist[step] = make_int2(-1, 0);
       }
       __syncthreads();
       mark(0);
@@ -704,7 +734,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     const int vb = pend ? __builtin_amdgcn_readfirstlane(pvb.y) : -1;
     const int nsv = ns + (vb >= 0 ? 1 : 0);
     // early poll of the pending exchange by wave 0 (consumed after the evaluation)
-    unsigned long long pg0 = 0, pg1 = 0, pg2 = 0;
+    GranV<kSub> pg{};
     // one node's packed key into the workgroup aggregate (LDS atomics), or the excluded pair
     auto route = [&](bool leader, int i, bool feas, bool e1, int raw, unsigned long long k) {
       const bool excl = leader && (i == vb || i == ns);
@@ -787,7 +817,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         }
         __syncthreads();
         mark(2);
-        if (pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(&pg0, &pg1, &pg2);
+        if (pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(pg);
         if (tid == 0) sh.nitems = 0;  // every thread has read tot; the next writer is past a barrier
         // fgd_score.go:100-141: every candidate lane scores itself; the node keeps the max,
         // ties to the lowest GPU index (fgd_score.go:128 keeps the first max)
@@ -803,7 +833,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         mark(3);
       }
     } else {
-      if (pend && a.K > 1 && wv == 0) poll_once(&pg0, &pg1, &pg2);
+      if (pend && a.K > 1 && wv == 0) poll_once(pg);
       for (int c0 = 0; c0 < nsv; c0 += kChunk) {
         const int cn = min(kChunk, nsv - c0);
         const int i = c0 + tid;
@@ -832,7 +862,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
       unsigned long long W = 0ull;
       int gc = 0, ge = 0, gl = 0, gh = 0;
       if (pend) {
-        W = exchange(pg0, pg1, pg2, &gc, &ge, &gl, &gh, &ok);
+        W = exchange(pg, &gc, &ge, &gl, &gh, &ok);
         owner = W != 0ull && W == p_key;
       }
       mark(5);
@@ -1019,6 +1049,7 @@ struct ksim_engine {
   std::vector<PodDev*> d_ev;
   std::vector<ResultDev*> d_res;
   std::vector<int> n_events;
+  std::vector<char> has_delete;  // the replica's stream has deletion events (k_replay keeps a bind history)
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
   int graph_R = -1;
@@ -1053,8 +1084,13 @@ static int upload_reps(ksim_engine* e) {
 
 template <int P>
 static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp) {
-  (void)hipFuncSetAttribute((const void*)k_replay<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_replay<P>, dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+  if (ra.K <= 64) {
+    (void)hipFuncSetAttribute((const void*)k_replay<P, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_replay<P, 1>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+  } else {
+    (void)hipFuncSetAttribute((const void*)k_replay<P, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_replay<P, 4>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+  }
 }
 
 extern "C" {
@@ -1147,6 +1183,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->d_ev.assign(n_replicas, nullptr);
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
+  e->has_delete.assign(n_replicas, 0);
   e->nt.assign(n_replicas, 0);
   e->d_snap.assign(n_replicas, nullptr);
   e->d_prev.assign(n_replicas, nullptr);
@@ -1429,6 +1466,8 @@ int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events,
   if (n > 0) KSIM_HIP(hipMemcpyAsync(e->d_ev[replica], h.data(), sizeof(PodDev) * n, hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemsetAsync(e->d_res[replica], 0xff, sizeof(ResultDev) * ne, e->stream));
   e->n_events[replica] = n;
+  e->has_delete[replica] = false;
+  for (int i = 0; i < n; ++i) e->has_delete[replica] = e->has_delete[replica] || events[i].is_delete;
   e->reps[replica].ev = e->d_ev[replica];
   e->reps[replica].res = e->d_res[replica];
   e->reps[replica].n_events = n;
@@ -1531,7 +1570,13 @@ static void print_replay_profile(ksim_engine* e, int R, int K, int steps) {
 // co-resident (they exchange granules every step), so R*K never exceeds one
 // workgroup per CU; K = 1 needs no co-residency at all.
 static int choose_wgs(const ksim_engine* e, int R) {
-  int K = e->wgs_req > 0 ? e->wgs_req : e->cus / R;
+  // auto: one workgroup per CU up to 64 per replica; large clusters (C5: 100k nodes) go wider
+  // so that a slice stays near 384 nodes (one to two FGD evaluation rounds per step)
+  int K = e->wgs_req;
+  if (K <= 0) {
+    K = std::min(e->cus / R, 64);
+    K = std::max(K, std::min(e->cus / R, (e->N + 383) / 384));
+  }
   K = std::max(1, std::min(K, ksim_replay::kMaxK));
   K = std::min(K, e->N);
   if (R * K > e->cus) K = 1;
@@ -1556,6 +1601,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   }
   KSIM_HIP(hipMemcpyAsync(e->d_replist, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
+  bool any_delete = false;
+  for (int r = 0; r < e->R; ++r) any_delete = any_delete || e->has_delete[r];
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   int first = 0;
@@ -1568,7 +1615,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       S = (e->N + K - 1) / K;
     }
     if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
-    const size_t need = (size_t)e->R * K * std::max(max_ev, 1);
+    const size_t need = any_delete ? (size_t)e->R * K * std::max(max_ev, 1) : 0;
     if (need > e->hist_cap) {
       if (e->d_hist) KSIM_HIP(hipFree(e->d_hist));
       KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
@@ -1582,7 +1629,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     ra.K = K;
     ra.S = S;
     ra.gran = e->d_gran;
-    ra.hist = e->d_hist;
+    ra.hist = any_delete ? e->d_hist : nullptr;
     ra.hist_stride = std::max(max_ev, 1);
     ra.fail = e->d_fail;
     ra.prof = nullptr;

@@ -44,7 +44,7 @@ constexpr int kRWaves = kRBlock / 64;
 constexpr int kChunk = kRBlock;      // nodes per chunk, one lane per node (non-FGD policies)
 constexpr int kFChunk = kRBlock / 8; // nodes per chunk, 8 lanes per node -- lane g <-> GPU g (FGD)
 constexpr int kRMaxCand = 9;         // FGD items per node: stale current state + up to 8 candidates
-constexpr int kMaxK = 64;          // workgroups per replica
+constexpr int kMaxK = 256;         // workgroups per replica (<= 64: one granule column per polling lane)
 constexpr int kGran = 3;           // granules per workgroup per step
 constexpr unsigned kSpinLimit = 1u << 22;  // ~seconds: only a non-resident workgroup can stall a poll
 constexpr int kEvBuf = 128;        // events staged in LDS per refill (4 KB)

@@ -133,7 +133,17 @@ __device__ __forceinline__ __int128 block_excl_scan128(__int128 v, __int128* s_w
   return base + incl - v;
 }
 
-// grid R: the initial cluster's report, then the inclusive prefix over the events (in place).
+// Field k of a RepAcc (bins 0-6 are 128-bit, counters 7-12 are 64-bit).
+__device__ __forceinline__ __int128 rep_get(const RepAcc* o, int k) {
+  return k < 7 ? o->bins[k] : (__int128)o->cnt[k - 7];
+}
+__device__ __forceinline__ void rep_set(RepAcc* o, int k, __int128 v) {
+  if (k < 7) o->bins[k] = v;
+  else o->cnt[k - 7] = (long long)v;
+}
+
+// grid R: the initial cluster's report, then the inclusive prefix over the events (in place),
+// one field at a time (keeps the 128-bit running sums in a few registers).
 __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
                                                             int N) {
   const int r = (int)blockIdx.x;
@@ -141,46 +151,42 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
   if (!rp.rep) return;
   __shared__ TypDev s_tp[kMaxTypical];
   __shared__ __int128 s_w[kScanBlock / 64];
+  __shared__ __int128 s_base[kFields];
   stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
   const int tid = (int)threadIdx.x;
   // the cluster as run() starts it (analysis.go:80-98 over the initial state)
-  __int128 acc[kFields];
+  {
+    __int128 acc[kFields];
 #pragma unroll
-  for (int k = 0; k < kFields; ++k) acc[k] = 0;
-  for (int i = tid; i < N; i += kScanBlock) {
-    __int128 f[kFields];
-    node_term(load_node(rp.init + i), rp.cap[i], s_tp, rp.ncpu, rp.nt, f);
+    for (int k = 0; k < kFields; ++k) acc[k] = 0;
+    for (int i = tid; i < N; i += kScanBlock) {
+      __int128 f[kFields];
+      node_term(load_node(rp.init + i), rp.cap[i], s_tp, rp.ncpu, rp.nt, f);
 #pragma unroll
-    for (int k = 0; k < kFields; ++k) acc[k] += f[k];
+      for (int k = 0; k < kFields; ++k) acc[k] += f[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) {
+      __int128 tot;
+      (void)block_excl_scan128(acc[k], s_w, &tot);
+      if (tid == 0) s_base[k] = tot;
+    }
   }
-  __int128 base[kFields];
-#pragma unroll
-  for (int k = 0; k < kFields; ++k) (void)block_excl_scan128(acc[k], s_w, &base[k]);
-  // contiguous chunk per thread: local totals, block exclusive scan, then the running sum
+  __syncthreads();
+  // contiguous chunk per thread: local total, block exclusive scan, then the running sum
   const int E = rp.n_events;
   const int per = (E + kScanBlock - 1) / kScanBlock;
   const int lo = min(E, tid * per), hi = min(E, lo + per);
-  __int128 loc[kFields];
-#pragma unroll
-  for (int k = 0; k < kFields; ++k) loc[k] = 0;
-  for (int e = lo; e < hi; ++e) {
-    __int128 f[kFields];
-    load_rep(rp.rep + e, f);
-#pragma unroll
-    for (int k = 0; k < kFields; ++k) loc[k] += f[k];
-  }
-  __int128 run[kFields];
-#pragma unroll
+#pragma unroll 1
   for (int k = 0; k < kFields; ++k) {
+    __int128 loc = 0;
+    for (int e = lo; e < hi; ++e) loc += rep_get(rp.rep + e, k);
     __int128 tot;
-    run[k] = base[k] + block_excl_scan128(loc[k], s_w, &tot);
-  }
-  for (int e = lo; e < hi; ++e) {
-    __int128 f[kFields];
-    load_rep(rp.rep + e, f);
-#pragma unroll
-    for (int k = 0; k < kFields; ++k) run[k] += f[k];
-    store_rep(rp.rep + e, run);
+    __int128 run = s_base[k] + block_excl_scan128(loc, s_w, &tot);
+    for (int e = lo; e < hi; ++e) {
+      run += rep_get(rp.rep + e, k);
+      rep_set(rp.rep + e, k, run);
+    }
   }
 }
 

@@ -353,6 +353,18 @@ class Engine:
                      arrived_gpu_milli=out[i].arrived_gpu_milli, used_cpu_milli=out[i].used_cpu_milli,
                      arrived_cpu_milli=out[i].arrived_cpu_milli) for i in range(n)]
 
+    def report_arrays(self, r):
+        """The reports of replica r as numpy arrays (frag_bins [n,7] float64, counters [n] int64)."""
+        n = self.n_events[r]
+        out = (Report * max(1, n))()
+        check(lib().ksim_engine_get_reports(self.h, r, out, n), "get_reports")
+        a = np.ctypeslib.as_array(out)[:n]
+        keys = ["used_nodes", "used_gpus", "used_gpu_milli", "total_gpus", "arrived_gpu_milli", "used_cpu_milli",
+                "arrived_cpu_milli"]
+        d = {k: np.array(a[k]) for k in keys}
+        d["frag_bins"] = np.array(a["frag_bins"])
+        return d
+
     def last_report_ms(self):
         ms = C.c_double(0)
         check(lib().ksim_engine_last_report_ms(self.h, C.byref(ms)), "last_report_ms")

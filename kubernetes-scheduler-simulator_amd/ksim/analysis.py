@@ -169,3 +169,43 @@ def curves(reports):
             lines.append(logrus_line(m))
     frag, allo = parse_log_lines(lines)
     return dict(alloc=alloc_curve(allo), frag=frag_curve(allo, frag), frag_ratio=frag_ratio_curve(allo, frag))
+
+
+def curves_arrays(arrs):
+    """Vectorised curves of one replica from ksim.Engine.report_arrays (for sweeps of ~1000
+    replicas).  Same values as curves() except that a bucket mean is summed in bincount order
+    instead of pandas' order, which can move a 2-decimal rounding by 0.01 in rare ties."""
+    import numpy as np
+    b = arrs["frag_bins"]
+    idle = np.zeros(len(b))
+    for k in range(7):
+        idle = idle + b[:, k]
+    frag = np.zeros(len(b))
+    for k in range(7):
+        if k != Q3:
+            frag = frag + b[:, k]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ratio = 100 * frag / idle
+    frag_p = np.array([float(_go_f2(x)) for x in frag.tolist()])    # the printed %.2f values
+    ratio_p = np.array([float(_go_f2(x)) for x in ratio.tolist()])
+    total = int(arrs["total_gpus"][0])
+    arrive = np.array([round(x, 0) for x in (arrs["arrived_gpu_milli"] / total / 10).tolist()])
+    alloc = np.array([round(x, 2) for x in (arrs["used_gpu_milli"] / total / 10).tolist()])
+    ok = (arrive >= 0) & (arrive <= 131)
+    idx = np.where(ok, arrive, 132).astype(np.int64)
+    cnt = np.bincount(idx, minlength=133)[:132]
+    sums = {name: np.bincount(idx, weights=v, minlength=133)[:132]
+            for name, v in (("alloc", alloc), ("frag", frag_p), ("ratio", ratio_p))}
+    out = {"alloc": {}, "frag": {}, "frag_ratio": {}}
+    for a in range(131):
+        if cnt[a] > 0:
+            sel = [a]
+        else:
+            sel = [x for x in (a - 1, a, a + 1) if 0 <= x < 132 and cnt[x] > 0]
+            if not sel:
+                continue
+        c = sum(cnt[x] for x in sel)
+        out["alloc"][a] = round(sum(sums["alloc"][x] for x in sel) / c, 2)
+        out["frag"][a] = round(100 * (sum(sums["frag"][x] for x in sel) / c) / 1000 / total, 2)
+        out["frag_ratio"][a] = sum(sums["ratio"][x] for x in sel) / c
+    return out

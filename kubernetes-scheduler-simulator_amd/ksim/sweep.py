@@ -1,0 +1,91 @@
+"""The paper sweep (C4): traces x policies x seeds as independent replicas on one GPU.
+
+The reference runs each (trace, policy, seed) experiment as its own `simon apply` process,
+1020 of them in ~10 h on 256 vCPUs (experiments/README.md:19-27,69-70; run lists in
+experiments/run_scripts/expected_run_scripts_0511.sh).  Here every experiment is one replica of
+one ksim.Engine: one k_replay launch per policy replays them all, the device computes every
+event's cluster report, and the host turns the reports into the allocation / fragmentation
+curves of experiments/analysis/merge_*_discrete.py (ksim.analysis).
+"""
+import time
+
+import numpy as np
+
+import ksim
+import ksim.analysis as A
+
+TRACES = ["openb_pod_list_cpu050", "openb_pod_list_cpu100", "openb_pod_list_cpu200", "openb_pod_list_cpu250",
+          "openb_pod_list_default", "openb_pod_list_gpushare100", "openb_pod_list_gpushare40",
+          "openb_pod_list_gpushare60", "openb_pod_list_gpushare80", "openb_pod_list_gpuspec10",
+          "openb_pod_list_gpuspec20", "openb_pod_list_gpuspec25", "openb_pod_list_gpuspec33",
+          "openb_pod_list_multigpu20", "openb_pod_list_multigpu30", "openb_pod_list_multigpu40",
+          "openb_pod_list_multigpu50"]
+# expected_results' sc_policy directories -> (score plugin, gpuSelMethod) (expected_run_scripts_0511.sh)
+POLICY_DIRS = {"01-Random": "Random", "02-DotProd": "DotProd", "03-GpuClustering": "GpuClustering",
+               "04-GpuPacking": "GpuPacking", "05-BestFit": "BestFit", "06-FGD": "FGD"}
+SEEDS = list(range(42, 52))
+
+
+def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
+    return [(t, p, s, tune) for t in traces for p in policies for s in seeds]
+
+
+def shard(items, rank, world):
+    """Replica-parallel split across ranks (no collective on the data path)."""
+    return items[rank::world]
+
+
+class Sweep:
+    """All experiments of a plan as replicas of one engine on one device."""
+
+    def __init__(self, experiments, device=0, report=True, wgs=0):
+        self.exps = list(experiments)
+        traces = {}
+        for (t, _, _, _) in self.exps:
+            if t not in traces:
+                traces[t] = ksim.Trace.openb(t[len("openb_pod_list_"):] if t.startswith("openb_pod_list_") else t)
+        n_nodes = {tr.num_nodes for tr in traces.values()}
+        assert len(n_nodes) == 1, "every trace of a sweep must share the node list"
+        self.eng = ksim.Engine(n_nodes.pop(), len(self.exps), device=device, wgs_per_replica=wgs)
+        if report:
+            self.eng.set_report(True)
+        typ = {name: tr.typical() for name, tr in traces.items()}
+        self.total_events = 0
+        for r, (t, p, s, tune) in enumerate(self.exps):
+            rp = traces[t].replay(seed=s, tune_ratio=tune, shuffle=True)
+            self.eng.set_nodes(r, rp.nodes)
+            arr, n = typ[t]
+            self.eng.set_typical(r, arr, n)
+            self.eng.set_policy(r, POLICY_DIRS[p], seed=s)
+            self.eng.load_events(r, rp.events, rp.n)
+            self.total_events += rp.n
+        self.report = report
+
+    def run(self):
+        t0 = time.perf_counter()
+        dev_ms = self.eng.run()
+        return dev_ms, time.perf_counter() - t0
+
+    def curves(self):
+        """{(trace, policy, seed): {"alloc": {arr%: val}, "frag": ..., "frag_ratio": ...}}"""
+        assert self.report
+        return {(t, p, s): A.curves_arrays(self.eng.report_arrays(r)) for r, (t, p, s, _) in enumerate(self.exps)}
+
+    def close(self):
+        self.eng.close()
+
+
+def mean_curve(curves, trace, policy, kind="alloc"):
+    """Mean over seeds of one (trace, policy) curve: {arrived %: mean}."""
+    rows = [c[kind] for (t, p, _), c in curves.items() if t == trace and p == policy]
+    keys = sorted(set.intersection(*[set(r) for r in rows]))
+    return {k: float(np.mean([r[k] for r in rows])) for k in keys}
+
+
+def expected_mean_curve(csv_path, trace, policy, seeds=SEEDS):
+    """The reference's expected_results/analysis_*_discrete.csv mean over seeds."""
+    import pandas as pd
+    df = pd.read_csv(csv_path)
+    df = df[(df.workload == trace) & (df.sc_policy == policy) & (df.seed.isin(list(seeds)))]
+    cols = [c for c in df.columns if c.isdigit()]
+    return {int(c): float(df[c].mean()) for c in cols if df[c].notna().all()}

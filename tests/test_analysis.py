@@ -64,3 +64,20 @@ def test_report_messages_format():
     assert line.endswith('Arrived GPU Milli: 5000\\n"\n')
     empty = dict(rep, frag_bins=[0.0] * 7)
     assert "Frag ratio: NaN%" in A.report_messages(empty)[0]
+
+
+def test_curves_arrays_fast_path_matches():
+    # the vectorised sweep path equals the merge_*_discrete.py path up to a 0.01 rounding tie
+    import numpy as np
+    for seed in GOLD["seeds"]:
+        reps = synth_reports(seed, GOLD["total_gpus"])
+        arrs = {k: np.array([r[k] for r in reps]) for k in reps[0] if k != "frag_bins"}
+        arrs["frag_bins"] = np.array([r["frag_bins"] for r in reps])
+        fast = A.curves_arrays(arrs)
+        want = GOLD["curves"][str(seed)]
+        assert {str(k) for k in fast["alloc"]} == set(want["alloc"])
+        for kind in ("alloc", "frag"):
+            for k, v in fast[kind].items():
+                assert abs(v - want[kind][str(k)]) <= 0.0100001, (kind, k, v, want[kind][str(k)])
+        for k, v in fast["frag_ratio"].items():
+            assert math.isclose(v, want["frag_ratio"][str(k)], rel_tol=1e-9)
