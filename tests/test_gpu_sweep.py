@@ -55,3 +55,26 @@ def test_default_trace_all_policies_vs_expected_results(default_sweep):
             assert abs(fo[k] - fr[k]) <= 0.3, (p, "frag", k, fo[k], fr[k])
     at130 = {p: ours[130] for p, ours, _, _, _ in rows}
     assert max(at130, key=at130.get) == "06-FGD" and min(at130, key=at130.get) == "01-Random"
+
+
+def test_full_paper_sweep_vs_expected_results():
+    # C4: all 1020 experiments (17 traces x 6 policies x 10 seeds) as replicas of one engine;
+    # every (trace, policy) 10-seed mean curve near the reference's, at every arrived-GPU %.
+    sw = SW.Sweep(SW.plan())
+    dev_ms, wall = sw.run()
+    curves = sw.curves()
+    sw.close()
+    worst = {}
+    for t in SW.TRACES:
+        for p in SW.POLICY_DIRS:
+            for kind, csv in (("alloc", ALLO), ("frag", FRAG)):
+                ours, ref = SW.mean_curve(curves, t, p, kind), SW.expected_mean_curve(csv, t, p)
+                keys = [k for k in ours if k in ref]
+                assert len(keys) >= 125, (t, p, kind)
+                worst[(t, p, kind)] = max(abs(ours[k] - ref[k]) for k in keys)
+    print("1020 experiments: %.0f ms device time; worst deviations:" % dev_ms,
+          sorted(worst.items(), key=lambda kv: -kv[1])[:5])
+    # measured (profiles/r01/sweep_compare.json): worst 0.85 (Random, itself not reproducible in the
+    # reference), <= 0.62 for every other policy; the reference's own seed spread is up to ~1.2
+    for (t, p, kind), dev in worst.items():
+        assert dev <= (1.5 if p == "01-Random" else 1.0), (t, p, kind, dev)
