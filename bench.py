@@ -88,6 +88,9 @@ def main():
                     help="c2: openb x 10 seeds per GPU (headline); c4: the paper sweep, 17 traces x 6 policies "
                          "x 10 seeds split over the GPUs; c5: synthetic 100k nodes x 1M pods, one replica per GPU")
     ap.add_argument("--report", action="store_true", help="also compute the per-event cluster report")
+    ap.add_argument("--sharded", action="store_true",
+                    help="c5 only: ONE cluster node-sharded over the ranks (RCCL exchange per pod; strong "
+                         "scaling) instead of one replica per rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,6 +115,11 @@ def main():
         eng = sweep.eng
         eng.total_events = sweep.total_events
         args.replicas = len(exps)
+    elif args.config == "c5" and args.sharded:
+        # one 100k-node cluster split by name rank over the ranks; every rank replays the same 1M events
+        trace = trace.synthetic(100_000, 1_000_000, seed=0)
+        args.replicas = 1
+        eng = _sharded_engine(local, rank, world, trace, dist)
     elif args.config == "c5":
         # nodes i.i.d. from the openb node specs (seed 0), 1M pods i.i.d. from the
         # default-trace rows; rank k replays its own draw (seed 2k+1), no tuning, trace order
@@ -142,6 +150,8 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     dt, job_events = reduce_job(dt, total_events * args.steps, dist, "cuda")
+    if args.sharded:
+        job_events = total_events * args.steps  # one cluster: every rank processed the same events
 
     steps_per_run = eng.last_run_steps()
     # roofline: the dominant kernel is k_replay, one launch per replay of all replicas; its duration is
@@ -190,7 +200,14 @@ def main():
                           "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
         # whole job: every rank's experiments per timed step (the reference: 1020 in ~10 h on 256 vCPU)
         line["experiments_per_s"] = args.replicas * world / (dt / args.steps)
-    if args.config == "c5":
+    if args.config == "c5" and args.sharded:
+        line["scaling"] = "strong"
+        line["config"] = {"workload": "C5: synthetic 100000 nodes x 1000000 pods, FGD, ONE cluster node-sharded "
+                                      "over %d GPU(s), RCCL all-gather of a 32-B record per pod" % world,
+                          "replicas_per_gpu": 1, "events_per_gpu": total_events,
+                          "parallelism": "nodeshard%d" % world}
+        line["data"] = "synthetic (SURVEY §8(d) C5): nodes and pods drawn i.i.d. from the openb default trace"
+    elif args.config == "c5":
         line["data"] = "synthetic (SURVEY §8(d) C5): nodes and pods drawn i.i.d. from the openb default trace"
         line["config"] = {"workload": "C5: synthetic 100000 nodes x 1000000 pods, FGD, one replica per GPU",
                           "replicas_per_gpu": 1, "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
@@ -207,6 +224,26 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _sharded_engine(device, rank, world, trace, dist):
+    """This rank's shard of the one C5 cluster (ksim.shard; RCCL id made on rank 0)."""
+    import ksim.shard as SH
+    rp = trace.replay(seed=1, tune_ratio=0.0, shuffle=False)
+    parts = SH.partition(rp.nodes, world)
+    off, local, idx = parts[rank]
+    box = [ksim.shard_comm_id() if rank == 0 else None]
+    if dist is not None:
+        dist.broadcast_object_list(box, src=0)
+    arr, n = trace.typical()
+    eng = ksim.Engine(len(idx), 1, device=device)
+    eng.set_shard(rank, world, off, trace.num_nodes, box[0])
+    eng.set_nodes(0, local)
+    eng.set_typical(0, arr, n)
+    eng.set_policy(0, "FGD")
+    eng.load_events(0, rp.events, rp.n)
+    eng.total_events = rp.n
+    return eng
 
 
 def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_mode=0, tune=1.3, shuffle=True,

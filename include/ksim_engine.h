@@ -205,6 +205,24 @@ int  ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int 
 /* Device time of the report kernels of the last run (ms; part of last_run_ms). */
 int  ksim_engine_last_report_ms(ksim_engine* e, double* ms);
 
+/* Node-sharded single cluster (SURVEY §8(e), C5 across GPUs).  One engine (R = 1) per shard holds
+ * the nodes whose global name ranks are [node_offset, node_offset + n_nodes): local node i must
+ * have name_rank == node_offset + i (call set_shard BEFORE set_nodes).  Every shard loads the same
+ * event stream.  Per pod step every shard filters and scores its nodes, the shards exchange one
+ * 32-byte record {best packed key, feasible count, error flag, BestFit min|max}, and only the
+ * shard owning the winning node runs Reserve + Bind (generic_scheduler.go:187-212 selectHost over
+ * the union of the shards).  Results carry global node ranks; the owner's record of a step is
+ * authoritative (others hold gpu_mask 0 and a provisional status).
+ *   comm_id != NULL  one process per GPU, exchange = ncclAllGather over RCCL (comm_id from
+ *                    ksim_shard_comm_id on one rank, broadcast by the caller); ksim_engine_run.
+ *   comm_id == NULL  world == 1, or an in-process group on one device run by ksim_shard_group_run
+ *                    (validation / tests). */
+#define KSIM_SHARD_ID_BYTES 128
+int  ksim_shard_comm_id(uint8_t* out /* KSIM_SHARD_ID_BYTES */);
+int  ksim_engine_set_shard(ksim_engine* e, int rank, int world, int node_offset, int n_global,
+                           const uint8_t* comm_id);
+int  ksim_shard_group_run(ksim_engine* const* engines, int world);
+
 /* Measurement.  Restarts from the set_nodes state and runs the first `n_steps`
  * pod steps of every replica as eager launches with an event pair around every
  * step kernel; returns the mean step-kernel duration in microseconds. */

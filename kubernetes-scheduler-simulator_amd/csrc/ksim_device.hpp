@@ -136,6 +136,8 @@ struct ReplicaDev {
   const int32_t* cap;    // [N] MilliCpuCapacity (utils.go:1101)
   const NodeRec* init;   // [N]
   int32_t* last;         // [N] k_step: last event that changed each node
+  int32_t node_off;      // node-sharded cluster: global index (= name rank) of local node 0, else 0
+  int32_t pad_;
 };
 
 // Per-event cluster report, exact (fixed point 2^-80 for the fp64 bins; see fix80).

@@ -24,7 +24,9 @@
 // Steps are captured K at a time into a hipGraph (kernel i reads step = base+i;
 // a one-thread kernel advances base) so a whole trace replays with no host
 // round trip per pod.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -56,7 +58,10 @@ struct StepArgs {
   int step_off;
   const PodDev* pod_override;  // single-pod calls
   ResultDev* res_override;
-  int mode;  // 0: commit (Reserve+Bind), 1: Filter+Score outputs only
+  int mode;  // 0: commit (Reserve+Bind), 1: Filter+Score outputs only, 2: shard totals -> send
+  unsigned long long* send;        // mode 2: this shard's {best key, nfeas, err, lo | hi << 32}
+  const unsigned long long* recv;  // k_shard_commit: the `world` gathered shard records
+  int world;
   uint8_t* out_feas;
   int32_t* out_score;
   int32_t* out_gpu;
@@ -330,6 +335,38 @@ __device__ __forceinline__ long long result_score(const ReplicaDev& rp, int nfea
 }
 
 
+// The end of a scheduling cycle once the cluster-wide best key and counts are known: the result,
+// Reserve's GPU selector and the Bind scatter (scheduler.go:509-554).  `node` is the local index
+// of the winning node, or -1 when another shard owns it (sharded mode: the result then carries the
+// winner's global rank and a provisional status; the owner's record is authoritative).
+__device__ void finish_cycle(const StepArgs& a, const ReplicaDev& rp, const PodDev& p, int step, ResultDev* res_slot,
+                             unsigned long long best, int nfeas, int anyerr, int glo, int ghi, int node) {
+  ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+  if (nfeas > 0) {
+    out.status = (nfeas > 1 && anyerr) ? ST_ERROR : ST_OK;  // framework.go:650-656: a Score error aborts
+    if (out.status == ST_OK) {
+      out.score = result_score(rp, nfeas, key_score(best), glo, ghi);
+      if (node < 0) {
+        out.node = (int)key_rank(best);  // another shard binds
+      } else {
+        NodeRec* nr = rp.nodes + node;
+        const NodeV wn = load_node(nr);
+        const int mask = select_gpus(wn, p, rp.gpusel, key_gpu(best), rp.seed, step);
+        if (mask < 0) {
+          out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
+          out.score = 0;
+        } else {
+          apply_bind(nr, rp.tags + (size_t)node * kTagStride, p, mask, +1);
+          if (rp.snap && !a.pod_override) note_change(rp, node, step);
+          out.node = rp.node_off + node;
+          out.gpu_mask = mask;
+        }
+      }
+    }
+  }
+  *res_slot = out;
+}
+
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __restrict__ tp_all) {
   const int r = a.rep_first + (int)blockIdx.x / a.bpr;
   const int b = (int)blockIdx.x % a.bpr;
@@ -343,14 +380,17 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
 
   if (p.flags & kPodDelete) {
     // simulator.go:416-422 deletePod -> informer DeleteFunc -> GpuSharePlugin.removePod
-    if (a.mode == 0 && b == 0 && tid == 0) {
+    if ((a.mode == 0 || a.mode == 2) && b == 0 && tid == 0) {
       ResultDev out{-1, 0, 0, 0, ST_DELETED};
       if (p.ref >= 0 && p.ref < step) {
         const ResultDev c = rp.res[p.ref];
-        if (c.node >= 0) {
+        const int local = c.node - rp.node_off;  // sharded: only the owner of the node undoes the bind
+        if (c.node >= 0 && c.status == ST_OK && local >= 0 && local < a.N) {
           const PodDev cp = rp.ev[p.ref];
-          apply_bind(rp.nodes + c.node, rp.tags + (size_t)c.node * kTagStride, cp, c.gpu_mask, -1);
-          if (rp.snap && !a.pod_override) note_change(rp, c.node, step);
+          apply_bind(rp.nodes + local, rp.tags + (size_t)local * kTagStride, cp, c.gpu_mask, -1);
+          if (rp.snap && !a.pod_override) note_change(rp, local, step);
+        }
+        if (c.node >= 0 && c.status == ST_OK) {
           out.node = c.node;
           out.gpu_mask = c.gpu_mask;
         }
@@ -456,29 +496,51 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
   const int ghi = __hip_atomic_exchange(&ac->hi, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&ac->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
-  if (nfeas > 0) {
-    out.status = (nfeas > 1 && anyerr) ? ST_ERROR : ST_OK;  // framework.go:650-656: a Score error aborts
-    if (out.status == ST_OK) {
-      out.score = result_score(rp, nfeas, key_score(best), glo, ghi);
-      // the rank -> node index map lives right after the replica's tags (see host)
-      const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
-      const int node = rank2idx[key_rank(best)];
-      NodeRec* nr = rp.nodes + node;
-      const NodeV wn = load_node(nr);
-      const int mask = select_gpus(wn, p, rp.gpusel, key_gpu(best), rp.seed, step);
-      if (mask < 0) {
-        out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
-        out.score = 0;
-      } else {
-        apply_bind(nr, rp.tags + (size_t)node * kTagStride, p, mask, +1);
-        if (rp.snap && !a.pod_override) note_change(rp, node, step);
-        out.node = node;
-        out.gpu_mask = mask;
-      }
+  if (a.mode == 2) {
+    // node-sharded cluster: this shard's totals go to the exchange (k_shard_commit finishes)
+    a.send[0] = best;
+    a.send[1] = (unsigned long long)nfeas;
+    a.send[2] = (unsigned long long)anyerr;
+    a.send[3] = (unsigned long long)(unsigned)glo | ((unsigned long long)(unsigned)ghi << 32);
+    return;
+  }
+  // the rank -> node index map lives right after the replica's tags (see host)
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
+  finish_cycle(a, rp, p, step, res_slot, best, nfeas, anyerr, glo, ghi, best ? rank2idx[key_rank(best)] : -1);
+}
+
+// Node-sharded cluster (ksim_engine_set_shard): one workgroup reduces the `world` shard records
+// gathered by the exchange and finishes the cycle; only the shard owning the winning node binds.
+// Node ranks are global and shard-contiguous (local node i has rank node_off + i).
+__global__ __launch_bounds__(64) void k_shard_commit(StepArgs a) {
+  const ReplicaDev rp = a.reps[0];
+  const int step = (a.base ? *a.base : 0) + a.step_off;
+  if (step >= rp.n_events || threadIdx.x != 0) return;
+  const PodDev p = rp.ev[step];
+  if (p.flags & kPodDelete) return;  // k_step applied it on the owner
+  unsigned long long best = 0ull;
+  int nfeas = 0, anyerr = 0, glo = 0x7fffffff, ghi = -1;
+  for (int k = 0; k < a.world; ++k) {
+    const unsigned long long* r4 = a.recv + 4 * k;
+    best = r4[0] > best ? r4[0] : best;
+    const int c = (int)r4[1];
+    nfeas += c;
+    anyerr |= (int)r4[2];
+    if (c > 0) {
+      glo = min(glo, (int)(unsigned)(r4[3] & 0xffffffffull));
+      ghi = max(ghi, (int)(unsigned)(r4[3] >> 32));
     }
   }
-  *res_slot = out;
+  const int local = best ? (int)key_rank(best) - rp.node_off : -1;
+  finish_cycle(a, rp, p, step, rp.res + step, best, nfeas, anyerr, glo, ghi, (local >= 0 && local < a.N) ? local : -1);
+}
+
+// In-process shard group: every shard's record to every shard's exchange buffer (one launch).
+__global__ void k_shard_gather(unsigned long long* const* sends, unsigned long long* const* recvs, int world) {
+  const int i = (int)threadIdx.x;  // world * world * 4 <= 1024
+  if (i >= world * world * 4) return;
+  const int dst = i / (world * 4), src = (i / 4) % world, f = i & 3;
+  recvs[dst][4 * src + f] = sends[src][f];
 }
 
 #include "ksim_replay.hpp"
@@ -1063,6 +1125,13 @@ struct ksim_engine {
   std::vector<int32_t*> d_prev;
   std::vector<RepAcc*> d_rep;
   std::vector<int64_t> total_gpus;
+  // node-sharded cluster (ksim_engine_set_shard)
+  int shard_world = 0;        // 0: not sharded
+  int shard_rank = 0, node_off = 0, n_global = 0;
+  ncclComm_t comm = nullptr;  // null: in-process shard group (ksim_shard_group_run) or world 1
+  unsigned long long* d_send = nullptr;  // this shard's record {best, nfeas, err, lo|hi}
+  unsigned long long* d_recv = nullptr;  // [world][4] gathered records
+  unsigned long long** d_ptrs = nullptr; // group mode: send / recv pointer tables
   int64_t last_steps = 0;
 };
 
@@ -1076,6 +1145,7 @@ static int check_gfx950(int dev) {
 }
 
 static int alloc_report(ksim_engine* e, int r);
+static void destroy_comm(ncclComm_t c);
 
 static int upload_reps(ksim_engine* e) {
   KSIM_HIP(hipMemcpyAsync(e->d_reps, e->reps.data(), sizeof(ReplicaDev) * e->R, hipMemcpyHostToDevice, e->stream));
@@ -1222,11 +1292,12 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (auto p : e->d_rep) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
-                  e->d_cap, e->d_last};
+                  e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
+  if (e->comm) destroy_comm(e->comm);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1265,11 +1336,14 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     const ksim_node& s = nodes[i];
     if (s.gpu_count < 0 || s.gpu_count > kMaxGpu || s.gpu_type < 0 || s.gpu_type >= KSIM_MAX_TYPES)
       return KSIM_ERANGE;
-    if (s.name_rank >= (uint32_t)e->N || seen[s.name_rank]) return KSIM_EINVAL;
+    // sharded cluster: ranks are global and shard-contiguous (local node i has rank node_off + i)
+    if (e->shard_world > 0 && s.name_rank != (uint32_t)(e->node_off + i)) return KSIM_EINVAL;
+    const uint32_t lr = s.name_rank - (uint32_t)e->node_off;
+    if (lr >= (uint32_t)e->N || seen[lr]) return KSIM_EINVAL;
     if (s.cpu_alloc_milli < 0 || s.cpu_alloc_milli > 0x3fffffff) return KSIM_ERANGE;
     cap[i] = (int32_t)s.cpu_alloc_milli;
     gpus += s.gpu_count;
-    seen[s.name_rank] = 1;
+    seen[lr] = 1;
     const int64_t cpu_left = s.cpu_alloc_milli - s.cpu_used_milli;
     const int64_t mem_left = s.mem_alloc_mib - s.mem_used_mib;
     const int64_t pods_left = (int64_t)s.pods_alloc - s.pods_used;
@@ -1290,7 +1364,7 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
       n.gl[g] = (uint16_t)left;
     }
     for (int k = 0; k < kNumTags; ++k) tags[(size_t)i * kTagStride + k] = (uint16_t)s.tag_count[k];
-    rank2idx[s.name_rank] = i;
+    rank2idx[lr] = i;
   }
   e->h_nodes[replica].assign(nodes, nodes + e->N);
   e->total_gpus[replica] = gpus;
@@ -1521,6 +1595,107 @@ static int run_report(ksim_engine* e, int max_ev) {
   return KSIM_OK;
 }
 
+// RCCL, loaded on first use (the node-sharded mode only): the library stays loadable without it.
+struct RcclApi {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*);
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*comm_destroy)(ncclComm_t);
+  const char* (*error_string)(ncclResult_t);
+};
+static RcclApi* rccl() {
+  static RcclApi api;
+  static int state = 0;  // 0 untried, 1 ok, -1 unavailable
+  if (state == 0) {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    state = -1;
+    if (h) {
+      api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
+      api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
+      api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+      api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+      api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+      if (api.get_unique_id && api.comm_init_rank && api.all_gather && api.comm_destroy && api.error_string) state = 1;
+    }
+  }
+  return state == 1 ? &api : nullptr;
+}
+
+static void destroy_comm(ncclComm_t c) {
+  if (rccl()) (void)rccl()->comm_destroy(c);
+}
+
+// One pod step of a sharded cluster, enqueued on `st`: local Filter+Score (k_step mode 2), the
+// exchange of the shard records, the cluster-wide finish on every shard (owner binds).
+static int shard_local(ksim_engine* e, hipStream_t st, const int* base, int step_off) {
+  StepArgs a = base_args(e);
+  a.base = base;
+  a.step_off = step_off;
+  a.mode = 2;
+  a.send = e->d_send;
+  hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, st, a, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  return KSIM_OK;
+}
+static int shard_commit(ksim_engine* e, hipStream_t st, const int* base, int step_off) {
+  StepArgs a = base_args(e);
+  a.base = base;
+  a.step_off = step_off;
+  a.recv = e->d_recv;
+  a.world = e->shard_world;
+  hipLaunchKernelGGL(k_shard_commit, dim3(1), dim3(64), 0, st, a);
+  KSIM_HIP(hipGetLastError());
+  return KSIM_OK;
+}
+static int shard_exchange(ksim_engine* e, hipStream_t st) {
+  if (e->comm) {
+    const ncclResult_t r = rccl()->all_gather(e->d_send, e->d_recv, 4, ncclUint64, e->comm, st);
+    if (r != ncclSuccess) {
+      std::fprintf(stderr, "ksim: ncclAllGather failed: %s\n", rccl()->error_string(r));
+      return KSIM_EHIP;
+    }
+    return KSIM_OK;
+  }
+  KSIM_HIP(hipMemcpyAsync(e->d_recv, e->d_send, 4 * sizeof(unsigned long long), hipMemcpyDeviceToDevice, st));
+  return KSIM_OK;
+}
+
+// Sharded run over RCCL (or a world of one): steps captured K at a time into a hipGraph when the
+// stream capture accepts the collective, else enqueued eagerly.
+static int run_sharded(ksim_engine* e, int max_ev) {
+  if (e->shard_world > 1 && !e->comm) return KSIM_ESTATE;  // in-process group: ksim_shard_group_run
+  int rc;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  const int K = std::min(e->K, std::max(max_ev, 1));
+  if (hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+    bool ok = true;
+    for (int i = 0; i < K && ok; ++i)
+      ok = shard_local(e, e->stream, e->d_base, i) == KSIM_OK && shard_exchange(e, e->stream) == KSIM_OK &&
+           shard_commit(e, e->stream, e->d_base, i) == KSIM_OK;
+    if (ok) hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_base, K);
+    const hipError_t ce = hipStreamEndCapture(e->stream, &g);
+    if (ok && ce == hipSuccess && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) ge = nullptr;
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+  }
+  if (ge) {
+    KSIM_HIP(hipMemsetAsync(e->d_base, 0, sizeof(int), e->stream));
+    for (int s0 = 0; s0 < max_ev; s0 += K) {
+      if (hipGraphLaunch(ge, e->stream) != hipSuccess) { (void)hipGraphExecDestroy(ge); return KSIM_EHIP; }
+    }
+    (void)hipGraphExecDestroy(ge);
+    return KSIM_OK;
+  }
+  for (int s = 0; s < max_ev; ++s) {
+    if ((rc = shard_local(e, e->stream, nullptr, s))) return rc;
+    if ((rc = shard_exchange(e, e->stream))) return rc;
+    if ((rc = shard_commit(e, e->stream, nullptr, s))) return rc;
+  }
+  return KSIM_OK;
+}
+
 static int build_graph(ksim_engine* e) {
   if (e->graph && e->graph_R == e->R) return KSIM_OK;
   if (e->graph) { (void)hipGraphExecDestroy(e->graph); e->graph = nullptr; }
@@ -1690,7 +1865,8 @@ int ksim_engine_run(ksim_engine* e) {
   int rc = reset_state(e);
   if (rc) return rc;
   if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N * e->R, e->stream));
-  rc = e->run_mode == 1 ? run_graph(e, max_ev) : run_persistent(e, max_ev);
+  if (e->shard_world > 0) rc = run_sharded(e, max_ev);
+  else rc = e->run_mode == 1 ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
   if (e->report) {
@@ -1705,10 +1881,103 @@ int ksim_engine_run(ksim_engine* e) {
   e->last_ms = ms;
   e->last_report_ms = e->report ? rms : 0.0;
   e->last_steps = max_ev;
-  if (e->run_mode != 1) {
+  if (e->run_mode != 1 && e->shard_world == 0) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
     if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
+  }
+  return KSIM_OK;
+}
+
+int ksim_shard_comm_id(uint8_t* out) {
+  if (!out) return KSIM_EINVAL;
+  RcclApi* r = rccl();
+  if (!r) return KSIM_ENOTSUP;
+  ncclUniqueId id;
+  if (r->get_unique_id(&id) != ncclSuccess) return KSIM_EHIP;
+  std::memcpy(out, id.internal, KSIM_SHARD_ID_BYTES);
+  return KSIM_OK;
+}
+
+int ksim_engine_set_shard(ksim_engine* e, int rank, int world, int node_offset, int n_global, const uint8_t* comm_id) {
+  if (!e || world < 1 || world > 16 || rank < 0 || rank >= world || node_offset < 0 || n_global < e->N ||
+      node_offset + e->N > n_global || n_global > kMaxRank || e->R != 1)
+    return KSIM_EINVAL;
+  if (e->shard_world > 0) return KSIM_ESTATE;  // once per engine, before set_nodes
+  KSIM_HIP(hipSetDevice(e->device));
+  if (comm_id) {
+    RcclApi* r = rccl();
+    if (!r) return KSIM_ENOTSUP;
+    ncclUniqueId id;
+    std::memcpy(id.internal, comm_id, KSIM_SHARD_ID_BYTES);
+    const ncclResult_t nr = r->comm_init_rank(&e->comm, world, id, rank);
+    if (nr != ncclSuccess) {
+      std::fprintf(stderr, "ksim: ncclCommInitRank failed: %s\n", r->error_string(nr));
+      e->comm = nullptr;
+      return KSIM_EHIP;
+    }
+  }
+  KSIM_HIP(hipMalloc(&e->d_send, 4 * sizeof(unsigned long long)));
+  KSIM_HIP(hipMalloc(&e->d_recv, 4 * sizeof(unsigned long long) * (size_t)world));
+  KSIM_HIP(hipMemset(e->d_send, 0, 4 * sizeof(unsigned long long)));
+  e->shard_world = world;
+  e->shard_rank = rank;
+  e->node_off = node_offset;
+  e->n_global = n_global;
+  e->reps[0].node_off = node_offset;
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_shard_group_run(ksim_engine* const* engines, int world) {
+  if (!engines || world < 1 || world > 16) return KSIM_EINVAL;
+  ksim_engine* e0 = engines[0];
+  int max_ev = 0;
+  for (int k = 0; k < world; ++k) {
+    ksim_engine* e = engines[k];
+    if (!e || e->shard_world != world || e->shard_rank != k || e->comm || e->device != e0->device || !e->d_ev[0])
+      return KSIM_EINVAL;
+    if (e->n_events[0] != e0->n_events[0]) return KSIM_EINVAL;  // every shard sees the same events
+    max_ev = std::max(max_ev, e->n_events[0]);
+  }
+  KSIM_HIP(hipSetDevice(e0->device));
+  if (!e0->d_ptrs) KSIM_HIP(hipMalloc(&e0->d_ptrs, sizeof(unsigned long long*) * 32));
+  std::vector<unsigned long long*> ptrs(32, nullptr);
+  for (int k = 0; k < world; ++k) {
+    ptrs[k] = engines[k]->d_send;
+    ptrs[16 + k] = engines[k]->d_recv;
+  }
+  hipStream_t st = e0->stream;
+  KSIM_HIP(hipMemcpyAsync(e0->d_ptrs, ptrs.data(), sizeof(unsigned long long*) * 32, hipMemcpyHostToDevice, st));
+  for (int k = 0; k < world; ++k) {
+    ksim_engine* e = engines[k];
+    KSIM_HIP(hipStreamSynchronize(e->stream));
+    KSIM_HIP(hipMemcpyAsync(e->d_nodes, e->d_nodes_init, sizeof(NodeRec) * (size_t)e->N, hipMemcpyDeviceToDevice, st));
+    KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride, hipMemcpyDeviceToDevice, st));
+    if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N, st));
+  }
+  KSIM_HIP(hipEventRecord(e0->ev0, st));
+  int rc;
+  for (int s = 0; s < max_ev; ++s) {
+    for (int k = 0; k < world; ++k)
+      if ((rc = shard_local(engines[k], st, nullptr, s))) return rc;
+    hipLaunchKernelGGL(k_shard_gather, dim3(1), dim3(1024), 0, st, (unsigned long long* const*)e0->d_ptrs,
+                       (unsigned long long* const*)(e0->d_ptrs + 16), world);
+    KSIM_HIP(hipGetLastError());
+    for (int k = 0; k < world; ++k)
+      if ((rc = shard_commit(engines[k], st, nullptr, s))) return rc;
+  }
+  for (int k = 0; k < world; ++k)
+    if (engines[k]->report && (rc = run_report(engines[k], max_ev))) return rc;
+  KSIM_HIP(hipEventRecord(e0->ev1, st));
+  KSIM_HIP(hipStreamSynchronize(st));
+  float ms = 0;
+  KSIM_HIP(hipEventElapsedTime(&ms, e0->ev0, e0->ev1));
+  for (int k = 0; k < world; ++k) {
+    engines[k]->last_ms = ms;
+    engines[k]->last_steps = max_ev;
   }
   return KSIM_OK;
 }

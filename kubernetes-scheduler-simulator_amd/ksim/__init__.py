@@ -130,6 +130,9 @@ SIGNATURES = {
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
     "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
     "ksim_engine_last_report_ms": (C.c_int, [_VP, _P(C.c_double)]),
+    "ksim_shard_comm_id": (C.c_int, [_P(C.c_uint8)]),
+    "ksim_engine_set_shard": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _P(C.c_uint8)]),
+    "ksim_shard_group_run": (C.c_int, [_P(_VP), C.c_int]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
     "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
     "ksim_trace_free": (None, [_VP]),
@@ -339,6 +342,12 @@ class Engine:
         check(lib().ksim_engine_last_run_ms(self.h, C.byref(ms)), "last_run_ms")
         return ms.value
 
+    def set_shard(self, rank, world, node_offset, n_global, comm_id=None):
+        """Make this engine shard `rank` of a node-sharded cluster (see ksim_engine.h); call before
+        set_nodes.  comm_id: bytes from shard_comm_id() (RCCL, one process per GPU) or None."""
+        cid = None if comm_id is None else (C.c_uint8 * SHARD_ID_BYTES).from_buffer_copy(bytes(comm_id))
+        check(lib().ksim_engine_set_shard(self.h, rank, world, node_offset, n_global, cid), "set_shard")
+
     def set_report(self, enable=True):
         """Per-event cluster report (analysis.go:59-119) computed on the device by run()."""
         check(lib().ksim_engine_set_report(self.h, 1 if enable else 0), "set_report")
@@ -395,6 +404,25 @@ class Engine:
         out = (Node * self.N)()
         check(lib().ksim_engine_get_nodes(self.h, r, out), "get_nodes")
         return out
+
+
+SHARD_ID_BYTES = 128
+
+
+def shard_comm_id():
+    """An RCCL unique id (ncclGetUniqueId) for ksim_engine_set_shard; make it on one rank."""
+    buf = (C.c_uint8 * SHARD_ID_BYTES)()
+    check(lib().ksim_shard_comm_id(buf), "shard_comm_id")
+    return bytes(buf)
+
+
+def shard_group_run(engines):
+    """Run an in-process shard group (engines[k] = shard k, all on one device); returns device ms."""
+    arr = (_VP * len(engines))(*[e.h for e in engines])
+    check(lib().ksim_shard_group_run(arr, len(engines)), "shard_group_run")
+    ms = C.c_double(0)
+    check(lib().ksim_engine_last_run_ms(engines[0].h, C.byref(ms)), "last_run_ms")
+    return ms.value
 
 
 def make_pod(cpu, milli=0, num=0, mem=0, type_mask=KSIM_TYPE_ANY, cpu_nz=None):
