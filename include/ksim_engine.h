@@ -155,7 +155,9 @@ typedef struct {
     int32_t nodes_per_block;       /* k_step: nodes per workgroup (default 64) */
     int32_t steps_per_graph;       /* k_step: pod steps captured per hipGraph (default 256) */
     int32_t wgs_per_replica;       /* k_replay: workgroups per replica (0 = CUs / replicas, <= 64) */
-    int32_t run_mode;              /* ksim_engine_run: 0 = persistent k_replay, 1 = k_step per pod (hipGraph) */
+    int32_t run_mode;              /* ksim_engine_run: 0 = auto (FGD: memoised k_memo when the cluster and its pod
+                                      classes fit in LDS, else k_replay), 1 = k_step per pod (hipGraph),
+                                      2 = k_replay only, 3 = k_memo required for FGD (KSIM_ENOTSUP otherwise) */
     int32_t reserved[3];
 } ksim_config;
 

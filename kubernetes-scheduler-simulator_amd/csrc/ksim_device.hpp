@@ -205,6 +205,55 @@ KSIM_HD double go_sigmoid(double x) { return 1.0 / (1.0 + go_exp(-x)); }
 KSIM_HD int fgd_frag_score(double cur, double nw) {
   return (int)(go_sigmoid((cur - nw) / 1000) * (double)100);
 }
+// The same score as a function of delta = cur - new (the first operation of the expression above).
+KSIM_HD int fgd_score_of_delta(double delta) { return (int)(go_sigmoid(delta / 1000) * (double)100); }
+
+// fgd_score_of_delta is a step function of delta: every step of it (delta/1000, negation, go_exp,
+// 1 + e, 1 / x, * 100, truncation) is monotone, so the score is #{k in 1..100 : delta >= th[k]}
+// where th[k] is the smallest double delta with score >= k.  build_score_thresholds finds every
+// th[k] by bisection over the ordered integer image of the doubles, then checks the step on
+// +-kScoreCheckUlps doubles around each threshold (the only place where a rounding blip of
+// go_exp could matter); it returns false if any check fails, and the table must not be used.
+// th[0] = -inf, th[101] = +inf.
+constexpr int kScoreCheckUlps = 4096;
+inline long long score_key_of(double d) {
+  const long long b = __builtin_bit_cast(long long, d);
+  return b >= 0 ? b : (long long)(0x8000000000000000ull - (unsigned long long)b);  // order preserving
+}
+inline double score_double_of(long long k) {
+  return __builtin_bit_cast(double, k >= 0 ? k : (long long)(0x8000000000000000ull - (unsigned long long)k));
+}
+inline bool build_score_thresholds(double* th /* [102] */) {
+  th[0] = -__builtin_huge_val();
+  th[101] = __builtin_huge_val();
+  const long long lo0 = score_key_of(-1.0e9), hi0 = score_key_of(1.0e9);
+  if (fgd_score_of_delta(-1.0e9) != 0 || fgd_score_of_delta(1.0e9) != 100) return false;
+  for (int k = 1; k <= 100; ++k) {
+    long long lo = lo0, hi = hi0;  // score(lo) < k <= score(hi)
+    while ((unsigned long long)hi - (unsigned long long)lo > 1ull) {  // the span exceeds INT64_MAX
+      const long long mid = (long long)((unsigned long long)lo + ((unsigned long long)hi - (unsigned long long)lo) / 2);
+      if (fgd_score_of_delta(score_double_of(mid)) >= k) hi = mid;
+      else lo = mid;
+    }
+    th[k] = score_double_of(hi);
+    for (long long j = -kScoreCheckUlps; j <= kScoreCheckUlps; ++j) {
+      const int s = fgd_score_of_delta(score_double_of(hi + j));
+      if ((j < 0 && s >= k) || (j >= 0 && s < k)) return false;
+    }
+    if (k > 1 && !(th[k] > th[k - 1])) return false;
+  }
+  return true;
+}
+// The score from the table: an fp32 estimate (error far below one score unit), corrected by the
+// two thresholds around it.  Equal to fgd_score_of_delta(delta) for every finite delta.
+KSIM_HD int fgd_score_lookup(double delta, const double* th) {
+  const float e = __builtin_expf((float)delta * -0.001f);
+  int a = (int)(100.0f / (1.0f + e));
+  a = a < 0 ? 0 : (a > 100 ? 100 : a);
+  if (delta >= th[a + 1]) ++a;
+  else if (delta < th[a]) --a;
+  return a;
+}
 
 // ---------------------------------------------------------------------------
 // F(state) = NodeGpuShareFragAmountScore (frag.go:200-203)
@@ -352,6 +401,11 @@ KSIM_HD bool filter_node(const NodeV& n, const PodDev& p) {
   }
   // multi-GPU two-pointer greedy: a device can host floor(idle/milli) slots
   int slots = 0;
+  if (p.milli == kMilli) {  // whole GPUs (every multi-GPU pod of the traces): floor(idle/1000) = idle == 1000
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) slots += (g < cnt && n.gl(g) == kMilli) ? 1 : 0;
+    return slots >= p.num;
+  }
 #pragma unroll
   for (int g = 0; g < kMaxGpu; ++g)
     if (g < cnt) slots += n.gl(g) / p.milli;

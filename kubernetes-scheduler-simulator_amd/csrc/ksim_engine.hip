@@ -545,6 +545,7 @@ __global__ void k_shard_gather(unsigned long long* const* sends, unsigned long l
 
 #include "ksim_replay.hpp"
 #include "ksim_report.hpp"
+#include "ksim_memo.hpp"
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
@@ -1078,7 +1079,8 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
 struct ksim_engine {
   int device = 0;
   int N = 0, R = 0, NB = 64, bpr = 0, K = 256;
-  int run_mode = 0;        // 0: persistent k_replay, 1: one k_step launch per pod (hipGraph)
+  int run_mode = 0;        // 0: auto (k_memo for FGD when it fits, else k_replay), 1: k_step per pod (hipGraph),
+                           // 2: k_replay only, 3: k_memo required for FGD
   int wgs_req = 0;         // requested workgroups per replica (0 = auto)
   int cus = 256;
   unsigned long long* d_gran = nullptr;
@@ -1112,6 +1114,26 @@ struct ksim_engine {
   std::vector<ResultDev*> d_res;
   std::vector<int> n_events;
   std::vector<char> has_delete;  // the replica's stream has deletion events (k_replay keeps a bind history)
+  // k_memo (memoised FGD replay): per replica the distinct pod requests of its creation events
+  // (PodDev.pad = class id) and how many events each has
+  std::vector<std::vector<PodDev>> h_cls;
+  std::vector<std::vector<int>> h_cls_n;
+  std::vector<std::vector<int>> h_ev_cls;  // class of each event, -1 delete
+  PodDev* d_m_pod = nullptr;
+  int* d_m_owner = nullptr;
+  int* d_m_wgcls = nullptr;
+  int* d_m_wgref = nullptr;
+  unsigned long long* d_m_wggrp = nullptr;
+  unsigned* d_win = nullptr;
+  int* d_m_evo = nullptr;
+  double* d_th = nullptr;       // FGD score steps (build_score_thresholds), null if unusable
+  size_t m_cap[7] = {0, 0, 0, 0, 0, 0, 0};
+  struct MemoPlan* mplan = nullptr;  // the FGD replicas' k_memo plan, uploaded before the timed run
+  bool mplan_dirty = true;           // events or policies changed since the plan was made
+  bool mplan_ok = false;
+  std::vector<int> mplan_reps;
+  int mplan_max_ev = -1;
+  int last_memo = 0;  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
   int graph_R = -1;
@@ -1161,6 +1183,252 @@ static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_repla
     (void)hipFuncSetAttribute((const void*)k_replay<P, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((k_replay<P, 4>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
   }
+}
+
+// ---- k_memo planning (memoised FGD replay, ksim_memo.hpp) ----
+struct MemoPlan {
+  int K = 0, Cw = 0, nfw = 0, Cmax = 1;
+  size_t lds = 0;
+  std::vector<PodDev> pod;                  // [Rg][Cmax]
+  std::vector<int> owner;                   // [Rg][Cmax]
+  std::vector<int> wgcls, wgref;            // [Rg][K][Cw]
+  std::vector<unsigned long long> wggrp;    // [Rg][K][Cw]
+};
+
+// Classes of one replica onto K workgroups, at most Cw slots each.  Classes with the same score
+// request (cpu_nz, milli, num) stay in one workgroup (their candidate states are the same, so one
+// refresh evaluates them once); groups go largest first to the workgroup with the fewest groups.
+static bool memo_assign(const std::vector<PodDev>& cls, int K, int Cw, std::vector<int>& slot_cls, std::vector<int>& owner) {
+  std::vector<std::pair<std::vector<int32_t>, std::vector<int>>> groups;
+  for (int c = 0; c < (int)cls.size(); ++c) {
+    const std::vector<int32_t> k{cls[c].cpu_nz, cls[c].milli, cls[c].num};
+    auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& g) { return g.first == k; });
+    if (it == groups.end()) groups.push_back({k, {c}});
+    else it->second.push_back(c);
+  }
+  std::stable_sort(groups.begin(), groups.end(),
+                   [](const auto& a, const auto& b) { return a.second.size() > b.second.size(); });
+  std::vector<int> used(K, 0), ng(K, 0);
+  slot_cls.assign((size_t)K * Cw, -1);
+  owner.assign(cls.size(), -1);
+  for (const auto& g : groups) {
+    const int sz = (int)g.second.size();
+    int best = -1;
+    for (int w = 0; w < K; ++w)
+      if (used[w] + sz <= Cw && (best < 0 || ng[w] < ng[best] || (ng[w] == ng[best] && used[w] < used[best]))) best = w;
+    if (best < 0) return false;
+    for (int c : g.second) {
+      slot_cls[(size_t)best * Cw + used[best]] = c;
+      owner[c] = (best << 8) | used[best];
+      ++used[best];
+    }
+    ++ng[best];
+  }
+  return true;
+}
+
+static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPlan& pl) {
+  using namespace ksim_memo;
+  const int Rg = (int)reps.size();
+  if (Rg == 0 || e->N > kMemoMaxRank + 1) return false;
+  pl.Cmax = 1;
+  for (int r : reps) pl.Cmax = std::max(pl.Cmax, (int)e->h_cls[r].size());
+  int K = e->wgs_req > 0 ? e->wgs_req : std::min(64, e->cus / Rg);
+  if (K < 1 || Rg * K > e->cus) return false;
+  for (;;) {
+    // slots per workgroup: the smallest Cw every replica's classes pack into
+    int Cw = std::max(1, (pl.Cmax + K - 1) / K);
+    std::vector<std::vector<int>> sc(Rg), ow(Rg);
+    for (;;) {
+      bool ok = Cw <= kMaxCw;
+      for (int i = 0; ok && i < Rg; ++i) ok = memo_assign(e->h_cls[reps[i]], K, Cw, sc[i], ow[i]);
+      if (ok || Cw > kMaxCw) break;
+      ++Cw;
+    }
+    int nfw = 0;
+    if (Cw <= kMaxCw)
+      for (int f : {16, 12, 8, 4})
+        if (memo_lds(e->N, Cw, f) <= 160 * 1024) { nfw = f; break; }
+    if (nfw > 0) {
+      pl.K = K;
+      pl.Cw = Cw;
+      pl.nfw = nfw;
+      pl.lds = memo_lds(e->N, Cw, nfw);
+      pl.pod.assign((size_t)Rg * pl.Cmax, PodDev{});
+      pl.owner.assign((size_t)Rg * pl.Cmax, -1);
+      pl.wgcls.assign((size_t)Rg * K * Cw, -1);
+      pl.wgref.assign((size_t)Rg * K * Cw, 0);
+      pl.wggrp.assign((size_t)Rg * K * Cw, 0ull);
+      for (int i = 0; i < Rg; ++i) {
+        const std::vector<PodDev>& cls = e->h_cls[reps[i]];
+        for (size_t c = 0; c < cls.size(); ++c) {
+          pl.pod[(size_t)i * pl.Cmax + c] = cls[c];
+          pl.owner[(size_t)i * pl.Cmax + c] = ow[i][c];
+        }
+        for (int w = 0; w < K; ++w) {
+          const size_t o = ((size_t)i * K + w) * Cw;
+          for (int j = 0; j < Cw; ++j) {
+            const int c = sc[i][(size_t)w * Cw + j];
+            pl.wgcls[o + j] = c;
+            pl.wgref[o + j] = j;
+            if (c < 0) continue;
+            for (int j2 = 0; j2 < j; ++j2) {  // first slot with the same score request
+              const int c2 = sc[i][(size_t)w * Cw + j2];
+              if (c2 >= 0 && cls[c2].cpu_nz == cls[c].cpu_nz && cls[c2].milli == cls[c].milli && cls[c2].num == cls[c].num) {
+                pl.wgref[o + j] = j2;
+                break;
+              }
+            }
+            pl.wggrp[o + pl.wgref[o + j]] |= 1ull << j;
+          }
+        }
+      }
+      return true;
+    }
+    if (e->wgs_req > 0 || K >= 64 || Rg * (K + 1) > e->cus) return false;
+    ++K;
+  }
+}
+
+template <typename T>
+static int ensure_buf(T*& p, size_t& cap, size_t n) {
+  if (n <= cap && p) return KSIM_OK;
+  if (p) KSIM_HIP(hipFree(p));
+  p = nullptr;
+  KSIM_HIP(hipMalloc(&p, sizeof(T) * std::max(n, (size_t)1)));
+  cap = n;
+  return KSIM_OK;
+}
+
+// The FGD score steps, built once per process on the host (nullptr if the check fails: k_memo
+// then evaluates the sigmoid expression itself).
+static const double* score_table() {
+  static double th[102];
+  static const bool ok = build_score_thresholds(th);
+  return ok ? th : nullptr;
+}
+
+// Plan and upload the k_memo launch of the FGD replicas (before the timed region of a run; cached
+// until events or policies change).
+static int prepare_memo(ksim_engine* e, int max_ev) {
+  if (e->run_mode == 1 || e->run_mode == 2 || e->shard_world > 0) return KSIM_OK;
+  std::vector<int> reps;
+  for (int r = 0; r < e->R; ++r)
+    if (e->reps[r].policy == POL_FGD) reps.push_back(r);
+  if (!e->mplan_dirty && reps == e->mplan_reps && max_ev == e->mplan_max_ev) return KSIM_OK;
+  e->mplan_dirty = false;
+  e->mplan_reps = reps;
+  e->mplan_max_ev = max_ev;
+  e->mplan_ok = false;
+  if (reps.empty()) return KSIM_OK;
+  if (!e->mplan) e->mplan = new MemoPlan();
+  MemoPlan& pl = *e->mplan;
+  if (!memo_plan(e, reps, pl)) return KSIM_OK;
+  const int Rg = (int)reps.size();
+  int rc;
+  if ((rc = ensure_buf(e->d_m_pod, e->m_cap[0], pl.pod.size()))) return rc;
+  if ((rc = ensure_buf(e->d_m_owner, e->m_cap[1], pl.owner.size()))) return rc;
+  if ((rc = ensure_buf(e->d_m_wgcls, e->m_cap[2], pl.wgcls.size()))) return rc;
+  if ((rc = ensure_buf(e->d_m_wgref, e->m_cap[3], pl.wgref.size()))) return rc;
+  if ((rc = ensure_buf(e->d_m_wggrp, e->m_cap[4], pl.wggrp.size()))) return rc;
+  const int stride = std::max(max_ev, 1);
+  if ((rc = ensure_buf(e->d_win, e->m_cap[5], (size_t)Rg * stride))) return rc;
+  if ((rc = ensure_buf(e->d_m_evo, e->m_cap[6], (size_t)Rg * stride))) return rc;
+  // owner code of every event: workgroup << 16 | first slot of its score group << 8 | slot; -1 delete
+  std::vector<int> evo((size_t)Rg * stride, -1);
+  for (int gi = 0; gi < Rg; ++gi) {
+    const std::vector<int>& ec = e->h_ev_cls[reps[gi]];
+    for (size_t i = 0; i < ec.size(); ++i) {
+      if (ec[i] < 0) continue;
+      const int o = pl.owner[(size_t)gi * pl.Cmax + ec[i]];
+      const int w = o >> 8, slot = o & 0xff;
+      const int ref = pl.wgref[((size_t)gi * pl.K + w) * pl.Cw + slot];
+      evo[(size_t)gi * stride + i] = (w << 16) | (ref << 8) | slot;
+    }
+  }
+  hipStream_t st = e->stream;
+  KSIM_HIP(hipMemcpyAsync(e->d_m_evo, evo.data(), sizeof(int) * evo.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_pod, pl.pod.data(), sizeof(PodDev) * pl.pod.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_owner, pl.owner.data(), sizeof(int) * pl.owner.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_wgcls, pl.wgcls.data(), sizeof(int) * pl.wgcls.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_wgref, pl.wgref.data(), sizeof(int) * pl.wgref.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_wggrp, pl.wggrp.data(), sizeof(unsigned long long) * pl.wggrp.size(),
+                          hipMemcpyHostToDevice, st));
+  if (!e->d_th && score_table()) {
+    KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
+    KSIM_HIP(hipMemcpyAsync(e->d_th, score_table(), sizeof(double) * 102, hipMemcpyHostToDevice, st));
+  }
+  KSIM_HIP(hipStreamSynchronize(st));  // the host vectors are pageable and short-lived
+  e->mplan_ok = true;
+  return KSIM_OK;
+}
+
+static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, int max_ev) {
+  int rc;
+  hipStream_t st = e->stream;
+  const int stride = std::max(max_ev, 1);
+  KSIM_HIP(hipMemsetAsync(e->d_win, 0, sizeof(unsigned) * (size_t)Rg * stride, st));
+  ksim_memo::MemoArgs ma;
+  ma.reps = e->d_reps;
+  ma.rep_list = e->d_replist + first;
+  ma.N = e->N;
+  ma.K = pl.K;
+  ma.Cw = pl.Cw;
+  ma.nfw = pl.nfw;
+  ma.Cmax = pl.Cmax;
+  ma.cls_pod = e->d_m_pod;
+  ma.cls_owner = e->d_m_owner;
+  ma.wg_cls = e->d_m_wgcls;
+  ma.wg_ref = e->d_m_wgref;
+  ma.wg_grp = e->d_m_wggrp;
+  ma.ev_owner = e->d_m_evo;
+  ma.th = e->d_th;
+  ma.win = e->d_win;
+  ma.win_stride = stride;
+  ma.fail = e->d_fail;
+  ma.prof = nullptr;
+  const char* pe = std::getenv("KSIM_PROFILE");
+  const bool profile = pe && pe[0] == '1';
+  if (profile) {
+    if ((rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)Rg * pl.K * ksim_memo::kProfPhases))) return rc;
+    KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
+    ma.prof = e->d_prof;
+  }
+  KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
+  hipLaunchKernelGGL(ksim_memo::k_memo, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  if (profile) {
+    KSIM_HIP(hipStreamSynchronize(st));
+    const int nb = Rg * pl.K, P = ksim_memo::kProfPhases;
+    std::vector<unsigned long long> h((size_t)nb * P);
+    KSIM_HIP(hipMemcpy(h.data(), e->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    static const char* names[] = {"init", "A:crit-F+list", "syncA", "B:publish", "B:eval", "syncB", "C:keys", "top2",
+                                  "poll+bind", "end-sync"};
+    std::fprintf(stderr, "ksim memo profile: %d workgroups (K=%d Cw=%d nfw=%d), %d steps; us/step mean [max]:", nb, pl.K,
+                 pl.Cw, pl.nfw, max_ev);
+    double init = 0;
+    for (int b = 0; b < nb; ++b) init += (double)h[(size_t)b * P] / 1e5;
+    std::fprintf(stderr, " (init %.3f ms)", init / nb);
+    for (int ph = 1; ph < 10; ++ph) {
+      double sum = 0, mx = 0;
+      for (int b = 0; b < nb; ++b) {
+        const double us = (double)h[(size_t)b * P + ph] / 100.0 / std::max(max_ev, 1);
+        sum += us;
+        mx = std::max(mx, us);
+      }
+      std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / nb, mx);
+    }
+    double cyc = 0, tick = 0;
+    for (int b = 0; b < nb; ++b) { cyc += (double)h[(size_t)b * P + 10]; tick += (double)h[(size_t)b * P + 11]; }
+    for (int ph = 12; ph < 14; ++ph) {
+      double sum = 0;
+      for (int b = 0; b < nb; ++b) sum += (double)h[(size_t)b * P + ph] / 100.0 / std::max(max_ev, 1);
+      std::fprintf(stderr, " %s %.3f;", ph == 12 ? "listwave-A" : "listwave-C", sum / nb);
+    }
+    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nb / 1e5);
+    std::fprintf(stderr, "\n");
+  }
+  return KSIM_OK;
 }
 
 extern "C" {
@@ -1254,6 +1522,9 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
   e->has_delete.assign(n_replicas, 0);
+  e->h_cls.resize(n_replicas);
+  e->h_cls_n.resize(n_replicas);
+  e->h_ev_cls.resize(n_replicas);
   e->nt.assign(n_replicas, 0);
   e->d_snap.assign(n_replicas, nullptr);
   e->d_prev.assign(n_replicas, nullptr);
@@ -1292,13 +1563,15 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (auto p : e->d_rep) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
-                  e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs};
+                  e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
+                  e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
   if (e->comm) destroy_comm(e->comm);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e->mplan;
   delete e;
 }
 
@@ -1422,6 +1695,7 @@ int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp,
 }
 
 int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed) {
+  if (e) e->mplan_dirty = true;
   if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
   if (policy < POL_FGD || policy > POL_RANDOM || gpusel < SEL_BEST || gpusel > SEL_FGD) return KSIM_ENOTSUP;
   e->reps[replica].policy = policy;
@@ -1524,12 +1798,46 @@ int ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int 
 }
 
 int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events, int n) {
+  if (e) e->mplan_dirty = true;
   if (!e || replica < 0 || replica >= e->R || n < 0 || (n > 0 && !events)) return KSIM_EINVAL;
   std::vector<PodDev> h(n);
   for (int i = 0; i < n; ++i) {
     int rc = to_pod_dev(events[i], &h[i]);
     if (rc) return rc;
     if ((h[i].flags & kPodDelete) && (h[i].ref < 0 || h[i].ref >= i)) return KSIM_EINVAL;
+  }
+  // pod classes for k_memo: the distinct Filter + Score requests of the creation events
+  {
+    std::vector<PodDev>& cls = e->h_cls[replica];
+    std::vector<int>& cn = e->h_cls_n[replica];
+    cls.clear();
+    cn.clear();
+    std::vector<std::pair<std::vector<int32_t>, int>> seen;  // small: linear probe by sorted insert
+    auto key_of = [](const PodDev& q) {
+      return std::vector<int32_t>{q.cpu_req, q.cpu_nz, q.mem, q.milli, q.num, (int32_t)q.tmask};
+    };
+    for (int i = 0; i < n; ++i) {
+      if (h[i].flags & kPodDelete) { h[i].pad = -1; continue; }
+      const std::vector<int32_t> k = key_of(h[i]);
+      auto it = std::lower_bound(seen.begin(), seen.end(), k,
+                                 [](const std::pair<std::vector<int32_t>, int>& a, const std::vector<int32_t>& b) {
+                                   return a.first < b;
+                                 });
+      int id;
+      if (it != seen.end() && it->first == k) {
+        id = it->second;
+      } else {
+        id = (int)cls.size();
+        seen.insert(it, {k, id});
+        cls.push_back(h[i]);
+        cls.back().pad = id;
+        cn.push_back(0);
+      }
+      h[i].pad = id;
+      ++cn[id];
+    }
+    e->h_ev_cls[replica].resize(n);
+    for (int i = 0; i < n; ++i) e->h_ev_cls[replica][i] = h[i].pad;
   }
   KSIM_HIP(hipSetDevice(e->device));
   if (e->d_ev[replica]) { KSIM_HIP(hipFree(e->d_ev[replica])); e->d_ev[replica] = nullptr; }
@@ -1763,6 +2071,7 @@ static size_t replay_lds(int S) {  // S real slots + the virtual node
          (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double) + sizeof(int));
 }
 
+
 // One k_replay launch per policy present (the kernel is specialised on the policy);
 // launches of different policies run back to back on the engine stream.
 static int run_persistent(ksim_engine* e, int max_ev) {
@@ -1781,8 +2090,25 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   int first = 0;
+  e->last_memo = 0;
   for (const auto& gp : groups) {
     const int Rg = gp.second;
+    // FGD: the memoised replay when the cluster and the classes fit (run_mode 0 / 3)
+    if (gp.first == POL_FGD && e->run_mode != 2) {
+      if (e->mplan_ok) {  // prepared by prepare_memo (the FGD replicas are the first group of `order`)
+        const MemoPlan& pl = *e->mplan;
+        const int rc = launch_memo(e, pl, Rg, first, max_ev);
+        if (rc) return rc;
+        e->last_K = pl.K;
+        e->last_groups = (int)groups.size();
+        e->last_memo += Rg;
+        first += Rg;
+        if (profile) std::fprintf(stderr, "ksim memo: %d replicas, K=%d, Cw=%d, F waves %d, LDS %zu B\n", Rg, pl.K, pl.Cw,
+                                  pl.nfw, pl.lds);
+        continue;
+      }
+      if (e->run_mode == 3) return KSIM_ENOTSUP;
+    }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
     while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && Rg * (K + 1) <= e->cus) {
@@ -1861,8 +2187,10 @@ int ksim_engine_run(ksim_engine* e) {
     max_ev = std::max(max_ev, e->n_events[r]);
   }
   KSIM_HIP(hipSetDevice(e->device));
+  int rc = prepare_memo(e, max_ev);
+  if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
-  int rc = reset_state(e);
+  rc = reset_state(e);
   if (rc) return rc;
   if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N * e->R, e->stream));
   if (e->shard_world > 0) rc = run_sharded(e, max_ev);

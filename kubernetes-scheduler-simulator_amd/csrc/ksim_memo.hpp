@@ -1,0 +1,651 @@
+// ksim_memo.hpp -- memoised whole-trace FGD replay (k_memo).
+//
+// Why: a pod step changes ONE node (the Bind of the winner, or a delete), and the FGD score of a
+// node for a pod depends only on that node's state and on the pod's request.  A trace has few
+// distinct requests (openb default: 151 pod classes over ~10.9k events), so the score of every
+// (pod class, node) pair is kept as a packed 32-bit key and only the changed node's keys are
+// recomputed per step; the per-pod argmax over all N nodes reads memoised keys instead of
+// re-running Filter + Score on N nodes (fgd_score.go:44-156, frag.go:148-203).  Results are the
+// same bits as k_replay / k_step / the oracle (the same device functions produce every key).
+//
+// Layout: replica r is run by K co-resident 1024-thread workgroups.  EVERY workgroup keeps the
+// whole cluster state in LDS (N x 32 B, node slot = name rank) and owns Cw of the replica's pod
+// classes (host assignment, classes with the same score request kept together), with the key of
+// every node for each owned class in LDS (Cw x N x 4 B).
+//
+// Per pod step s (class c_s, owner workgroup o_s), with d = the node changed by event s-1:
+//   1. every workgroup refreshes the keys of d for its classes: wave 0 lists the states to
+//      evaluate (d's current state + one candidate per GPU value class / the Sub state, per
+//      distinct score request that some owned class finds feasible; c_s's first), every wave
+//      evaluates one state's F (wave_F: lane t classifies typical pod t, lanes 0-5 fold the six
+//      bins of F in typical-pod order), wave 0 turns them into keys and updates counts;
+//   2. o_s takes the winner = max(top-2 of c_s's keys with d excluded, d's fresh key), runs
+//      Reserve's GPU selector and publishes {node, mask} as one 4-byte granule win[s] (written
+//      once per run, so no slot reuse and no tag), and writes the result;
+//   3. the owner of the NEXT create event's class computes that class's top-2 keys (all fresh
+//      but the node step s will change -- the exclusion in 2 handles it);
+//   4. every workgroup reads win[s] (relaxed agent-scope poll) and applies the Bind to its LDS
+//      copy of the cluster; that node is the next step's d.
+// Delete events need no exchange: every workgroup reads the creation's granule and unbinds.
+// Every spin is bounded; a timeout sets *fail and stops the replica on every workgroup.
+#pragma once
+
+namespace ksim_memo {
+
+using namespace ksim;
+
+constexpr int kMBlock = 1024;
+constexpr int kMWaves = kMBlock / 64;
+constexpr int kMaxCw = 64;                 // class slots per workgroup (one wave-0 lane each)
+constexpr int kMaxItems = 1 + 8 * kMaxCw;  // F evaluations per refresh: current + 8 per request
+constexpr int kFoldRows = 6;               // Q1, Q2 (+Q3 frag), Q4, XL, XR, NA
+constexpr int kFoldBuf = kFoldRows * 64;   // doubles per evaluating wave
+constexpr int kEvBuf = 128;
+constexpr unsigned kSpinLimit = 1u << 22;
+
+struct MemoArgs {
+  ReplicaDev* reps;
+  const int* rep_list;   // replica of each group of K workgroups
+  int N, K, Cw;
+  int nfw;               // waves with a fold buffer (F evaluators)
+  int Cmax;              // class table stride
+  const PodDev* cls_pod;     // [launch replica][Cmax] representative request of each class
+  const int* cls_owner;      // [launch replica][Cmax] (workgroup << 8) | slot
+  const int* wg_cls;         // [launch replica][K][Cw] class of each slot, -1 empty
+  const int* wg_ref;         // [launch replica][K][Cw] first slot with the same score request
+  const unsigned long long* wg_grp;  // [launch replica][K][Cw] slots sharing the request (on the first)
+  const int* ev_owner;       // [launch replica][win_stride] owner code of each event's class, -1 delete
+  const double* th;          // [102] FGD score steps, or null: the direct sigmoid expression
+  unsigned* win;             // [launch replica][win_stride] winner granules, zeroed before launch
+  int win_stride;
+  int* fail;
+  unsigned long long* prof;  // optional [R*K][kProfPhases] (KSIM_PROFILE=1)
+};
+constexpr int kProfPhases = 16;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C
+
+struct __align__(16) MemoShared {
+  PodDev ev[kEvBuf];
+  int evo[kEvBuf];    // owner code of each staged event: workgroup << 16 | first slot of its group << 8 | slot
+  PodDev cls[kMaxCw];
+  TypDev tp[kMaxTypical];
+  NodeRec dnode;      // the record of the node the previous event changed (d)
+  double th[104];     // FGD score steps (build_score_thresholds), th[0] = -inf, th[101] = +inf
+  unsigned long long grp[kMaxCw];
+  int cls_id[kMaxCw];
+  int sc_ref[kMaxCw];
+  int cnt[kMaxCw];
+  unsigned ikey[kMaxItems + 3];
+  double F[kMaxItems + 1];
+  double Fc[10];      // the step's own class: F of d's current state and of its candidates (waves 0-8)
+  uint8_t item_code[kMaxItems + 7];
+  uint8_t item_slot[kMaxItems + 7];
+  unsigned wtop[kMWaves][2];
+  unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
+  int nitems;
+  int dirty;          // node (rank) changed by the previous event, -1 none
+  int stop;
+  unsigned pay;       // this step's granule (its owner)
+  unsigned long long prof[kProfPhases];
+};
+static_assert(sizeof(MemoShared) % 16 == 0, "keep the node records 16-B aligned");
+
+// Packed 32-bit key of (pod class, node): [30:24] score + 1 | [23:12] 4095 - rank | [11:8] gpu
+// field (15 - g for a share pod placed on GPU g, 0 otherwise) | 0.  0 = infeasible.  Max key =
+// max score, ties to the smallest name (selectHost, generic_scheduler.go:187-212); for one node
+// the max over its candidates keeps the lowest GPU index (fgd_score.go:128).
+constexpr int kMemoMaxRank = 0xFFF;
+KSIM_HD unsigned pack_key32(int score, int rank, int gf) {
+  return ((unsigned)(score + 1) << 24) | ((unsigned)(kMemoMaxRank - rank) << 12) | ((unsigned)gf << 8);
+}
+KSIM_HD int key32_score(unsigned k) { return (int)(k >> 24) - 1; }
+KSIM_HD int key32_rank(unsigned k) { return kMemoMaxRank - (int)((k >> 12) & 0xFFFu); }
+KSIM_HD int key32_gpu(unsigned k) {
+  const int gf = (int)((k >> 8) & 0xFu);
+  return gf ? 15 - gf : -1;
+}
+
+// Granule of step s: bit 0 written | [23:8] rank + 1 (0: nothing bound) | [31:24] GPU mask.
+KSIM_HD unsigned pack_pay(int rank, int mask) {
+  return 1u | ((unsigned)(rank + 1) << 8) | ((unsigned)(mask & 0xff) << 24);
+}
+
+__device__ __forceinline__ unsigned gload32(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore32(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Bit g set iff GPU g has at least m milli left (packed u16 compares; the GPUs beyond gpu_cnt hold 0).
+// first_of_class(n, m) == first_of_class(n, 0) & ge_mask(n, m).
+__device__ __forceinline__ unsigned ge_mask(const NodeV& n, int m) {
+  using ksim_replay::u16x2;
+  const uint32_t mp = (uint32_t)m * 0x10001u;
+  unsigned lt = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u16x2 d = (u16x2)(__builtin_bit_cast(u16x2, n.g[i]) - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};
+    const uint32_t x = __builtin_bit_cast(uint32_t, d);
+    lt |= ((x & 1u) | ((x >> 15) & 2u)) << (2 * i);
+  }
+  return ~lt & 0xFFu;
+}
+
+// Top-2 merge of two disjoint sets of distinct keys.
+__device__ __forceinline__ void merge2(unsigned& a1, unsigned& a2, unsigned b1, unsigned b2) {
+  const unsigned lo = a1 < b1 ? a1 : b1, hi2 = a2 > b2 ? a2 : b2;
+  a1 = a1 > b1 ? a1 : b1;
+  a2 = lo > hi2 ? lo : hi2;
+}
+template <int kCtrl>
+__device__ __forceinline__ void merge2_dpp(unsigned& a1, unsigned& a2) {
+  merge2(a1, a2, (unsigned)ksim_replay::dpp_i<kCtrl>((int)a1), (unsigned)ksim_replay::dpp_i<kCtrl>((int)a2));
+}
+// Top-2 over the 64 lanes (every lane active): quad xor 1, xor 2, row half mirror, row mirror, then
+// the four rows -- the same DPP pattern as wave_max_dpp.
+__device__ __forceinline__ void wave_top2(unsigned& a1, unsigned& a2) {
+  merge2_dpp<0xB1>(a1, a2);
+  merge2_dpp<0x4E>(a1, a2);
+  merge2_dpp<0x141>(a1, a2);
+  merge2_dpp<0x140>(a1, a2);
+  unsigned r1 = (unsigned)__builtin_amdgcn_readlane((int)a1, 0), r2 = (unsigned)__builtin_amdgcn_readlane((int)a2, 0);
+  merge2(r1, r2, (unsigned)__builtin_amdgcn_readlane((int)a1, 16), (unsigned)__builtin_amdgcn_readlane((int)a2, 16));
+  merge2(r1, r2, (unsigned)__builtin_amdgcn_readlane((int)a1, 32), (unsigned)__builtin_amdgcn_readlane((int)a2, 32));
+  merge2(r1, r2, (unsigned)__builtin_amdgcn_readlane((int)a1, 48), (unsigned)__builtin_amdgcn_readlane((int)a2, 48));
+  a1 = r1;
+  a2 = r2;
+}
+
+// Key of one (node, class) pair, one thread (initial fill).  Same functions, same order as the
+// k_replay evaluation: Filter, then F of the current state and of each candidate state.
+__device__ __forceinline__ unsigned memo_key_scalar(const NodeV& n, const PodDev& p, double F0, int rank,
+                                                    const ReplicaDev& rp, const TypDev* __restrict__ tp) {
+  if (!filter_node(n, p)) return 0u;
+  if (!is_share_pod(p)) {
+    const double Fk = eval_fgd_item(n, 9, p, rp, tp);  // fgd_score.go:137-141 NodeResource.Sub
+    return pack_key32(fgd_frag_score(F0, Fk), rank, 0);
+  }
+  unsigned bk = pack_key32(0, rank, 0);  // feasible with no fitting GPU (milli 0, GPU-less node)
+  const unsigned fm = first_of_class(n, p.milli);
+  for (int g = 0; g < kMaxGpu; ++g) {
+    if ((fm >> g) & 1u) {
+      const double Fk = eval_fgd_item(n, 1 + g, p, rp, tp);  // fgd_score.go:111-118
+      const unsigned k = pack_key32(fgd_frag_score(F0, Fk), rank, 15 - g);
+      bk = k > bk ? k : bk;
+    }
+  }
+  return bk;
+}
+
+// F = NodeGpuShareFragAmountScore of one state (frag.go:148-203, 411-418, 460-493) by ONE wave:
+// lane t classifies typical pod t (64 per round) into (row, value) exactly as frag_F does, writes
+// its value into its row of the wave's fold buffer (zeros elsewhere), and lane b < 6 then folds
+// row b in typical-pod order.  Rows: 0 Q1, 1 Q2 (+ Q3's frag part), 2 Q4, 3 XL, 4 XR, 5 NA.
+// Every bin receives the same sequence of fp64 adds as frag_F's (+0.0 for the typical pods that
+// do not touch it, the identity on these non-negative sums), and F adds the bins in index order
+// 0,1,3,4,5,6, so F is bit-identical.  All lanes return F.
+__device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int total, uint32_t typebit, bool typed,
+                                         const TypDev* ltp, int ncpu, int nt, int lane, double* buf) {
+  using ksim_replay::u16x2;
+  const double dtot = (double)total;
+  double acc = 0.0;
+  for (int t0 = 0; t0 < nt; t0 += 64) {
+    const int t = t0 + lane;
+    int row = -1;
+    double val = 0.0;
+    if (t < nt) {
+      const TypDev e = ltp[t];
+      const bool cpu_ok = cpuL >= e.cpu;
+      const double x = e.freq * dtot;  // freq * float64(gpuMilliLeftTotal)
+      if (t < ncpu) {
+        row = cpu_ok ? 3 : 4;  // GetNodePodFrag case 1 (frag.go:463-469)
+        val = x;
+      } else {
+        const uint32_t mp = (uint32_t)e.milli * 0x10001u;
+        uint32_t frag = 0u, nlt = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
+          const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
+          frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+          nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
+        }
+        const bool gpu_ok = kMaxGpu - (int)nlt >= e.num_eff;      // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+        const bool acc_ok = !typed || (e.tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+        row = !acc_ok ? 5 : (cpu_ok ? 1 : (gpu_ok ? 2 : 0));
+        val = (acc_ok && cpu_ok && gpu_ok) ? e.freq * (double)(int)frag : x;  // Q3: frag part to Q2
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kFoldRows; ++b) buf[b * 64 + lane] = row == b ? val : 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // row b folds its columns in order: XL / XR (rows 3, 4) only hold CPU-only typical pods
+    // [0, cend), the other rows only GPU ones [cend, tn); every other cell is +0.0, so reading a
+    // pair that straddles a range end adds an exact zero
+    const int tn = min(64, nt - t0);
+    const int cend = min(max(ncpu - t0, 0), tn);
+    if (lane < kFoldRows) {
+      const bool cpu_row = lane == 3 || lane == 4;
+      const int lo = cpu_row ? 0 : (cend >> 1), hi = cpu_row ? ((cend + 1) >> 1) : ((tn + 1) >> 1);
+      const double2* rw = reinterpret_cast<const double2*>(buf + lane * 64);
+#pragma unroll 8
+      for (int k = lo; k < hi; ++k) {
+        const double2 v = rw[k];
+        acc += v.x;
+        acc += v.y;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // FragAmountSumExceptQ3 (frag.go:411-418): Q1 + Q2 + Q4 + XL + XR + NA, in this order
+  double out = 0.0;
+  out += readlane_d(acc, 0);
+  out += readlane_d(acc, 1);
+  out += readlane_d(acc, 2);
+  out += readlane_d(acc, 3);
+  out += readlane_d(acc, 4);
+  out += readlane_d(acc, 5);
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// k_memo.  Dynamic LDS: MemoShared | NodeRec nodes[N] (slot = name rank) | u32 keys[Cw][N] |
+// f64 fold buffers [nfw][6][64] (the initial F of every node at start-up) | i32 last[N] (cluster
+// report: the last event that changed each node).
+// Per step the phases are (barriers between):
+//   A  owner of the step's class: waves 0-8 evaluate F of d's current state and of its candidate
+//      states for that class (no list: wave k <-> candidate k) -- the critical path;
+//      list wave (15): the work list of d's other requests;
+//   B  owner: wave 0 scores, updates the class group's keys, takes the winner and publishes;
+//      the other waves evaluate the listed states;
+//   C  list wave: the listed requests' keys; then (next step's owner) top-2; then wave 0 reads
+//      the step's granule and applies the Bind.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __restrict__ tp_all) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  MemoShared& sh = *reinterpret_cast<MemoShared*>(smem);
+  constexpr int kLW = kMWaves - 1;  // the list wave
+  const int gi = (int)blockIdx.x / a.K;  // replica position in this launch
+  const int r = a.rep_list[gi];
+  const int w = (int)blockIdx.x % a.K;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const ReplicaDev rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
+  const int N = a.N, Cw = a.Cw;
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
+  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(MemoShared));
+  unsigned* s_keys = reinterpret_cast<unsigned*>(s_nodes + N);
+  double* s_fold = reinterpret_cast<double*>(reinterpret_cast<char*>(s_keys) + (((size_t)Cw * N * 4 + 15) & ~(size_t)15));
+  int* s_last = reinterpret_cast<int*>(reinterpret_cast<char*>(s_fold) +
+                                       std::max((size_t)a.nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15));
+  const PodDev* cls_pod = a.cls_pod + (size_t)gi * a.Cmax;
+  const size_t wgo = ((size_t)gi * a.K + w) * Cw;
+  unsigned* win = a.win + (size_t)gi * a.win_stride;
+  const int* evo = a.ev_owner + (size_t)gi * a.win_stride;
+  const bool is_w0 = w == 0;
+
+  // ---- start-up: the cluster in rank order, the owned classes, the typical table
+  for (int i = tid; i < N; i += kMBlock) {
+    store_node(&s_nodes[i], load_node(rp.nodes + rank2idx[i]));
+    s_last[i] = -1;
+  }
+  for (int j = tid; j < kMaxCw; j += kMBlock) {
+    const int cid = j < Cw ? a.wg_cls[wgo + j] : -1;
+    sh.cls_id[j] = cid;
+    sh.sc_ref[j] = j < Cw ? a.wg_ref[wgo + j] : j;
+    sh.grp[j] = j < Cw ? a.wg_grp[wgo + j] : 0ull;
+    sh.cnt[j] = 0;
+    if (cid >= 0) sh.cls[j] = cls_pod[cid];
+    else reinterpret_cast<uint4*>(&sh.cls[j])[0] = reinterpret_cast<uint4*>(&sh.cls[j])[1] = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < rp.nt * 2; i += kMBlock)
+    reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
+  if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; }
+  // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
+  const bool prof = a.prof != nullptr;
+  if (prof && tid < kProfPhases) sh.prof[tid] = 0ull;
+  unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto mark = [&](int ph) {
+    if (prof && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - t_last;
+      t_last = t;
+    }
+  };
+  __syncthreads();
+  // F of every node's initial state, then the key of every (owned class, node) pair
+  double* s_F0 = s_fold;
+  for (int i = tid; i < N; i += kMBlock) s_F0[i] = eval_fgd_item(load_node(&s_nodes[i]), 0, PodDev{}, rp, tp);
+  __syncthreads();
+  for (int x = tid; x < Cw * N; x += kMBlock) {
+    const int j = x / N, i = x - j * N;
+    unsigned k = 0u;
+    if (sh.cls_id[j] >= 0) k = memo_key_scalar(load_node(&s_nodes[i]), sh.cls[j], s_F0[i], i, rp, tp);
+    s_keys[x] = k;
+  }
+  __syncthreads();
+  for (int j = wv; j < Cw; j += kMWaves) {  // feasible nodes per class
+    int c = 0;
+    for (int i0 = 0; i0 < N; i0 += 64) c += __popcll(__ballot(i0 + lane < N && s_keys[(size_t)j * N + i0 + lane] != 0u));
+    if (lane == 0) sh.cnt[j] = c;
+  }
+
+  // top-2 keys of class slot `slot` over all nodes (every thread of the workgroup calls it)
+  auto top2 = [&](int slot) {
+    const unsigned* kr = s_keys + (size_t)slot * N;
+    unsigned a1 = 0u, a2 = 0u;
+    for (int i = tid; i < N; i += kMBlock) {
+      const unsigned k = kr[i];
+      if (k > a1) { a2 = a1; a1 = k; } else if (k > a2) { a2 = k; }
+    }
+    wave_top2(a1, a2);
+    if (lane == 0) { sh.wtop[wv][0] = a1; sh.wtop[wv][1] = a2; }
+    __syncthreads();
+    if (wv == 0) {
+      a1 = lane < kMWaves ? sh.wtop[lane][0] : 0u;
+      a2 = lane < kMWaves ? sh.wtop[lane][1] : 0u;
+      wave_top2(a1, a2);
+      if (lane == 0) { sh.t2a = a1; sh.t2b = a2; }
+    }
+  };
+  const bool use_th = a.th != nullptr;
+  if (use_th)
+    for (int i = tid; i < 102; i += kMBlock) sh.th[i] = a.th[i];
+  // the first create event's class
+  {
+    int s0 = 0;
+    while (s0 < rp.n_events && evo[s0] < 0) ++s0;
+    __syncthreads();
+    if (s0 < rp.n_events && (evo[s0] >> 16) == w) top2(evo[s0] & 0xff);
+  }
+  __syncthreads();
+  mark(0);
+  auto score_of = [&](double delta) { return use_th ? fgd_score_lookup(delta, sh.th) : fgd_score_of_delta(delta); };
+
+  // list wave, lane j <-> class slot j: the slot's request and group, kept in registers
+  PodDev lq{};
+  bool l_valid = false, l_rep = false, l_share = false;
+  int l_ref = 0;
+  unsigned long long l_grp = 0ull;
+  if (wv == kLW) {
+    l_valid = lane < Cw && sh.cls_id[lane] >= 0;
+    if (l_valid) lq = sh.cls[lane];
+    l_ref = sh.sc_ref[lane];
+    l_grp = sh.grp[lane];
+    l_rep = l_valid && l_ref == lane;
+    l_share = is_share_pod(lq);
+  }
+  // list-wave state of the current refresh
+  bool r_feas = false, r_need = false, r_skip = false;
+  int r_base = 0, r_ni = 0;
+
+  for (int step = 0; step < rp.n_events; ++step) {
+    const int eb = step & (kEvBuf - 1);
+    if (eb == 0) {
+      const int ne = min(kEvBuf, rp.n_events - step);
+      const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+      for (int i = tid; i < ne * 2; i += kMBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
+      for (int i = tid; i < ne; i += kMBlock) sh.evo[i] = evo[step + i];
+      __syncthreads();
+    }
+    // one LDS round trip: the event, its owner code, d and d's record
+    const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
+    const int oc = __builtin_amdgcn_readfirstlane(sh.evo[eb]);
+    const int d = __builtin_amdgcn_readfirstlane(sh.dirty);
+    const NodeV dn = ksim_replay::uniform_node(&sh.dnode);
+    const bool del = (p.flags & kPodDelete) != 0u;
+    const bool own = oc >= 0 && (oc >> 16) == w;
+    const int oslot = own ? (oc & 0xff) : -1;
+    const int crep = own ? ((oc >> 8) & 0xff) : -1;
+
+    // ---- A: the step's own class on d (owner, waves 0-8) | the list of d's other requests (list wave)
+    if (d >= 0) {
+      if (own && wv <= 8) {
+        const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
+        int code = -1;
+        if (wv == 0) code = 0;
+        else if (is_share_pod(cp)) code = (((first_of_class(dn, 0) & ge_mask(dn, cp.milli)) >> (wv - 1)) & 1u) ? wv : -1;
+        else if (wv == 1) code = 9;
+        if (code >= 0) {
+          int cpuL, total;
+          uint32_t gs[4];
+          ksim_replay::fgd_candidate(dn, code, cp, &cpuL, gs, &total);
+          const double F = wave_F(cpuL, gs, total, 1u << dn.gpu_type(), rp.typed != 0, sh.tp, rp.ncpu, rp.nt, lane,
+                                  s_fold + (size_t)wv * kFoldBuf);
+          if (lane == 0) sh.Fc[wv] = F;
+        }
+      }
+      if (wv == kLW) {
+        const unsigned long long tl0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        r_skip = own && l_valid && l_ref == crep;  // the step's own group: its keys are set in B
+        r_feas = l_valid && !r_skip && filter_node(dn, lq);
+        const unsigned long long FM = __ballot(r_feas);
+        r_need = l_rep && !r_skip && (FM & l_grp) != 0ull;
+        unsigned cm = 0u;
+        if (r_need) cm = l_share ? (first_of_class(dn, 0) & ge_mask(dn, lq.milli)) : 0x100u;
+        r_ni = __popc(cm);
+        // exclusive prefix of r_ni over the lanes (r_ni <= 8: four bit planes)
+        int excl = 0, tot = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const unsigned long long m = __ballot((r_ni >> b) & 1);
+          excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+          tot += __popcll(m) << b;
+        }
+        const int i0 = own ? 0 : 1;  // item 0 = d's current state unless the owner evaluated it (Fc[0])
+        r_base = i0 + excl;
+        int o = r_base;
+        unsigned mm = cm;
+        while (mm) {
+          const int g = __builtin_ctz(mm);
+          mm &= mm - 1u;
+          sh.item_code[o] = (uint8_t)(l_share ? 1 + g : 9);
+          sh.item_slot[o] = (uint8_t)lane;
+          ++o;
+        }
+        if (lane == 0) {
+          if (!own) {
+            sh.item_code[0] = 0;
+            sh.item_slot[0] = 0;
+          }
+          sh.nitems = tot > 0 ? i0 + tot : 0;
+          if (prof) sh.prof[12] += __builtin_amdgcn_s_memrealtime() - tl0;
+        }
+      }
+    }
+    mark(1);
+    __syncthreads();
+    mark(2);
+    // ---- B: the owner publishes the step's winner (wave 0); the listed states are evaluated
+    if (own && wv == 0) {
+      unsigned fresh = 0u;
+      if (d >= 0) {
+        const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
+        const bool cshare = is_share_pod(cp);
+        const unsigned fm = cshare ? (first_of_class(dn, 0) & ge_mask(dn, cp.milli)) : 0u;
+        const bool has = lane >= 1 && lane <= 8 && (cshare ? ((fm >> (lane - 1)) & 1u) != 0u : lane == 1);
+        int k = 0;
+        if (has) k = (int)pack_key32(score_of(sh.Fc[0] - sh.Fc[lane]), d, cshare ? 15 - (lane - 1) : 0);
+        unsigned gk = (unsigned)ksim_replay::wave_max_dpp(k);
+        const unsigned z = pack_key32(0, d, 0);  // feasible with no fitting GPU
+        gk = gk > z ? gk : z;
+        const int j = lane;
+        if (j < Cw && ((sh.grp[crep] >> j) & 1ull)) {
+          const PodDev q = sh.cls[j];
+          const unsigned nk = filter_node(dn, q) ? gk : 0u;
+          unsigned* kp = s_keys + (size_t)j * N + d;
+          const unsigned old = *kp;
+          *kp = nk;
+          sh.cnt[j] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        fresh = s_keys[(size_t)oslot * N + d];
+      }
+      const unsigned t2a = sh.t2a, t2b = sh.t2b;
+      const unsigned ex = (d >= 0 && t2a != 0u && key32_rank(t2a) == d) ? t2b : t2a;
+      const unsigned W = fresh > ex ? fresh : ex;
+      const int nfeas = sh.cnt[oslot];
+      if (lane == 0) {
+        ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+        unsigned pay = 1u;
+        if (W != 0u) {
+          out.status = ST_OK;
+          out.score = result_score(rp, nfeas, key32_score(W), 0, 0);
+          const int rk = key32_rank(W);
+          const int mask = select_gpus(load_node(&s_nodes[rk]), p, rp.gpusel, key32_gpu(W), rp.seed, step);
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+            out.score = 0;
+          } else {
+            out.node = rank2idx[rk];
+            out.gpu_mask = mask;
+            pay = pack_pay(rk, mask);
+          }
+        }
+        gstore32(win + step, pay);
+        rp.res[step] = out;
+        sh.pay = pay;
+      }
+    }
+    mark(3);
+    if (d >= 0) {
+      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+      const int wlo = own ? 1 : 0;  // wave 0 publishes when the step is this workgroup's
+      if (wv >= wlo && wv < a.nfw) {
+        double* fb = s_fold + (size_t)wv * kFoldBuf;
+        for (int it = wv - wlo; it < nit; it += a.nfw - wlo) {
+          const int code = sh.item_code[it];
+          const PodDev q = ksim_replay::uniform_pod(&sh.cls[sh.item_slot[it]]);
+          int cpuL, total;
+          uint32_t gs[4];
+          ksim_replay::fgd_candidate(dn, code, q, &cpuL, gs, &total);
+          const double F = wave_F(cpuL, gs, total, 1u << dn.gpu_type(), rp.typed != 0, sh.tp, rp.ncpu, rp.nt, lane, fb);
+          if (lane == 0) sh.F[it] = F;
+        }
+      }
+    }
+    mark(4);
+    __syncthreads();
+    mark(5);
+    // ---- C: the listed requests' keys (list wave)
+    if (d >= 0 && wv == kLW) {
+      const unsigned long long tl0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+      const double F0 = own ? sh.Fc[0] : sh.F[0];
+      for (int it = (own ? 0 : 1) + lane; it < nit; it += 64) {
+        const int code = sh.item_code[it];
+        sh.ikey[it] = pack_key32(score_of(F0 - sh.F[it]), d, code <= 8 ? 15 - (code - 1) : 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      unsigned gk = r_need ? pack_key32(0, d, 0) : 0u;
+      for (int k = 0; k < r_ni; ++k) {
+        const unsigned x = sh.ikey[r_base + k];
+        gk = x > gk ? x : gk;
+      }
+      const unsigned gkj = __shfl(gk, l_valid ? l_ref : 0, 64);
+      if (l_valid && !r_skip) {
+        const unsigned nk = r_feas ? gkj : 0u;
+        unsigned* kp = s_keys + (size_t)lane * N + d;
+        const unsigned old = *kp;
+        *kp = nk;
+        sh.cnt[lane] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
+      }
+      if (prof && lane == 0) sh.prof[13] += __builtin_amdgcn_s_memrealtime() - tl0;
+    }
+    mark(6);
+    // ---- top-2 of the next create event's class (its owner), on keys fresh but for this step's node
+    if (step + 1 < rp.n_events) {
+      const int nb = (step + 1) & (kEvBuf - 1);
+      const int ocn = __builtin_amdgcn_readfirstlane(nb != 0 ? sh.evo[nb] : evo[step + 1]);
+      if (ocn >= 0 && (ocn >> 16) == w) {
+        __syncthreads();
+        top2(ocn & 0xff);
+      }
+    }
+    mark(7);
+    // ---- this step's outcome on every workgroup: the Bind (or the delete) on the LDS cluster
+    if (wv == 0 && lane == 0) {
+      unsigned pay = 0u;
+      int sign = +1;
+      PodDev bp = p;
+      bool ok = true;
+      if (del) {
+        sign = -1;
+        if (p.ref >= 0 && p.ref < step) {
+          pay = gload32(win + p.ref);  // written before this workgroup passed step p.ref
+          bp = rp.ev[p.ref];
+        }
+      } else if (own) {
+        pay = sh.pay;
+      } else {
+        unsigned spins = 0;
+        while ((pay = gload32(win + step)) == 0u) {
+          if (++spins > kSpinLimit) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      int nd = -1;
+      if (!ok) {
+        sh.stop = 1;
+        atomicOr(a.fail, 1);
+      } else {
+        const int rk = (int)((pay >> 8) & 0xffffu) - 1;
+        const int mask = (int)(pay >> 24);
+        if (rk >= 0) {
+          NodeV n = load_node(&s_nodes[rk]);
+          bind_node(n, bp, mask, sign);
+          store_node(&s_nodes[rk], n);
+          store_node(&sh.dnode, n);
+          const int idx = rank2idx[rk];
+          if (del && is_w0) rp.res[step] = ResultDev{idx, mask, 0, 0, ST_DELETED};
+          if (rp.snap && (del ? is_w0 : own)) {  // cluster report: the state this event left
+            store_node(rp.snap + step, n);
+            rp.prev[step] = s_last[rk];
+          }
+          s_last[rk] = step;
+          if (is_w0 && bp.tag >= 0) {  // affinity tags (final state; GpuClustering's input)
+            uint16_t* tg = rp.tags + (size_t)idx * kTagStride + bp.tag;
+            *tg = (uint16_t)((int)*tg + sign);
+          }
+          nd = rk;
+        } else if (del && is_w0) {
+          rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
+        }
+      }
+      sh.dirty = nd;
+    }
+    mark(8);
+    __syncthreads();
+    mark(9);
+    if (sh.stop) break;
+  }
+  if (prof && tid == 0) {
+    sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
+    sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;
+  }
+  __syncthreads();
+  if (prof && tid < kProfPhases) a.prof[(size_t)blockIdx.x * kProfPhases + tid] = sh.prof[tid];
+  // final cluster state
+  if (is_w0 && !sh.stop)
+    for (int i = tid; i < N; i += kMBlock) store_node(rp.nodes + rank2idx[i], load_node(&s_nodes[i]));
+}
+
+// LDS bytes of k_memo's dynamic region (must match the carving in the kernel).
+inline size_t memo_lds(int N, int Cw, int nfw) {
+  const size_t keys = ((size_t)Cw * N * 4 + 15) & ~(size_t)15;
+  const size_t fold = std::max((size_t)nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15);
+  return sizeof(MemoShared) + (size_t)N * sizeof(NodeRec) + keys + fold + (size_t)N * 4;
+}
+
+}  // namespace ksim_memo

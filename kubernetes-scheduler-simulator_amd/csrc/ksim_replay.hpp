@@ -193,6 +193,18 @@ __device__ __forceinline__ PodDev uniform_pod(const PodDev* s) {
   return p;
 }
 
+// An LDS node record as wave-uniform values.
+__device__ __forceinline__ NodeV uniform_node(const NodeRec* s) {
+  NodeV n = load_node(s);
+  n.cpu_left = __builtin_amdgcn_readfirstlane(n.cpu_left);
+  n.mem_left = __builtin_amdgcn_readfirstlane(n.mem_left);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) n.g[i] = __builtin_amdgcn_readfirstlane(n.g[i]);
+  n.meta = __builtin_amdgcn_readfirstlane(n.meta);
+  n.name_rank = __builtin_amdgcn_readfirstlane(n.name_rank);
+  return n;
+}
+
 // ---- quad (4-lane) broadcasts: every lane of a quad gets lane J's value ----
 template <int J>
 __device__ __forceinline__ int qbc(int v) {

@@ -11,6 +11,11 @@ extern "C" {
 
 double dm_go_exp(double x) { return go_exp(x); }
 
+// FGD score from delta = cur - new: direct, and through the threshold table k_memo uses
+int dm_score_of_delta(double delta) { return fgd_score_of_delta(delta); }
+int dm_score_thresholds(double* th102) { return build_score_thresholds(th102) ? 1 : 0; }
+int dm_score_lookup(double delta, const double* th102) { return fgd_score_lookup(delta, th102); }
+
 // host copy of the engine's split table: CPU-only entries first, then GPU entries (order kept)
 static int split_table(int T, const int* tpi4, const double* tpf, TypDev* out, int* ncpu, bool* typed) {
   int k = 0;

@@ -166,3 +166,39 @@ def test_fix80_exact_scaling(dm):
         dm.dm_fix80(x, C.byref(lo), C.byref(hi))
         got = (hi.value << 64) | lo.value
         assert got == int(Fraction(x) * 2 ** 80), x
+
+
+def test_fgd_score_threshold_table(dm):
+    # k_memo scores through a table of the 100 score steps of int64(sigmoid(delta/1000)*100)
+    # (ksim_device.hpp build_score_thresholds / fgd_score_lookup): equal to the direct
+    # expression (and so to the oracle's) on random deltas and on every step +-3 ulps
+    import struct
+    th = (C.c_double * 102)()
+    dm.dm_score_thresholds.argtypes = [C.c_double * 102]
+    dm.dm_score_lookup.argtypes = [C.c_double, C.c_double * 102]
+    dm.dm_score_of_delta.argtypes = [C.c_double]
+    assert dm.dm_score_thresholds(th) == 1
+    L = O.lib()
+
+    def direct(x):
+        return dm.dm_score_of_delta(x)
+
+    def nxt(x, k):
+        b = struct.unpack("<q", struct.pack("<d", x))[0]
+        key = b if b >= 0 else -(b & 0x7FFFFFFFFFFFFFFF)
+        key += k
+        b = key if key >= 0 else (-key) | (1 << 63)
+        return struct.unpack("<d", struct.pack("<Q", b))[0]
+
+    rnd = random.Random(6)
+    xs = [rnd.uniform(-1e4, 1e4) for _ in range(40000)] + [rnd.uniform(-50, 50) for _ in range(20000)]
+    xs += [0.0, -0.0, 1e9, -1e9, 1e300, -1e300]
+    for k in range(1, 101):
+        xs += [nxt(th[k], j) for j in range(-3, 4)]
+    for x in xs:
+        s = direct(x)
+        assert dm.dm_score_lookup(x, th) == s, x
+        # the oracle computes the same expression from (cur, new) = (x, 0)
+        sig = 1.0 / (1.0 + L.orc_go_exp(-(x / 1000)))
+        assert s == int(sig * 100)
+    assert [direct(th[k]) for k in range(1, 101)] == list(range(1, 101))

@@ -1,0 +1,151 @@
+"""GPU parity of the memoised FGD replay (k_memo, run_mode 3) against the oracle and against the
+scanning replay (k_replay, run_mode 2).
+
+k_memo keeps the key of every (pod class, node) pair and recomputes only the node the previous
+event changed; the bar is the same as every other path: bit-exact (node, GPU set, score, feasible
+count, status) per event and the same final cluster state.  Every test needs a gfx950 device.
+"""
+import pytest
+
+import helpers
+import ksim
+import pyoracle as O
+from test_gpu_parity import assert_same, engine_run, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+MEMO, SCAN = 3, 2
+
+
+@pytest.fixture(scope="module")
+def default_trace():
+    return ksim.Trace.openb("default")
+
+
+def test_memo_full_openb_fgd(default_trace):
+    # C2 at one seed: 10 953 events on 1213 nodes, memo == oracle == k_replay
+    rp = default_trace.replay(seed=42)
+    res, state = engine_run(default_trace, rp, None, rp.n, "FGD", run_mode=MEMO)
+    want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, None)
+    scan, _ = engine_run(default_trace, rp, None, rp.n, "FGD", run_mode=SCAN)
+    assert res == scan
+
+
+@pytest.mark.parametrize("wgs", [3, 4, 8, 25, 64])
+def test_memo_workgroups_invariance(default_trace, wgs):
+    # any number of class-owning workgroups per replica gives the same decisions
+    rp = default_trace.replay(seed=6)
+    keep = list(range(0, default_trace.num_nodes, 3))
+    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", run_mode=MEMO, wgs=wgs)
+    want, want_state, _ = oracle_run(default_trace, rp, keep, 1500, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, keep)
+
+
+@pytest.mark.parametrize("trace_name", ["gpuspec33", "multigpu50", "gpushare100", "cpu250"])
+def test_memo_other_traces(trace_name):
+    # gpuspec33: 457 pod classes and typed typical pods (the NA bin)
+    t = ksim.Trace.openb(trace_name)
+    rp = t.replay(seed=43)
+    keep = list(range(1, t.num_nodes, 3))
+    n_ev = min(rp.n, 2500)
+    res, state = engine_run(t, rp, keep, n_ev, "FGD", run_mode=MEMO)
+    want, want_state, _ = oracle_run(t, rp, keep, n_ev, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, keep)
+
+
+def test_memo_ten_replicas_ragged(default_trace):
+    # the C2 layout (10 seeds, one engine) with ragged stream lengths: memo == k_replay
+    arr, n = default_trace.typical()
+    outs = {}
+    for mode in (MEMO, SCAN):
+        eng = ksim.Engine(default_trace.num_nodes, 10, run_mode=mode)
+        for r in range(10):
+            rp = default_trace.replay(seed=42 + r)
+            eng.set_nodes(r, rp.nodes)
+            eng.set_typical(r, arr, n)
+            eng.set_policy(r, "FGD")
+            eng.load_events(r, rp.events, rp.n - 97 * r)
+        eng.run()
+        outs[mode] = [eng.results(r) for r in range(10)]
+        if mode == MEMO:
+            assert eng.last_run_wgs() >= 8
+        eng.close()
+    for r in range(10):
+        assert outs[MEMO][r] == outs[SCAN][r], "replica %d" % r
+
+
+def test_memo_mixed_policies(default_trace):
+    # FGD replicas take k_memo, the others k_replay, in one run (run_mode 0 = auto)
+    cfgs = [(42, "FGD", O.POL_FGD, O.SEL_FGD), (43, "BestFit", O.POL_BESTFIT, O.SEL_BEST),
+            (45, "FGD", O.POL_FGD, O.SEL_FGD)]
+    keep = list(range(0, default_trace.num_nodes, 4))
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(len(keep), len(cfgs))
+    rps = []
+    for r, (seed, name, _, _) in enumerate(cfgs):
+        rp = default_trace.replay(seed=seed)
+        rps.append(rp)
+        eng.set_nodes(r, helpers.subset_nodes(rp, keep))
+        eng.set_typical(r, arr, n)
+        eng.set_policy(r, name)
+        eng.load_events(r, rp.events, 1100 + 100 * r)
+    eng.run()
+    for r, (seed, name, pol, sel) in enumerate(cfgs):
+        want, _, _ = oracle_run(default_trace, rps[r], keep, 1100 + 100 * r, pol, sel)
+        assert eng.results(r) == want, "replica %d (%s)" % (r, name)
+    eng.close()
+
+
+def test_memo_deletions(default_trace):
+    rp = default_trace.replay(seed=9)
+    keep = list(range(0, default_trace.num_nodes, 9))
+    evs, oev = helpers.delete_stream(default_trace, rp, 900, 0.3, seed=0)
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(len(keep), 1, run_mode=MEMO, wgs_per_replica=6)
+    eng.set_nodes(0, helpers.subset_nodes(rp, keep))
+    eng.set_typical(0, arr, n)
+    eng.set_policy(0, "FGD")
+    eng.load_events(0, evs, len(evs))
+    eng.run()
+    got = eng.results(0)
+    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev, policy=O.POL_FGD,
+                                       gpu_sel=O.SEL_FGD, threads=16)
+    assert_same(got, want, eng.nodes(0), want_state, keep)
+    assert any(r[4] == ksim.DELETED and r[0] >= 0 for r in got)
+    eng.close()
+
+
+def test_memo_tiny_cluster(default_trace):
+    # 3 nodes, more workgroups than classes and nodes; the cluster fills up and pods fail
+    rp = default_trace.replay(seed=3)
+    keep = [5, 600, 1100]
+    res, state = engine_run(default_trace, rp, keep, 400, "FGD", run_mode=MEMO, wgs=16)
+    want, want_state, _ = oracle_run(default_trace, rp, keep, 400, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, keep)
+    assert any(r[4] == ksim.UNSCHEDULABLE for r in res)
+
+
+def test_memo_rerun_same_results(default_trace):
+    # run() restarts from the set_nodes state: two runs of one engine agree
+    rp = default_trace.replay(seed=44)
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=MEMO)
+    eng.set_nodes(0, rp.nodes)
+    eng.set_typical(0, arr, n)
+    eng.set_policy(0, "FGD")
+    eng.load_events(0, rp.events, 3000)
+    eng.run()
+    a = eng.results(0)
+    eng.run()
+    assert eng.results(0) == a
+    eng.close()
+
+
+def test_memo_not_applicable_is_loud(default_trace):
+    # one workgroup cannot hold 151 classes x 404 nodes of keys: run_mode 3 refuses (no silent scan)
+    rp = default_trace.replay(seed=6)
+    keep = list(range(0, default_trace.num_nodes, 3))
+    with pytest.raises(ksim.KsimError):
+        engine_run(default_trace, rp, keep, rp.n, "FGD", run_mode=MEMO, wgs=1)

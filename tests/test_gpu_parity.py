@@ -84,7 +84,7 @@ def test_replay_workgroups_invariance(default_trace, wgs):
     # k_replay path: the granule all-gather gives the same decisions for any split of the nodes
     rp = default_trace.replay(seed=6)
     keep = list(range(0, default_trace.num_nodes, 3))
-    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", wgs=wgs)
+    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", wgs=wgs, run_mode=2)
     want, want_state, _ = oracle_run(default_trace, rp, keep, 1500, O.POL_FGD, O.SEL_FGD)
     assert_same(res, want, state, want_state, keep)
 

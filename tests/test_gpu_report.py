@@ -70,9 +70,9 @@ def test_report_subset_all_policies(default_trace, name, pol, sel):
     assert got[-1]["used_gpu_milli"] > 0 and got[-1]["arrived_gpu_milli"] > got[-1]["used_gpu_milli"]
 
 
-@pytest.mark.parametrize("run_mode,wgs", [(0, 1), (0, 5), (0, 64), (1, 0)])
+@pytest.mark.parametrize("run_mode,wgs", [(2, 1), (2, 5), (2, 64), (1, 0), (3, 1), (3, 7), (3, 0)])
 def test_report_execution_paths(default_trace, run_mode, wgs):
-    # k_replay with any workgroup split, and the k_step (hipGraph) path, record the same report
+    # k_replay (2) with any workgroup split, the k_step (hipGraph) path (1) and k_memo (3) record the same report
     rp = default_trace.replay(seed=3)
     keep, nodes, onodes = subset(default_trace, rp, 4)
     n_ev = 1200
@@ -87,7 +87,7 @@ def test_report_with_deletions(default_trace):
     rp = default_trace.replay(seed=9)
     keep, nodes, onodes = subset(default_trace, rp, 9)
     evs, oev = helpers.delete_stream(default_trace, rp, 900, 0.3, seed=1)
-    for run_mode in (0, 1):
+    for run_mode in (1, 2, 3):
         res, got = engine_reports(default_trace, nodes, evs, len(evs), "FGD", run_mode=run_mode)
         want_res, _, want = O.run_events(onodes, helpers.oracle_typical(default_trace), oev, policy=O.POL_FGD,
                                          gpu_sel=O.SEL_FGD, threads=16, with_report=True)
