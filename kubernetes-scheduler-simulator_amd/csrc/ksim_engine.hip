@@ -1387,8 +1387,19 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ma.win_stride = stride;
   ma.fail = e->d_fail;
   ma.prof = nullptr;
+  ma.trace = nullptr;
+  ma.trace_steps = 0;
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
+  const bool tracing = pe && pe[0] == '2';
+  unsigned long long* d_trace = nullptr;
+  const int TS = std::min(max_ev, 4000);
+  if (tracing) {
+    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * 4 * (size_t)Rg * pl.K * TS));
+    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * (size_t)Rg * pl.K * TS, st));
+    ma.trace = d_trace;
+    ma.trace_steps = TS;
+  }
   if (profile) {
     if ((rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)Rg * pl.K * ksim_memo::kProfPhases))) return rc;
     KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
@@ -1397,6 +1408,48 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   hipLaunchKernelGGL(ksim_memo::k_memo, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma, (const TypDev*)e->d_tp);
   KSIM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
+                     e->d_reps, (const int*)(e->d_replist + first), e->N);
+  KSIM_HIP(hipGetLastError());
+  if (tracing) {
+    // per step: owner's start -> publish, publish -> each other workgroup's receive, receive -> start
+    // (s_memrealtime, 100 MHz); replica 0 only
+    KSIM_HIP(hipStreamSynchronize(st));
+    const int K = pl.K;
+    std::vector<unsigned long long> h((size_t)4 * Rg * K * TS);
+    KSIM_HIP(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    KSIM_HIP(hipFree(d_trace));
+    std::vector<int> evo((size_t)TS);
+    KSIM_HIP(hipMemcpy(evo.data(), e->d_m_evo, sizeof(int) * TS, hipMemcpyDeviceToHost));
+    auto at = [&](int w, int s, int k) { return (double)h[((size_t)w * TS + s) * 4 + k]; };
+    double crit = 0, hand = 0, hmax = 0, period = 0, lag = 0, f0 = 0, spin = 0;
+    int nc = 0, nh = 0, nf = 0;
+    for (int s = 1; s + 1 < TS; ++s) {
+      if (evo[s] < 0 || evo[s + 1] < 0) continue;
+      const int o = evo[s] >> 16, o2 = evo[s + 1] >> 16;
+      crit += at(o, s, 1) - at(o, s, 0);
+      if (at(o, s, 2) > 0 && at(o, s, 3) > 0) {
+        f0 += at(o, s, 3) - at(o, s, 0);   // start -> all critical F done
+        spin += at(o, s, 2) - at(o, s, 3); // -> fresh key known
+        ++nf;
+      }
+      period += at(o2, s + 1, 1) - at(o, s, 1);
+      if (o2 != o) lag += at(o2, s + 1, 0) - at(o2, s, 1);  // next owner: receive s -> start s+1
+      ++nc;
+      for (int w = 0; w < K; ++w) {
+        if (w == o) continue;
+        const double d = at(w, s, 1) - at(o, s, 1);
+        hand += d;
+        hmax = std::max(hmax, d);
+        ++nh;
+      }
+    }
+    if (nc && nh)
+      std::fprintf(stderr, "ksim memo trace (replica 0, %d steps, us): owner start->publish %.3f; publish->receive mean %.3f max %.3f; "
+                   "next owner receive->start %.3f; publish->publish %.3f; owner start->all F done %.3f, ->fresh key %.3f\n",
+                   TS, crit / nc / 100, hand / nh / 100, hmax / 100, lag / nc / 100, period / nc / 100,
+                   nf ? f0 / nf / 100 : 0.0, nf ? (f0 + spin) / nf / 100 : 0.0);
+  }
   if (profile) {
     KSIM_HIP(hipStreamSynchronize(st));
     const int nb = Rg * pl.K, P = ksim_memo::kProfPhases;

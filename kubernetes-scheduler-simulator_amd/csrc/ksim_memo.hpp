@@ -60,15 +60,20 @@ struct MemoArgs {
   int win_stride;
   int* fail;
   unsigned long long* prof;  // optional [R*K][kProfPhases] (KSIM_PROFILE=1)
+  unsigned long long* trace; // optional [R*K][trace_steps][2] (KSIM_PROFILE=2): step start, publish / receive
+  int trace_steps;
 };
 constexpr int kProfPhases = 16;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C
 
 struct __align__(16) MemoShared {
   PodDev ev[kEvBuf];
-  int evo[kEvBuf];    // owner code of each staged event: workgroup << 16 | first slot of its group << 8 | slot
+  int evo[kEvBuf + 4];  // owner code of each staged event (+ the next window's first): workgroup << 16 |
+                        // first slot of its group << 8 | slot; -1 delete
   PodDev cls[kMaxCw];
   TypDev tp[kMaxTypical];
   NodeRec dnode;      // the record of the node the previous event changed (d)
+  unsigned dfirst;    // first_of_class(dnode, 0): GPUs holding the first occurrence of their milli-left value
+  unsigned pad_dfirst[3];
   double th[104];     // FGD score steps (build_score_thresholds), th[0] = -inf, th[101] = +inf
   unsigned long long grp[kMaxCw];
   int cls_id[kMaxCw];
@@ -82,6 +87,7 @@ struct __align__(16) MemoShared {
   unsigned wtop[kMWaves][2];
   unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
   int nitems;
+  int crit_done;      // owner: critical F evaluations finished (waves 1-8 count up, wave 0 waits)
   int dirty;          // node (rank) changed by the previous event, -1 none
   int stop;
   unsigned pay;       // this step's granule (its owner)
@@ -107,6 +113,33 @@ KSIM_HD int key32_gpu(unsigned k) {
 // Granule of step s: bit 0 written | [23:8] rank + 1 (0: nothing bound) | [31:24] GPU mask.
 KSIM_HD unsigned pack_pay(int rank, int mask) {
   return 1u | ((unsigned)(rank + 1) << 8) | ((unsigned)(mask & 0xff) << 24);
+}
+
+// Global-memory access through address-space-1 pointers: ReplicaDev's pointers are generic, and a
+// flat_store counts in lgkmcnt as well as vmcnt, so every later LDS wait (s_waitcnt lgkmcnt(0))
+// would stall until the store is acknowledged by memory.  global_* stores count in vmcnt only.
+template <typename T>
+__device__ __forceinline__ void gput(T* p, const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized records");
+  const unsigned* src = reinterpret_cast<const unsigned*>(&v);
+  __attribute__((address_space(1))) unsigned* dst = (__attribute__((address_space(1))) unsigned*)(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+}
+template <typename T>
+__device__ __forceinline__ T gget(const T* p) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized records");
+  T v;
+  unsigned* dst = reinterpret_cast<unsigned*>(&v);
+  const __attribute__((address_space(1))) unsigned* src = (const __attribute__((address_space(1))) unsigned*)(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+  return v;
+}
+__device__ __forceinline__ void gput_node(NodeRec* p, const NodeV& n) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  gput(q, make_uint4((uint32_t)n.cpu_left, (uint32_t)n.mem_left, n.g[0], n.g[1]));
+  gput(q + 1, make_uint4(n.g[2], n.g[3], n.meta, n.name_rank));
 }
 
 __device__ __forceinline__ unsigned gload32(const unsigned* p) {
@@ -135,6 +168,26 @@ __device__ __forceinline__ unsigned ge_mask(const NodeV& n, int m) {
     lt |= ((x & 1u) | ((x >> 15) & 2u)) << (2 * i);
   }
   return ~lt & 0xFFu;
+}
+
+// fgd_score_lookup with the hardware's fast exp2 / reciprocal for the estimate (error ~1e-6
+// relative, far below the one score unit the two threshold compares correct).
+__device__ __forceinline__ int score_lookup_dev(double delta, const double* th) {
+  const float e = __builtin_amdgcn_exp2f((float)delta * -0.0014426950408889634f);  // exp(-delta/1000)
+  int a = (int)(100.0f * __builtin_amdgcn_rcpf(1.0f + e));
+  a = a < 0 ? 0 : (a > 100 ? 100 : a);
+  if (delta >= th[a + 1]) ++a;
+  else if (delta < th[a]) --a;
+  return a;
+}
+
+// first_of_class(n, 0) computed lane-parallel (lane g < 8 tests GPU g): a few VALU instructions
+// and one ballot instead of 28 scalar compares.  Every lane must be active.
+__device__ __forceinline__ unsigned first_mask_lanes(const NodeV& n, int lane) {
+  const int g = lane & 7;
+  const int v = ksim_replay::gl_dyn(n, g);
+  const bool first = lane < 8 && g < n.gpu_cnt() && (ksim_replay::gl_equal_mask(n, v) & ((1u << g) - 1u)) == 0u;
+  return (unsigned)__ballot(first) & 0xFFu;
 }
 
 // Top-2 merge of two disjoint sets of distinct keys.
@@ -197,49 +250,47 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
   double acc = 0.0;
   for (int t0 = 0; t0 < nt; t0 += 64) {
     const int t = t0 + lane;
-    int row = -1;
-    double val = 0.0;
-    if (t < nt) {
-      const TypDev e = ltp[t];
-      const bool cpu_ok = cpuL >= e.cpu;
-      const double x = e.freq * dtot;  // freq * float64(gpuMilliLeftTotal)
-      if (t < ncpu) {
-        row = cpu_ok ? 3 : 4;  // GetNodePodFrag case 1 (frag.go:463-469)
-        val = x;
-      } else {
-        const uint32_t mp = (uint32_t)e.milli * 0x10001u;
-        uint32_t frag = 0u, nlt = 0u;
+    // branch free: every lane reads a valid entry (clamped) and classifies it both ways
+    const int tc = t < nt ? t : nt - 1;
+    const uint4 e4 = reinterpret_cast<const uint4*>(ltp)[2 * tc];  // cpu, milli, num_eff, tmask
+    const double fr = ltp[tc].freq;
+    asm volatile("" ::"v"(e4.y), "v"(e4.z), "v"(e4.w));  // one LDS round trip for the whole entry
+    const bool cpu_ok = cpuL >= (int)e4.x;
+    const double x = fr * dtot;  // freq * float64(gpuMilliLeftTotal)
+    const uint32_t mp = e4.y * 0x10001u;
+    uint32_t frag = 0u, nlt = 0u;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
-          const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
-          frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
-          nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
-        }
-        const bool gpu_ok = kMaxGpu - (int)nlt >= e.num_eff;      // CanNodeHostPodOnGpuMemory (frag.go:447-458)
-        const bool acc_ok = !typed || (e.tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
-        row = !acc_ok ? 5 : (cpu_ok ? 1 : (gpu_ok ? 2 : 0));
-        val = (acc_ok && cpu_ok && gpu_ok) ? e.freq * (double)(int)frag : x;  // Q3: frag part to Q2
-      }
+    for (int i = 0; i < 4; ++i) {
+      const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
+      const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
+      frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+      nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
     }
+    const bool gpu_ok = kMaxGpu - (int)nlt >= (int)e4.z;       // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+    const bool acc_ok = !typed || (e4.w & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+    const bool is_cpu = t < ncpu;                          // GetNodePodFrag case 1 (frag.go:463-469): XL / XR
+    int row = is_cpu ? (cpu_ok ? 3 : 4) : (!acc_ok ? 5 : (cpu_ok ? 1 : (gpu_ok ? 2 : 0)));
+    row = t < nt ? row : -1;
+    const double y = fr * (double)(int)frag;  // Q3: frag part to Q2
+    const double val = (!is_cpu && acc_ok && cpu_ok && gpu_ok) ? y : x;
 #pragma unroll
     for (int b = 0; b < kFoldRows; ++b) buf[b * 64 + lane] = row == b ? val : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // row b folds its columns in order: XL / XR (rows 3, 4) only hold CPU-only typical pods
-    // [0, cend), the other rows only GPU ones [cend, tn); every other cell is +0.0, so reading a
-    // pair that straddles a range end adds an exact zero
-    const int tn = min(64, nt - t0);
-    const int cend = min(max(ncpu - t0, 0), tn);
+    // lane b < 6 folds row b in typical-pod order; columns past the chunk's last typical pod hold
+    // +0.0, so the uniform 8-pair batches only ever add exact zeros beyond it
+    const int np = (min(64, nt - t0) + 1) >> 1;
     if (lane < kFoldRows) {
-      const bool cpu_row = lane == 3 || lane == 4;
-      const int lo = cpu_row ? 0 : (cend >> 1), hi = cpu_row ? ((cend + 1) >> 1) : ((tn + 1) >> 1);
       const double2* rw = reinterpret_cast<const double2*>(buf + lane * 64);
-#pragma unroll 8
-      for (int k = lo; k < hi; ++k) {
-        const double2 v = rw[k];
-        acc += v.x;
-        acc += v.y;
+      for (int k0 = 0; k0 < np; k0 += 8) {
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = rw[k0 + i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc += v[i].x;
+          acc += v[i].y;
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -308,7 +359,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   }
   for (int i = tid; i < rp.nt * 2; i += kMBlock)
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
-  if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; }
+  if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; sh.crit_done = 0; }
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
   const bool prof = a.prof != nullptr;
   if (prof && tid < kProfPhases) sh.prof[tid] = 0ull;
@@ -369,7 +420,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   }
   __syncthreads();
   mark(0);
-  auto score_of = [&](double delta) { return use_th ? fgd_score_lookup(delta, sh.th) : fgd_score_of_delta(delta); };
+  auto score_of = [&](double delta) { return use_th ? score_lookup_dev(delta, sh.th) : fgd_score_of_delta(delta); };
 
   // list wave, lane j <-> class slot j: the slot's request and group, kept in registers
   PodDev lq{};
@@ -393,15 +444,18 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     if (eb == 0) {
       const int ne = min(kEvBuf, rp.n_events - step);
       const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
-      for (int i = tid; i < ne * 2; i += kMBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
-      for (int i = tid; i < ne; i += kMBlock) sh.evo[i] = evo[step + i];
+      for (int i = tid; i < ne * 2; i += kMBlock) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
+      for (int i = tid; i <= ne; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
       __syncthreads();
     }
+    if (a.trace && tid == 0 && step < a.trace_steps)
+      a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4] = __builtin_amdgcn_s_memrealtime();
     // one LDS round trip: the event, its owner code, d and d's record
     const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
     const int oc = __builtin_amdgcn_readfirstlane(sh.evo[eb]);
     const int d = __builtin_amdgcn_readfirstlane(sh.dirty);
     const NodeV dn = ksim_replay::uniform_node(&sh.dnode);
+    const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
     const bool del = (p.flags & kPodDelete) != 0u;
     const bool own = oc >= 0 && (oc >> 16) == w;
     const int oslot = own ? (oc & 0xff) : -1;
@@ -413,7 +467,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
         int code = -1;
         if (wv == 0) code = 0;
-        else if (is_share_pod(cp)) code = (((first_of_class(dn, 0) & ge_mask(dn, cp.milli)) >> (wv - 1)) & 1u) ? wv : -1;
+        else if (is_share_pod(cp)) code = (((dfirst & ge_mask(dn, cp.milli)) >> (wv - 1)) & 1u) ? wv : -1;
         else if (wv == 1) code = 9;
         if (code >= 0) {
           int cpuL, total;
@@ -423,6 +477,10 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
                                   s_fold + (size_t)wv * kFoldBuf);
           if (lane == 0) sh.Fc[wv] = F;
         }
+        if (wv > 0 && lane == 0) {  // hand the candidate's F to wave 0 without a workgroup barrier
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_fetch_add(&sh.crit_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       if (wv == kLW) {
         const unsigned long long tl0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -431,7 +489,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         const unsigned long long FM = __ballot(r_feas);
         r_need = l_rep && !r_skip && (FM & l_grp) != 0ull;
         unsigned cm = 0u;
-        if (r_need) cm = l_share ? (first_of_class(dn, 0) & ge_mask(dn, lq.milli)) : 0x100u;
+        if (r_need) cm = l_share ? (dfirst & ge_mask(dn, lq.milli)) : 0x100u;
         r_ni = __popc(cm);
         // exclusive prefix of r_ni over the lanes (r_ni <= 8: four bit planes)
         int excl = 0, tot = 0;
@@ -462,39 +520,39 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         }
       }
     }
-    mark(1);
-    __syncthreads();
-    mark(2);
-    // ---- B: the owner publishes the step's winner (wave 0); the listed states are evaluated
+    // ---- the owner publishes the step's winner (wave 0, as soon as waves 1-8 have their F)
     if (own && wv == 0) {
-      unsigned fresh = 0u;
+      unsigned fresh = 0u, old_own = 0u, gk_crit = 0u;
       if (d >= 0) {
+        if (lane == 0) {  // wait for waves 1-8 (LDS counter; every one of them arrives)
+          while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8)
+            __builtin_amdgcn_s_sleep(0);
+          sh.crit_done = 0;
+          if (a.trace && step < a.trace_steps)
+            a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
         const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
         const bool cshare = is_share_pod(cp);
-        const unsigned fm = cshare ? (first_of_class(dn, 0) & ge_mask(dn, cp.milli)) : 0u;
+        const unsigned fm = cshare ? (dfirst & ge_mask(dn, cp.milli)) : 0u;
         const bool has = lane >= 1 && lane <= 8 && (cshare ? ((fm >> (lane - 1)) & 1u) != 0u : lane == 1);
         int k = 0;
         if (has) k = (int)pack_key32(score_of(sh.Fc[0] - sh.Fc[lane]), d, cshare ? 15 - (lane - 1) : 0);
         unsigned gk = (unsigned)ksim_replay::wave_max_dpp(k);
         const unsigned z = pack_key32(0, d, 0);  // feasible with no fitting GPU
-        gk = gk > z ? gk : z;
-        const int j = lane;
-        if (j < Cw && ((sh.grp[crep] >> j) & 1ull)) {
-          const PodDev q = sh.cls[j];
-          const unsigned nk = filter_node(dn, q) ? gk : 0u;
-          unsigned* kp = s_keys + (size_t)j * N + d;
-          const unsigned old = *kp;
-          *kp = nk;
-          sh.cnt[j] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        fresh = s_keys[(size_t)oslot * N + d];
+        gk_crit = gk > z ? gk : z;
+        // the step's own class first (the rest of its group after the granule is out)
+        const PodDev oq = ksim_replay::uniform_pod(&sh.cls[oslot]);
+        fresh = filter_node(dn, oq) ? gk_crit : 0u;
+        old_own = s_keys[(size_t)oslot * N + d];
+        if (a.trace && lane == 0 && step < a.trace_steps)
+          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
       }
       const unsigned t2a = sh.t2a, t2b = sh.t2b;
       const unsigned ex = (d >= 0 && t2a != 0u && key32_rank(t2a) == d) ? t2b : t2a;
       const unsigned W = fresh > ex ? fresh : ex;
-      const int nfeas = sh.cnt[oslot];
+      const int nfeas = sh.cnt[oslot] + (d >= 0 ? (fresh != 0u ? 1 : 0) - (old_own != 0u ? 1 : 0) : 0);
       if (lane == 0) {
         ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
         unsigned pay = 1u;
@@ -507,23 +565,39 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
             out.status = ST_ERROR;
             out.score = 0;
           } else {
-            out.node = rank2idx[rk];
+            out.node = rk;  // name rank; k_memo_finish maps it to the node index
             out.gpu_mask = mask;
             pay = pack_pay(rk, mask);
           }
         }
         gstore32(win + step, pay);
-        rp.res[step] = out;
+        asm volatile("" ::: "memory");
+        if (a.trace && step < a.trace_steps)
+          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        gput(rp.res + step, out);
         sh.pay = pay;
       }
+      if (d >= 0) {  // every class of the step's score group on d (its own included)
+        const int j = lane;
+        if (j < Cw && ((sh.grp[crep] >> j) & 1ull)) {
+          const PodDev q = sh.cls[j];
+          const unsigned nk = filter_node(dn, q) ? gk_crit : 0u;
+          unsigned* kp = s_keys + (size_t)j * N + d;
+          const unsigned old = *kp;
+          *kp = nk;
+          sh.cnt[j] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
+        }
+      }
     }
+    mark(1);
+    __syncthreads();
+    mark(2);
     mark(3);
     if (d >= 0) {
       const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
-      const int wlo = own ? 1 : 0;  // wave 0 publishes when the step is this workgroup's
-      if (wv >= wlo && wv < a.nfw) {
+      if (wv < a.nfw) {
         double* fb = s_fold + (size_t)wv * kFoldBuf;
-        for (int it = wv - wlo; it < nit; it += a.nfw - wlo) {
+        for (int it = wv; it < nit; it += a.nfw) {
           const int code = sh.item_code[it];
           const PodDev q = ksim_replay::uniform_pod(&sh.cls[sh.item_slot[it]]);
           int cpuL, total;
@@ -566,8 +640,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     mark(6);
     // ---- top-2 of the next create event's class (its owner), on keys fresh but for this step's node
     if (step + 1 < rp.n_events) {
-      const int nb = (step + 1) & (kEvBuf - 1);
-      const int ocn = __builtin_amdgcn_readfirstlane(nb != 0 ? sh.evo[nb] : evo[step + 1]);
+      const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + 1]);
       if (ocn >= 0 && (ocn >> 16) == w) {
         __syncthreads();
         top2(ocn & 0xff);
@@ -575,7 +648,10 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     }
     mark(7);
     // ---- this step's outcome on every workgroup: the Bind (or the delete) on the LDS cluster
-    if (wv == 0 && lane == 0) {
+    if (wv == 0) {
+      int nd_w = -1;
+      NodeV nn{};
+      if (lane == 0) {
       unsigned pay = 0u;
       int sign = +1;
       PodDev bp = p;
@@ -584,7 +660,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         sign = -1;
         if (p.ref >= 0 && p.ref < step) {
           pay = gload32(win + p.ref);  // written before this workgroup passed step p.ref
-          bp = rp.ev[p.ref];
+          bp = gget(rp.ev + p.ref);
         }
       } else if (own) {
         pay = sh.pay;
@@ -594,6 +670,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           if (++spins > kSpinLimit) { ok = false; break; }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (a.trace && step < a.trace_steps)
+          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
       }
       int nd = -1;
       if (!ok) {
@@ -607,23 +685,36 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           bind_node(n, bp, mask, sign);
           store_node(&s_nodes[rk], n);
           store_node(&sh.dnode, n);
-          const int idx = rank2idx[rk];
-          if (del && is_w0) rp.res[step] = ResultDev{idx, mask, 0, 0, ST_DELETED};
+          nn = n;
+          // (results carry name ranks and the affinity tags are applied by k_memo_finish: nothing
+          // here waits on global memory)
+          if (del && is_w0) gput(rp.res + step, ResultDev{rk, mask, 0, 0, ST_DELETED});
           if (rp.snap && (del ? is_w0 : own)) {  // cluster report: the state this event left
-            store_node(rp.snap + step, n);
-            rp.prev[step] = s_last[rk];
+            gput_node(rp.snap + step, n);
+            gput(rp.prev + step, s_last[rk]);
           }
           s_last[rk] = step;
-          if (is_w0 && bp.tag >= 0) {  // affinity tags (final state; GpuClustering's input)
-            uint16_t* tg = rp.tags + (size_t)idx * kTagStride + bp.tag;
-            *tg = (uint16_t)((int)*tg + sign);
-          }
           nd = rk;
         } else if (del && is_w0) {
-          rp.res[step] = ResultDev{-1, 0, 0, 0, ST_DELETED};
+          gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_DELETED});
         }
       }
       sh.dirty = nd;
+      nd_w = nd;
+      }  // lane 0
+      // the first-occurrence GPU mask of the changed node, for the next step's candidate lists
+      nd_w = __builtin_amdgcn_readfirstlane(nd_w);
+      if (nd_w >= 0) {
+        NodeV u;
+        u.cpu_left = __builtin_amdgcn_readfirstlane(nn.cpu_left);
+        u.mem_left = __builtin_amdgcn_readfirstlane(nn.mem_left);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u.g[i] = __builtin_amdgcn_readfirstlane(nn.g[i]);
+        u.meta = __builtin_amdgcn_readfirstlane(nn.meta);
+        u.name_rank = __builtin_amdgcn_readfirstlane(nn.name_rank);
+        const unsigned fmk = first_mask_lanes(u, lane);
+        if (lane == 0) sh.dfirst = fmk;
+      }
     }
     mark(8);
     __syncthreads();
@@ -639,6 +730,28 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   // final cluster state
   if (is_w0 && !sh.stop)
     for (int i = tid; i < N; i += kMBlock) store_node(rp.nodes + rank2idx[i], load_node(&s_nodes[i]));
+}
+
+// After k_memo: results carry name ranks -> node indices, and every Bind / delete adds its pod's
+// affinity tag (pod.go:111-123) to the node's counts (commutative u32 atomics on the packed u16
+// pairs: any transient borrow between the halves cancels, the final counts are exact).
+__global__ void k_memo_finish(ReplicaDev* reps, const int* rep_list, int N) {
+  const ReplicaDev rp = reps[rep_list[blockIdx.y]];
+  const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (e >= rp.n_events) return;
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
+  ResultDev r = rp.res[e];
+  if (r.node < 0) return;
+  const int idx = rank2idx[r.node];
+  rp.res[e].node = idx;
+  const PodDev p = rp.ev[e];
+  const bool del = (p.flags & kPodDelete) != 0u;
+  if (!(del ? r.status == ST_DELETED : r.status == ST_OK)) return;
+  const int tag = del ? rp.ev[p.ref].tag : p.tag;
+  if (tag < 0) return;
+  const size_t h = (size_t)idx * kTagStride + tag;
+  unsigned* word = reinterpret_cast<unsigned*>(rp.tags) + (h >> 1);
+  atomicAdd(word, (unsigned)(del ? -1 : 1) << (16 * (h & 1)));
 }
 
 // LDS bytes of k_memo's dynamic region (must match the carving in the kernel).

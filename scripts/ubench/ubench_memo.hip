@@ -64,7 +64,19 @@ __global__ void k_ub(const TypDev* tp_g, int nt, int ncpu, const NodeRec* nodes,
   int v = lane;
   for (int it = 0; it < 64; ++it) v = reinterpret_cast<volatile int*>(fold)[(v + it) & 63] & 63;
   unsigned long long t6 = __builtin_amdgcn_s_memtime();
+  asm volatile("" ::"v"(v));
+  // 7. dependent v_add_f64 chain (the fold's critical path)
+  double z = acc * 1e-300;
+  const double inc = tp_g[lane & 7].freq;
+  asm volatile("" ::"v"(inc));
+  const unsigned long long t6b = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int it = 0; it < 64; ++it) z += inc;
+  asm volatile("" ::"v"(z));
+  unsigned long long t7 = __builtin_amdgcn_s_memtime();
+  t6 = t6b;
   if (lane == 0) {
+    out[6] = (t7 - t6) / 64;
     out[0] = (t1 - t0) / 64;
     out[1] = (t2 - t1) / 64;
     out[2] = (t3 - t2) / 64;
@@ -72,7 +84,7 @@ __global__ void k_ub(const TypDev* tp_g, int nt, int ncpu, const NodeRec* nodes,
     out[4] = (t5 - t4) / 16;
     out[5] = (t6 - t5) / 64;
   }
-  sink[lane] = acc + y + sc + cnt + v;
+  sink[lane] = acc + y + sc + cnt + v + z;
 }
 
 int main() {
@@ -125,10 +137,10 @@ int main() {
     hipLaunchKernelGGL(k_ub, dim3(1), dim3(64), 0, 0, d_tp, nt, ncpu, d_n, d_p, d_o, d_s, d_th);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
   }
-  unsigned long long o[6];
+  unsigned long long o[7];
   (void)hipMemcpy(o, d_o, sizeof o, hipMemcpyDeviceToHost);
   std::printf("s_memtime ticks per op: wave_F %llu, score direct %llu, score table %llu, filter+cand-mask %llu, "
-              "scalar eval_fgd_item %llu, LDS round trip %llu\n",
-              o[0], o[1], o[2], o[3], o[4], o[5]);
+              "scalar eval_fgd_item %llu, LDS round trip %llu, dependent f64 add %llu\n",
+              o[0], o[1], o[2], o[3], o[4], o[5], o[6]);
   return 0;
 }

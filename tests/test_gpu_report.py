@@ -70,7 +70,7 @@ def test_report_subset_all_policies(default_trace, name, pol, sel):
     assert got[-1]["used_gpu_milli"] > 0 and got[-1]["arrived_gpu_milli"] > got[-1]["used_gpu_milli"]
 
 
-@pytest.mark.parametrize("run_mode,wgs", [(2, 1), (2, 5), (2, 64), (1, 0), (3, 1), (3, 7), (3, 0)])
+@pytest.mark.parametrize("run_mode,wgs", [(2, 1), (2, 5), (2, 64), (1, 0), (3, 3), (3, 7), (3, 0)])
 def test_report_execution_paths(default_trace, run_mode, wgs):
     # k_replay (2) with any workgroup split, the k_step (hipGraph) path (1) and k_memo (3) record the same report
     rp = default_trace.replay(seed=3)
