@@ -8,9 +8,10 @@ fixed (rank k replays seeds 42+10k .. 51+10k): weak scaling, replicas only, no
 collective on the data path.
 
 One JSON line on rank 0.  Extra keys: node_evals_per_s, roofline (dominant
-kernel k_replay -- one persistent launch replays every replica -- priced against
-HBM with SURVEY §8(d)'s 32 B per node-evaluation + 56 B per pod), and cpu_baseline
-(the C oracle -- a restatement of the Go path -- on the host cores).
+kernel: k_memo for FGD -- one persistent launch replays every replica with the
+(pod class, node) keys memoised -- else k_replay; priced against HBM with SURVEY
+§8(d)'s 32 B per node-evaluation + 56 B per pod), and cpu_baseline (the C oracle
+-- a restatement of the Go path -- on the host cores).
 
 Multi-GPU (torchrun, one rank per GPU): each rank replays its own seeds on its own
 GPU; the only collectives are the timing barrier and the job reduction (max time,
@@ -30,9 +31,9 @@ import ksim  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
-# HBM bytes per k_replay launch of this default workload from the PMC passes of
+# HBM bytes per launch of the dominant kernel of this default workload from the PMC passes of
 # scripts/profile_round.sh (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "round_end", "pmc.json")
+PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("memo", "round_end")]
 
 
 def cpu_baseline(trace, seed, threads):
@@ -80,7 +81,8 @@ def main():
     ap.add_argument("--replicas", type=int, default=10, help="seeds per GPU (C2: 10)")
     ap.add_argument("--nodes-per-block", type=int, default=0)
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per replica (0 = auto)")
-    ap.add_argument("--run-mode", type=int, default=0, help="0 persistent k_replay, 1 k_step per pod")
+    ap.add_argument("--run-mode", type=int, default=0,
+                    help="0 auto (FGD: k_memo), 1 k_step per pod, 2 k_replay only, 3 k_memo required")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | ...")
@@ -154,8 +156,9 @@ def main():
         job_events = total_events * args.steps  # one cluster: every rank processed the same events
 
     steps_per_run = eng.last_run_steps()
-    # roofline: the dominant kernel is k_replay, one launch per replay of all replicas; its duration is
-    # the hipEvent pair around the launch on the engine stream (mean over the timed runs)
+    kernel = eng.last_run_path()
+    # roofline: the dominant kernel (k_memo / k_replay) is one launch per replay of all replicas; its
+    # duration is the hipEvent pair around the launch on the engine stream (mean over the timed runs)
     kern_us = dev_ms / args.steps * 1000.0
     bytes_per_launch = total_events * (BYTES_PER_NODE_EVAL * trace.num_nodes + BYTES_PER_POD)
     achieved = bytes_per_launch / (kern_us * 1e-6) / 1e9
@@ -164,11 +167,14 @@ def main():
     traffic, traffic_src = None, None
     default_cfg = (args.config == "c2" and args.policy == "FGD" and args.replicas == 10 and args.run_mode == 0
                    and args.wgs == 0 and not args.report)
-    if default_cfg and os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("hbm_bytes_per_dispatch")
-        traffic_src = os.path.relpath(PMC_FILE, ROOT)
+    for pf in PMC_FILES:  # PMC bytes of THIS kernel on this workload (profiles/ summary), if profiled
+        if default_cfg and os.path.exists(pf):
+            with open(pf) as f:
+                pmc = json.load(f)
+            if pmc.get("kernel") == kernel and pmc.get("hbm_bytes_per_dispatch"):
+                traffic = pmc["hbm_bytes_per_dispatch"]
+                traffic_src = os.path.relpath(pf, ROOT)
+                break
     line = {
         "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
         "value": value,
@@ -190,7 +196,7 @@ def main():
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "k_replay", "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
+                     "kernel": kernel, "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
                      "wgs_per_replica": eng.last_run_wgs()},
     }
     if args.config == "c4":

@@ -235,6 +235,15 @@ int  ksim_engine_last_run_ms(ksim_engine* e, double* ms);
 int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
 /* Workgroups per replica used by the last run. */
 int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
+/* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),
+ * KSIM_PATH_MEMO (k_memo, memoised FGD keys), KSIM_PATH_MIXED (k_memo for the FGD replicas, k_replay
+ * for the others), KSIM_PATH_STEP (k_step per pod, hipGraph), KSIM_PATH_SHARDED (node-sharded). */
+#define KSIM_PATH_REPLAY  0
+#define KSIM_PATH_MEMO    1
+#define KSIM_PATH_MIXED   2
+#define KSIM_PATH_STEP    3
+#define KSIM_PATH_SHARDED 4
+int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus
 }

@@ -2413,6 +2413,15 @@ int ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica) {
   return KSIM_OK;
 }
 
+int ksim_engine_last_run_path(ksim_engine* e, int* path) {
+  if (!e || !path) return KSIM_EINVAL;
+  if (e->shard_world > 0) *path = KSIM_PATH_SHARDED;
+  else if (e->run_mode == 1) *path = KSIM_PATH_STEP;
+  else if (e->last_memo == 0) *path = KSIM_PATH_REPLAY;
+  else *path = e->last_memo == e->R ? KSIM_PATH_MEMO : KSIM_PATH_MIXED;
+  return KSIM_OK;
+}
+
 int ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us) {
   if (!e || !mean_kernel_us || n_steps <= 0) return KSIM_EINVAL;
   KSIM_HIP(hipSetDevice(e->device));

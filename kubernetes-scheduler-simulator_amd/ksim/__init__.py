@@ -127,6 +127,7 @@ SIGNATURES = {
     "ksim_engine_last_run_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
     "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
+    "ksim_engine_last_run_path": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
     "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
     "ksim_engine_last_report_ms": (C.c_int, [_VP, _P(C.c_double)]),
@@ -383,6 +384,12 @@ class Engine:
         s = C.c_int64(0)
         check(lib().ksim_engine_last_run_steps(self.h, C.byref(s)), "last_run_steps")
         return s.value
+
+    def last_run_path(self):
+        """'k_replay' | 'k_memo' | 'k_memo+k_replay' | 'k_step' | 'sharded': the kernels the last run() used."""
+        k = C.c_int(0)
+        check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
+        return ["k_replay", "k_memo", "k_memo+k_replay", "k_step", "sharded"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)

@@ -1,5 +1,6 @@
-"""Summarise a profile_round.sh run: k_replay duration (kernel trace) and HBM bytes per
-k_replay dispatch from the FETCH_SIZE / WRITE_SIZE passes.  FETCH_SIZE is doubled
+"""Summarise a profile_round.sh run: the dominant kernel's duration (kernel trace: the kernel with
+the largest total time, k_memo or k_replay) and its HBM bytes per dispatch from the FETCH_SIZE /
+WRITE_SIZE passes.  FETCH_SIZE is doubled
 (MI355X_MICROARCH.md, HBM section: on gfx950 it reports half the bytes of wide
 coalesced reads); WRITE_SIZE is taken as is.  FETCH/WRITE_SIZE are in KiB."""
 import csv
@@ -18,18 +19,29 @@ def rows(pattern):
 
 
 def main(d):
-    kt = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_trace.csv")) if "k_replay" in r.get("Kernel_Name", "")]
+    def kernel_of(name):  # demangled or mangled names
+        if "k_memo(" in name or "k_memoENS" in name:
+            return "k_memo"
+        return "k_replay" if "k_replay" in name else name
+
+    allk = rows(os.path.join(d, "kt", "**", "*kernel_trace.csv"))
+    tot = {}
+    for r in allk:
+        k = kernel_of(r.get("Kernel_Name", ""))
+        tot[k] = tot.get(k, 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    kname = max(tot, key=tot.get)
+    kt = [r for r in allk if kernel_of(r.get("Kernel_Name", "")) == kname]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt]
 
     def counter(sub, name):
         vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
-                if "k_replay" in r.get("Kernel_Name", "") and r.get("Counter_Name") == name]
+                if kernel_of(r.get("Kernel_Name", "")) == kname and r.get("Counter_Name") == name]
         return vals
 
     fetch = counter("fetch", "FETCH_SIZE")
     write = counter("write", "WRITE_SIZE")
     res = {
-        "kernel": "k_replay",
+        "kernel": kname,
         "dispatches": len(durs),
         "mean_duration_ns": sum(durs) / len(durs) if durs else None,
         "fetch_kib_per_dispatch_raw": (sum(fetch) / len(fetch)) if fetch else None,

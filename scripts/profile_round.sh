@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profile of the bench workload (run on a gpurun box):
-#   1. rocprofv3 --kernel-trace --stats     -> k_replay duration (must agree with bench.py's hipEvents)
-#   2. rocprofv3 --pmc FETCH_SIZE           -> HBM read bytes per k_replay dispatch (x2, gfx950 correction)
+#   1. rocprofv3 --kernel-trace --stats     -> the dominant kernel's duration (k_memo; must agree with bench.py's hipEvents)
+#   2. rocprofv3 --pmc FETCH_SIZE           -> HBM read bytes per dispatch (x2, gfx950 correction)
 #   3. rocprofv3 --pmc WRITE_SIZE           -> HBM write bytes per dispatch
 # (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass; no --pmc with sys/runtime traces)
 #   4. the default bench line (with cpu_baseline)
