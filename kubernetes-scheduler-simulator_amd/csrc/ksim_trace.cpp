@@ -13,6 +13,7 @@
 #include <tuple>
 #include <vector>
 
+#include "go_rand.hpp"
 #include "ksim_trace.h"
 
 namespace {
@@ -32,8 +33,8 @@ struct Pod {
   std::string spec;   // normalised pipe list
 };
 
-// xoshiro256** seeded through splitmix64: the documented stand-in for Go's
-// global math/rand source (DESIGN.md "Event-order contract").
+// xoshiro256** seeded through splitmix64: draws of the synthetic-cluster generator
+// (ksim_trace_synthetic; not part of the reference).  Replays use Go's math/rand (go_rand.hpp).
 struct Rng {
   uint64_t s[4];
   static uint64_t splitmix(uint64_t& x) {
@@ -368,39 +369,38 @@ int ksim_trace_typical(const ksim_trace* t, const ksim_typical_cfg* cfg, ksim_ty
 int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
                       int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix) {
   if (!t || !cfg || !n_events || !nodes) return KSIM_EINVAL;
-  Rng rng(cfg->seed);
-  (void)rng.int63();  // core.go:115-116: rand.Int() consumed by a Debugf argument
+  // Go's global math/rand, seeded as core.go:115 does; the draws below are every draw the
+  // reference makes from it between rand.Seed and the first scheduling cycle.
+  ksim_go::Rand rng((int64_t)cfg->seed);
+  (void)rng.Int();  // core.go:116: rand.Int() evaluated as a Debugf argument
   const int np = (int)t->pods.size();
   std::vector<int> order(np);
   for (int i = 0; i < np; ++i) order[i] = i;  // name order
   if (cfg->shuffle) {
-    // SortClusterPods (simulator.go:975-984): sort by name, then rand.Shuffle
-    for (int i = np - 1; i > 0; --i) {
-      const int j = (int)rng.intn(i + 1);
-      std::swap(order[i], order[j]);
-    }
+    // SortClusterPods (simulator.go:975-984): sort.Slice by name, then rand.Shuffle
+    rng.Shuffle(np, [&](int64_t i, int64_t j) { std::swap(order[i], order[j]); });
   }
   // TunePodsByNodeTotalResource (simulator.go:1201-1248)
   int64_t pod_total = 0, node_total = 0;
   for (int i = 0; i < np; ++i) pod_total += (int64_t)t->pods[i].gpu_milli * t->pods[i].gpu_count;
   for (auto& n : t->nodes) node_total += (int64_t)n.gpu * 1000;
   std::vector<int> ev = order;
-  std::vector<int> tuned_from;  // clone source per appended event
   const double ratio = cfg->tune_ratio;
   if (ratio > 0) {
     const double target = ratio * (double)node_total;
     if ((double)pod_total > target) {
-      // tuneDownPods (simulator.go:1254-1261)
+      // tuneDownPods (simulator.go:1249-1262): rand.Intn(len(pods)), remove that index
       while ((double)pod_total > ratio * (double)node_total && !ev.empty()) {
-        const int idx = (int)rng.intn((int64_t)ev.size());
+        const int idx = (int)rng.Intn((int64_t)ev.size());
         const Pod& p = t->pods[ev[idx]];
         ev.erase(ev.begin() + idx);
         pod_total -= (int64_t)p.gpu_milli * p.gpu_count;
       }
     } else if ((double)pod_total < target) {
-      // tuneUpPods (simulator.go:1263-1282): note the MilliGpu vs TotalMilliGpu asymmetry
+      // tuneUpPods (simulator.go:1263-1282): rand.Intn(len(workloadPods)) over the name-sorted
+      // workload (simulator.go:966-968); note the MilliGpu vs TotalMilliGpu asymmetry
       for (;;) {
-        const int idx = (int)rng.intn(np);
+        const int idx = (int)rng.Intn(np);
         const Pod& p = t->pods[idx];
         if ((double)(pod_total + p.gpu_milli) > ratio * (double)node_total) break;
         pod_total += (int64_t)p.gpu_milli * p.gpu_count;
@@ -409,14 +409,13 @@ int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod*
     }
   }
   *n_events = (int)ev.size();
+  // RunCluster -> runScheduler (simulator.go:286-289) starts the informers and waits for their
+  // caches; each reflector's watch loop draws rand.Float64() once (reflector.go:400)
+  const int draws = cfg->informer_draws < 0 ? KSIM_REPLAY_INFORMER_DRAWS : cfg->informer_draws;
+  for (int i = 0; i < draws; ++i) (void)rng.Float64();
   // node naming: sort by name, rand.Perm prefix (simulator.go:577-588)
   const int nn = (int)t->nodes.size();
-  std::vector<int> perm(nn);
-  for (int i = 0; i < nn; ++i) {
-    const int j = (int)rng.intn(i + 1);
-    perm[i] = perm[j];
-    perm[j] = i;
-  }
+  const std::vector<int> perm = rng.Perm(nn);
   std::vector<std::string> full(nn);
   char buf[32];
   for (int i = 0; i < nn; ++i) {
@@ -445,6 +444,39 @@ int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod*
     if (pod_index) pod_index[k] = ev[k];
   }
   return KSIM_OK;
+}
+
+int ksim_go_rand(int64_t seed, int op, int64_t arg, int n, int64_t* out) {
+  if (n < 0 || (n > 0 && !out)) return KSIM_EINVAL;
+  if ((op == KSIM_GO_INTN || op == KSIM_GO_PERM) && arg <= 0) return KSIM_EINVAL;
+  ksim_go::Rand r(seed);
+  switch (op) {
+    case KSIM_GO_INT63:
+      for (int i = 0; i < n; ++i) out[i] = r.Int63();
+      return KSIM_OK;
+    case KSIM_GO_INTN:
+      for (int i = 0; i < n; ++i) out[i] = r.Intn(arg);
+      return KSIM_OK;
+    case KSIM_GO_FLOAT64:
+      for (int i = 0; i < n; ++i) {
+        const double f = r.Float64();
+        std::memcpy(&out[i], &f, sizeof f);
+      }
+      return KSIM_OK;
+    case KSIM_GO_PERM: {
+      if (n < arg) return KSIM_ERANGE;
+      const std::vector<int> m = r.Perm((int)arg);
+      for (int64_t i = 0; i < arg; ++i) out[i] = m[i];
+      return KSIM_OK;
+    }
+    case KSIM_GO_SHUFFLE: {
+      for (int i = 0; i < n; ++i) out[i] = i;
+      r.Shuffle(n, [&](int64_t i, int64_t j) { std::swap(out[i], out[j]); });
+      return KSIM_OK;
+    }
+    default:
+      return KSIM_EINVAL;
+  }
 }
 
 }  // extern "C"

@@ -94,7 +94,7 @@ class TypicalCfg(C.Structure):
 
 
 class ReplayCfg(C.Structure):
-    _fields_ = [("seed", C.c_uint64), ("tune_ratio", C.c_double), ("shuffle", C.c_int32), ("reserved", C.c_int32)]
+    _fields_ = [("seed", C.c_uint64), ("tune_ratio", C.c_double), ("shuffle", C.c_int32), ("informer_draws", C.c_int32)]
 
 
 assert C.sizeof(Node) == 128 and C.sizeof(Pod) == 48 and C.sizeof(Typical) == 32 and C.sizeof(Result) == 24
@@ -146,6 +146,7 @@ SIGNATURES = {
     "ksim_trace_typical": (C.c_int, [_VP, _P(TypicalCfg), _P(Typical), C.c_int, _P(C.c_int)]),
     "ksim_trace_replay": (C.c_int, [_VP, _P(ReplayCfg), _P(Pod), C.c_int, _P(C.c_int), _P(C.c_int32), _P(Node),
                                     _P(C.c_int32)]),
+    "ksim_go_rand": (C.c_int, [C.c_int64, C.c_int, C.c_int64, C.c_int, _P(C.c_int64)]),
 }
 
 
@@ -178,6 +179,19 @@ def check(rc, what):
 
 def device_count():
     return lib().ksim_device_count()
+
+
+GO_INT63, GO_INTN, GO_FLOAT64, GO_PERM, GO_SHUFFLE = range(5)
+
+
+def go_rand(seed, op, n, arg=0):
+    """n draws of Go's math/rand after rand.Seed(seed) (include/ksim_trace.h ksim_go_rand)."""
+    out = (C.c_int64 * max(1, n))()
+    check(lib().ksim_go_rand(seed, op, arg, n, out), "ksim_go_rand")
+    if op == GO_FLOAT64:
+        import struct
+        return [struct.unpack("<d", struct.pack("<q", v))[0] for v in out[:n]]
+    return list(out[:n])
 
 
 # ---------------------------------------------------------------------------
@@ -249,9 +263,9 @@ class Trace:
         check(lib().ksim_trace_typical(self.h, C.byref(cfg), arr, cap, C.byref(n)), "ksim_trace_typical")
         return arr, n.value
 
-    def replay(self, seed, tune_ratio=1.3, shuffle=True):
+    def replay(self, seed, tune_ratio=1.3, shuffle=True, informer_draws=-1):
         """Event stream + empty cluster for one replica (SortClusterPods + tuning + node naming)."""
-        cfg = ReplayCfg(seed, tune_ratio, 1 if shuffle else 0, 0)
+        cfg = ReplayCfg(seed, tune_ratio, 1 if shuffle else 0, informer_draws)
         nn = self.num_nodes
         nodes = (Node * nn)()
         prefix = (C.c_int32 * nn)()

@@ -173,8 +173,13 @@ def curves(reports):
 
 def curves_arrays(arrs):
     """Vectorised curves of one replica from ksim.Engine.report_arrays (for sweeps of ~1000
-    replicas).  Same values as curves() except that a bucket mean is summed in bincount order
-    instead of pandas' order, which can move a 2-decimal rounding by 0.01 in rare ties."""
+    replicas), equal to curves(), i.e. to the reference's scripts, value for value.
+
+    arrived_gpu_milli only grows (simulator.go:407-409 adds on creation, nothing subtracts), so
+    the rows merge_*_discrete.py select for one arrived-GPU % -- and for its +-1 fallback -- are a
+    contiguous run of events in event order.  Their mean is taken as pandas takes it
+    (nanops.nanmean: numpy's pairwise sum of that run / count) and rounded as round() rounds a
+    numpy float64."""
     import numpy as np
     b = arrs["frag_bins"]
     idle = np.zeros(len(b))
@@ -188,24 +193,19 @@ def curves_arrays(arrs):
         ratio = 100 * frag / idle
     frag_p = np.array([float(_go_f2(x)) for x in frag.tolist()])    # the printed %.2f values
     ratio_p = np.array([float(_go_f2(x)) for x in ratio.tolist()])
-    total = int(arrs["total_gpus"][0])
+    total = arrs["total_gpus"][0]
     arrive = np.array([round(x, 0) for x in (arrs["arrived_gpu_milli"] / total / 10).tolist()])
     alloc = np.array([round(x, 2) for x in (arrs["used_gpu_milli"] / total / 10).tolist()])
-    ok = (arrive >= 0) & (arrive <= 131)
-    idx = np.where(ok, arrive, 132).astype(np.int64)
-    cnt = np.bincount(idx, minlength=133)[:132]
-    sums = {name: np.bincount(idx, weights=v, minlength=133)[:132]
-            for name, v in (("alloc", alloc), ("frag", frag_p), ("ratio", ratio_p))}
+    assert len(arrive) == 0 or bool(np.all(np.diff(arrive) >= 0)), "arrived GPU milli must not decrease"
     out = {"alloc": {}, "frag": {}, "frag_ratio": {}}
     for a in range(131):
-        if cnt[a] > 0:
-            sel = [a]
-        else:
-            sel = [x for x in (a - 1, a, a + 1) if 0 <= x < 132 and cnt[x] > 0]
-            if not sel:
+        lo, hi = np.searchsorted(arrive, a, "left"), np.searchsorted(arrive, a, "right")
+        if hi == lo:
+            lo, hi = np.searchsorted(arrive, a - 1, "left"), np.searchsorted(arrive, a + 1, "right")
+            if hi == lo:
                 continue
-        c = sum(cnt[x] for x in sel)
-        out["alloc"][a] = round(sum(sums["alloc"][x] for x in sel) / c, 2)
-        out["frag"][a] = round(100 * (sum(sums["frag"][x] for x in sel) / c) / 1000 / total, 2)
-        out["frag_ratio"][a] = sum(sums["ratio"][x] for x in sel) / c
+        cnt = np.float64(hi - lo)
+        out["alloc"][a] = float(round(alloc[lo:hi].sum() / cnt, 2))
+        out["frag"][a] = float(round(100 * (frag_p[lo:hi].sum() / cnt) / 1000 / total, 2))
+        out["frag_ratio"][a] = float(ratio_p[lo:hi].sum() / cnt)
     return out

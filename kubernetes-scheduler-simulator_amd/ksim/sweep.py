@@ -1,5 +1,9 @@
 """The paper sweep (C4): traces x policies x seeds as independent replicas on one GPU.
 
+Seeds reproduce the reference's event streams and node names exactly (Go math/rand,
+csrc/go_rand.hpp), so each experiment's curves can be compared row for row with the
+reference's expected_results (row_mismatches).
+
 The reference runs each (trace, policy, seed) experiment as its own `simon apply` process,
 1020 of them in ~10 h on 256 vCPUs (experiments/README.md:19-27,69-70; run lists in
 experiments/run_scripts/expected_run_scripts_0511.sh).  Here every experiment is one replica of
@@ -80,6 +84,31 @@ def mean_curve(curves, trace, policy, kind="alloc"):
     rows = [c[kind] for (t, p, _), c in curves.items() if t == trace and p == policy]
     keys = sorted(set.intersection(*[set(r) for r in rows]))
     return {k: float(np.mean([r[k] for r in rows])) for k in keys}
+
+
+def expected_rows(csv_path):
+    """expected_results/analysis_*_discrete.csv -> {(trace, policy, seed): {arrived %: value}}"""
+    import pandas as pd
+    df = pd.read_csv(csv_path)
+    cols = [c for c in df.columns if c.isdigit()]
+    out = {}
+    for rec in df.to_dict(orient="records"):
+        out[(rec["workload"], rec["sc_policy"], int(rec["seed"]))] = {
+            int(c): float(rec[c]) for c in cols if rec[c] == rec[c]}  # NaN: no data at that %
+    return out
+
+
+def row_mismatches(curves, kind, expected):
+    """Per experiment: the arrived-GPU % at which our curve differs from the reference's row
+    (values compared exactly: both are 2-decimal roundings of the same computation)."""
+    out = {}
+    for key, c in curves.items():
+        ref = expected.get(key)
+        if ref is None:
+            continue
+        ours = c[kind]
+        out[key] = sorted(k for k in set(ours) | set(ref) if ours.get(k) != ref.get(k))
+    return out
 
 
 def expected_mean_curve(csv_path, trace, policy, seeds=SEEDS):

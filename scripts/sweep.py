@@ -2,7 +2,8 @@
 write its curves in the format of the reference's experiments/analysis/expected_results:
   <out>/analysis_allo_discrete.csv, <out>/analysis_frag_discrete.csv  (one row per experiment)
   <out>/compare.json   per (trace, policy): max |ours - reference| of the 10-seed mean curves
-                       over arrived-GPU % 0..130, and the sweep's timing
+                       over arrived-GPU % 0..130; per policy: how many experiments reproduce
+                       the reference's row exactly; the sweep's timing
 Multi-GPU: torchrun --nproc-per-node N scripts/sweep.py; rank k replays experiments k::N (no
 collective on the data path); each rank writes its own CSV files (suffix .rank<k>).
 """
@@ -70,9 +71,20 @@ def main():
                     worst[kind] = max(worst[kind], dev)
                 summary["pairs"]["%s/%s" % (t, p)] = d
         summary["worst_max_abs_dev"] = worst
+        # row for row: every experiment's curve against the reference's row of the same seed
+        rows = {}
+        for kind, csv in (("alloc", "analysis_allo_discrete.csv"), ("frag", "analysis_frag_discrete.csv")):
+            mm = SW.row_mismatches(curves, kind, SW.expected_rows(os.path.join(EXPECTED, csv)))
+            for p in SW.POLICY_DIRS:
+                sel = {k: v for k, v in mm.items() if k[1] == p}
+                rows.setdefault(p, {})[kind] = {
+                    "rows": len(sel), "identical": sum(1 for v in sel.values() if not v),
+                    "differing": ["%s/%d: %d points from %s" % (k[0], k[2], len(v), v[0])
+                                  for k, v in sorted(sel.items()) if v][:20]}
+        summary["rows_identical"] = rows
     with open(os.path.join(args.out, "compare.json" + suffix), "w") as f:
         json.dump(summary, f, indent=1)
-    print(json.dumps({k: v for k, v in summary.items() if k != "pairs"}))
+    print(json.dumps({k: (v if k != "rows_identical" else {p: {kk: vv["identical"] for kk, vv in d.items()} for p, d in v.items()}) for k, v in summary.items() if k != "pairs"}))
 
 
 if __name__ == "__main__":
