@@ -33,7 +33,7 @@ BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # HBM bytes per launch of the dominant kernel of this default workload from the PMC passes of
 # scripts/profile_round.sh (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section)
-PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("memo", "round_end")]
+PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("gorand", "memo", "round_end")]
 
 
 def cpu_baseline(trace, seed, threads):
@@ -187,7 +187,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32+f64",
-        "data": "Alibaba openb trace (data/openb, from the reference's data/csv), documented event order",
+        "data": "Alibaba openb trace (data/openb, from the reference's data/csv), the reference's own event order (Go math/rand replay)",
         "config": {"workload": "C2: openb 1213 GPU nodes x openb_pod_list_default, FGD, tune 1.3, shuffled, "
                                "%d seeds per GPU replayed to completion" % args.replicas,
                    "replicas_per_gpu": args.replicas, "events_per_gpu": total_events,
@@ -200,7 +200,7 @@ def main():
                      "wgs_per_replica": eng.last_run_wgs()},
     }
     if args.config == "c4":
-        line["data"] = "Alibaba openb traces (data/openb: 17 pod lists), documented event order"
+        line["data"] = "Alibaba openb traces (data/openb: 17 pod lists), the reference's own event order (Go math/rand replay)"
         line["config"] = {"workload": "C4: paper sweep, 17 traces x 6 policies x seeds 42-51, tune 1.3, "
                                       "per-event cluster report", "replicas_per_gpu": args.replicas,
                           "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
