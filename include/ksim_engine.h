@@ -66,7 +66,10 @@ enum ksim_policy {
     KSIM_POLICY_DOTPROD = 2,        /* dimExtMethod=merge, normMethod=max (paper configuration) */
     KSIM_POLICY_GPUPACKING = 3,
     KSIM_POLICY_GPUCLUSTERING = 4,
-    KSIM_POLICY_RANDOM = 5
+    KSIM_POLICY_RANDOM = 5,
+    KSIM_POLICY_PWR = 6,            /* PWRScore (pkg/simulator/plugin/pwr_score.go), weight 1000 */
+    KSIM_POLICY_PWR_FGD = 7         /* PWRScore + FGDScore, weighted (ksim_engine_set_weights; default
+                                       500 / 500 = "PWR 500 FGD 500", generate_run_scripts.py:40) */
 };
 
 /* Open-Gpu-Share gpuSelMethod (pkg/type/config.go:36-42; "FGDScore" selects the FGD selector) */
@@ -74,7 +77,8 @@ enum ksim_gpusel {
     KSIM_GPUSEL_BEST = 0,
     KSIM_GPUSEL_WORST = 1,
     KSIM_GPUSEL_RANDOM = 2,
-    KSIM_GPUSEL_FGD = 3
+    KSIM_GPUSEL_FGD = 3,
+    KSIM_GPUSEL_PWR = 4             /* "PWRScore": allocateGpuIdBasedOnPWRScore (pwr_score.go:214-219) */
 };
 
 /* Result status (framework.Status codes) */
@@ -95,8 +99,30 @@ typedef struct {
     int32_t  pods_used;            /* len(nodeInfo.Pods) */
     int32_t  gpu_used_milli[KSIM_MAX_GPU]; /* DeviceInfo.GetUsedGpuMilli per device */
     int32_t  tag_count[KSIM_NUM_TAGS];     /* pods per GpuClustering tag on the node */
-    int32_t  reserved;
+    int32_t  cpu_model;            /* alibabacloud.com/cpu-model as a ksim_power_model CPU id (0 = no label) */
 } ksim_node;
+
+/* The PWR energy model (GetEnergyConsumptionNode, pkg/type/resource.go:536-563, with the tables of
+ * pkg/type/open-gpu-share/utils/const.go:41-124): node power = CPU power + GPU power, in watts.
+ *   GPU: idle_w * fully-free GPUs + full_w * the others, for GPU model id t (skipped for a model
+ *        flagged gpu_unlabelled: a node without gpu-card-model label);
+ *   CPU: ceil(cap/1000/2) physical cores, floor(left/1000/2) idle; CPUs of cpu_cores cores each,
+ *        idle_w per idle CPU + full_w per active CPU.
+ * A GPU model outside gpu_valid | gpu_unlabelled, or a CPU model outside cpu_valid, makes the PWR
+ * Score fail (the reference calls a nil func / divides by a zero core count).
+ * ksim_trace_power_model fills it from the reference's tables for a trace's vocabulary. */
+#define KSIM_MAX_CPU_MODELS 8
+typedef struct {
+    double   gpu_idle_w[KSIM_MAX_TYPES];
+    double   gpu_full_w[KSIM_MAX_TYPES];
+    double   cpu_idle_w[KSIM_MAX_CPU_MODELS];
+    double   cpu_full_w[KSIM_MAX_CPU_MODELS];
+    double   cpu_cores[KSIM_MAX_CPU_MODELS];
+    uint32_t gpu_valid;
+    uint32_t gpu_unlabelled;
+    uint32_t cpu_valid;
+    uint32_t reserved;
+} ksim_power_model;
 
 /* A pod (creation or deletion event).  PodResource (pkg/type/resource.go:51-58)
  * plus the Filter request vector (fit.go computePodResourceRequest). */
@@ -173,6 +199,10 @@ void ksim_engine_destroy(ksim_engine* e);
 int  ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes);
 int  ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp, int n);
 int  ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed);
+/* PWR policies: the energy model (required before running a PWR replica) and, for
+ * KSIM_POLICY_PWR_FGD, the two plugin weights of the scheduler configuration. */
+int  ksim_engine_set_power_model(ksim_engine* e, int replica, const ksim_power_model* pm);
+int  ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t w_fgd);
 
 /* Plugin-level entry points (no state change).  For one pod, Filter + Score
  * every node of the replica: feasible[n] (0/1), score[n] (the plugin's Score

@@ -100,6 +100,14 @@ int  ksim_trace_typical(const ksim_trace* t, const ksim_typical_cfg* cfg, ksim_t
 int  ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
                        int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix);
 
+/* The PWR energy model of the reference (const.go:41-124) for this trace's GPU-model
+ * vocabulary: models named in MapGpuTypeModelEnergy get their idle / full watts (G2 -> A10,
+ * G3 -> A100), the empty name is "no label"; CPU model ids are
+ *   0 ""  1 Intel-Xeon-8269CY  2 Intel-Xeon-8163  3 Intel-Xeon-ES-2682-V4  4 Intel-Xeon-6326
+ *   5 Intel-Xeon-8369B
+ * (the openb node lists carry no cpu-model label: every node is CPU model 0). */
+int  ksim_trace_power_model(const ksim_trace* t, ksim_power_model* out);
+
 /* Go math/rand (src/math/rand) on a source seeded with rand.Seed(seed): n draws of
  *   KSIM_GO_INT63    Int63()
  *   KSIM_GO_INTN     Intn(arg)

@@ -138,6 +138,12 @@ struct ReplicaDev {
   int32_t* last;         // [N] k_step: last event that changed each node
   int32_t node_off;      // node-sharded cluster: global index (= name rank) of local node 0, else 0
   int32_t pad_;
+  // PWR (pwr_score.go): energy model, CPU model id per node, per-node PWR scratch of the
+  // two-phase k_step cycle (raw PWR score | packed FGD score and GPU choices), plugin weights
+  const struct PowerDev* pw;
+  const uint8_t* cpum;   // [N]
+  int2* pws;             // [N]
+  int32_t w_pwr, w_fgd;
 };
 
 // Per-event cluster report, exact (fixed point 2^-80 for the fp64 bins; see fix80).
@@ -159,8 +165,22 @@ struct __align__(64) Accum {
   int32_t pad[9];
 };
 
-enum : int { POL_FGD = 0, POL_BESTFIT = 1, POL_DOTPROD = 2, POL_PACKING = 3, POL_CLUSTERING = 4, POL_RANDOM = 5 };
-enum : int { SEL_BEST = 0, SEL_WORST = 1, SEL_RANDOM = 2, SEL_FGD = 3 };
+enum : int { POL_FGD = 0, POL_BESTFIT = 1, POL_DOTPROD = 2, POL_PACKING = 3, POL_CLUSTERING = 4, POL_RANDOM = 5,
+             POL_PWR = 6, POL_PWR_FGD = 7 };
+enum : int { SEL_BEST = 0, SEL_WORST = 1, SEL_RANDOM = 2, SEL_FGD = 3, SEL_PWR = 4 };
+KSIM_HD bool is_pwr_policy(int pol) { return pol == POL_PWR || pol == POL_PWR_FGD; }
+
+// PWR energy model (== ksim_power_model): resource.go:536-563 GetEnergyConsumptionNode with the
+// const.go:41-124 tables, indexed by GPU model id and CPU model id
+constexpr int kMaxCpuModels = 8;
+struct PowerDev {
+  double gidle[32], gfull[32];
+  double cidle[kMaxCpuModels], cfull[kMaxCpuModels], cnc[kMaxCpuModels];
+  uint32_t gvalid;  // GPU model ids with an energy model (MapGpuTypeModelEnergy)
+  uint32_t gnone;   // GPU model ids standing for "no gpu-card-model label" (GpuType == "": no GPU term)
+  uint32_t cvalid;
+  uint32_t pad;
+};
 enum : int { ST_OK = 0, ST_UNSCHED = 1, ST_ERROR = 2, ST_DELETED = 3 };
 
 // ---------------------------------------------------------------------------
@@ -462,6 +482,76 @@ KSIM_HD int exclusive_gpu_mask(const NodeV& n, const PodDev& p) {
   }
   return req > 0 ? -1 : mask;
 }
+
+// GetEnergyConsumptionNode (resource.go:536-563) of a node state; false when the reference would
+// fail (a GPU model without an energy model: nil func call; an unknown CPU model).  Go's
+// operation order; every term is an exact small integer in fp64.
+KSIM_HD bool node_energy(int cpuL, int cap, int cm, const int (&gl)[kMaxGpu], int cnt, int gtype, const PowerDev& pw,
+                         double* energy) {
+  double gpu = 0;
+  if (!((pw.gnone >> gtype) & 1u)) {
+    if (!((pw.gvalid >> gtype) & 1u)) return false;
+    int free_gpus = 0;  // GetFullyFreeGpuNum (resource.go:170-177)
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) free_gpus += (g < cnt && gl[g] == kMilli) ? 1 : 0;
+    const double num_idle = (double)free_gpus;
+    const double num_working = (double)cnt - num_idle;
+    gpu = (pw.gidle[gtype] * num_idle) + (pw.gfull[gtype] * num_working);
+  }
+  if (!((pw.cvalid >> cm) & 1u)) return false;
+  const double real_cores = ceil((double)cap / (double)kMilli / 2);
+  const double idle_cores = floor((double)cpuL / (double)kMilli / 2);
+  const double working_cores = real_cores - idle_cores;
+  const double nc = pw.cnc[cm];
+  const double num_cpus = ceil(real_cores / nc);
+  const double num_active = ceil(working_cores / nc);
+  const double num_idle_cpus = num_cpus - num_active;
+  const double cpu = (pw.cidle[cm] * num_idle_cpus) + (pw.cfull[cm] * num_active);
+  *energy = cpu + gpu;  // pwr_score.go:147 old_CPU_energy + old_GPU_energy
+  return true;
+}
+
+// calculatePWRShareExtendScore (pwr_score.go:143-212): int64(old - new) energy; share pods try every
+// fitting GPU (first, then strictly better; *gpu = its index), others take NodeResource.Sub
+// (resource.go:454-480).  *err when the energy model fails.
+KSIM_HD int pwr_score(const NodeV& n, const PodDev& p, int cap, int cm, const PowerDev& pw, int* gpu, bool* err) {
+  int gl[kMaxGpu];
+  unpack_gl(n, gl);
+  const int cnt = n.gpu_cnt(), gt = n.gpu_type();
+  double old_e = 0, new_e = 0;
+  *gpu = -1;
+  *err = !node_energy(n.cpu_left, cap, cm, gl, cnt, gt, pw, &old_e);
+  if (*err) return 0;
+  if (is_share_pod(p)) {
+    int score = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      if (g < cnt && gl[g] >= p.milli) {
+        int c[kMaxGpu];
+#pragma unroll
+        for (int h = 0; h < kMaxGpu; ++h) c[h] = gl[h] - (h == g ? (int)p.milli : 0);
+        (void)node_energy(n.cpu_left - p.cpu_nz, cap, cm, c, cnt, gt, pw, &new_e);
+        const int s = (int)(long long)(old_e - new_e);
+        if (*gpu < 0 || s > score) { score = s; *gpu = g; }
+      }
+    }
+    return score;
+  }
+  bool ok = false;
+  int cpuL = n.cpu_left;
+  const unsigned sm = sub_gpu_mask(gl, cnt, cpuL, p, &ok);
+  if (ok) {
+    cpuL -= p.cpu_nz;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g)
+      if ((sm >> g) & 1u) gl[g] -= p.milli;
+  }
+  (void)node_energy(cpuL, cap, cm, gl, cnt, gt, pw, &new_e);
+  return (int)(long long)(old_e - new_e);
+}
+
+// PWRScorePlugin.NormalizeScore (pwr_score.go:104-141)
+KSIM_HD int pwr_normalize(int s, int lo, int hi) { return lo == hi ? 100 : (int)((long long)(s - lo) * 100 / (hi - lo)); }
 
 // getBestFitScore (best_fit_score.go:66-97); -1 = error
 KSIM_HD int bestfit_score(const NodeV& n, const PodDev& p, int total) {

@@ -29,6 +29,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +101,7 @@ __device__ int select_gpus(const NodeV& n, const PodDev& p, int gpusel, int fgd_
   if (!is_share_pod(p)) return exclusive_gpu_mask(n, p);              // exclusive branch of every selector
   switch (gpusel) {
     case SEL_FGD:                                                     // fgd_score.go:153-156
+    case SEL_PWR:                                                     // pwr_score.go:214-219
       return fgd_gpu < 0 ? -1 : (1 << fgd_gpu);
     case SEL_RANDOM: {                                                // :325-343 (Random contract)
       const uint64_t nk = rand_node_key(seed, step, n.name_rank);
@@ -222,7 +224,7 @@ __device__ __forceinline__ int cheap_score(const NodeV& n, const PodDev& p, uint
 // point at global memory (k_step) or LDS (k_replay).
 __device__ __forceinline__ bool node_phase1(const NodeV& n, const PodDev& p, const ReplicaDev& rp,
                                             const uint16_t* tags, int step, bool share, int* raw, int* nc,
-                                            bool* err) {
+                                            bool* err, int node = 0, int* pgpu = nullptr) {
   *raw = 0;
   *nc = 0;
   *err = false;
@@ -252,6 +254,16 @@ __device__ __forceinline__ bool node_phase1(const NodeV& n, const PodDev& p, con
       if (p.tag == -2) *err = true;
       else *raw = clustering_score(tags, p.tag, total);
       break;
+    case POL_PWR:
+    case POL_PWR_FGD: {  // pwr_score.go:48-91 (+ FGD's candidates for the weighted combination)
+      int g = -1;
+      bool perr = false;
+      *raw = pwr_score(n, p, rp.cap[node], rp.cpum[node], *rp.pw, &g, &perr);
+      *err = perr;
+      if (pgpu) *pgpu = g;
+      if (rp.policy == POL_PWR_FGD) *nc = share ? 1 + __builtin_popcount(first_of_class(n, p.milli)) : 2;
+      break;
+    }
     default:  // POL_RANDOM: RandomScorePlugin.PreScore pick, as a 24-bit hash key
       *raw = (int)(rand_node_key(rp.seed, step, n.name_rank) >> 40);
       break;
@@ -331,6 +343,7 @@ __device__ __forceinline__ long long result_score(const ReplicaDev& rp, int nfea
   if (nfeas <= 1) return 0;
   if (rp.policy == POL_BESTFIT) return (hi > lo ? 100 : 0) * 1000LL;  // NormalizeScore (plugin_utils.go:48-74)
   if (rp.policy == POL_RANDOM) return 100 * 1000LL;
+  if (rp.policy == POL_PWR_FGD) return (long long)wscore;  // already w_pwr * PWR + w_fgd * FGD
   return (long long)wscore * 1000LL;
 }
 
@@ -366,6 +379,10 @@ __device__ void finish_cycle(const StepArgs& a, const ReplicaDev& rp, const PodD
   }
   *res_slot = out;
 }
+
+// PWR raw scores are energy deltas old - new <= 0 W (pwr_score.go:167,200); biased into the
+// non-negative range of the Accum min / max.
+constexpr int kPwrBias = 1 << 30;
 
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __restrict__ tp_all) {
   const int r = a.rep_first + (int)blockIdx.x / a.bpr;
@@ -410,18 +427,21 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
 
   const int n0 = b * a.NB;
   const int nb = max(0, min(a.NB, a.N - n0));
-  const bool fgd = rp.policy == POL_FGD;
+  const bool fgd = rp.policy == POL_FGD || rp.policy == POL_PWR_FGD;
+  const bool pwr = is_pwr_policy(rp.policy);
   const bool share = is_share_pod(p);
 
-  // ---- phase 1: Filter (+ cheap scores) ----
+  // ---- phase 1: Filter (+ cheap scores; PWR's raw score) ----
   bool feas = false, err = false;
-  int raw = 0, nc = 0, gpu = -1;
+  int raw = 0, nc = 0, gpu = -1, pgpu = -1;
   NodeV n{};
   if (tid < nb) {
     n = load_node(rp.nodes + n0 + tid);
     store_node(&s_node[tid], n);
-    feas = node_phase1(n, p, rp, rp.tags + (size_t)(n0 + tid) * kTagStride, step, share, &raw, &nc, &err);
+    feas = node_phase1(n, p, rp, rp.tags + (size_t)(n0 + tid) * kTagStride, step, share, &raw, &nc, &err, n0 + tid,
+                       &pgpu);
   }
+  const int praw = raw;  // PWR policies: the PWR score before NormalizeScore
 
   // ---- phase 2: FGD candidate evaluation over a compacted work list ----
   if (fgd) {
@@ -449,14 +469,23 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
   if (a.mode == 1) {
     if (tid < nb) {
       a.out_feas[n0 + tid] = feas ? 1 : 0;
-      a.out_score[n0 + tid] = feas ? raw : 0;
-      a.out_gpu[n0 + tid] = feas ? select_gpus(n, p, rp.gpusel, gpu, rp.seed, step) : 0;
+      a.out_score[n0 + tid] = feas ? (pwr ? praw : raw) : 0;
+      a.out_gpu[n0 + tid] = feas ? select_gpus(n, p, rp.gpusel, rp.gpusel == SEL_PWR ? pgpu : gpu, rp.seed, step) : 0;
     }
     return;
   }
+  if (pwr && tid < nb) {
+    // phase A of a PWR cycle: PWRScorePlugin.NormalizeScore needs the min / max raw score over the
+    // feasible nodes first, so the per-node scores wait in HBM for k_step_pwr (same step, next launch)
+    const int fgpu = rp.policy == POL_PWR_FGD ? gpu : -1;
+    rp.pws[n0 + tid] = make_int2(feas ? praw : INT_MIN,
+                                 (rp.policy == POL_PWR_FGD ? (raw & 0xff) : 0) | ((pgpu + 1) & 0xf) << 8 |
+                                     ((fgpu + 1) & 0xf) << 12);
+  }
+  if (pwr) raw = praw + kPwrBias;  // the min / max accumulators start at -1 (raw PWR scores are <= 0)
 
   // ---- phase 3: workgroup reduction of the packed argmax key ----
-  unsigned long long key = feas ? pack_key((unsigned)raw, n.name_rank, gpu) : 0ull;
+  unsigned long long key = (feas && !pwr) ? pack_key((unsigned)raw, n.name_rank, gpu) : 0ull;
   int cnt = feas ? 1 : 0;
   int lo = feas ? raw : 0x7fffffff, hi = feas ? raw : -1;
   key = wave_max_u64(key);
@@ -485,6 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
     __hip_atomic_fetch_max(&ac->hi, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (errb) __hip_atomic_fetch_or(&ac->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (pwr) return;  // k_step_pwr finishes the cycle
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every contribution performed before the ticket
   const unsigned t = __hip_atomic_fetch_add(&ac->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t != (unsigned)(a.bpr - 1)) return;
@@ -505,6 +535,57 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
     return;
   }
   // the rank -> node index map lives right after the replica's tags (see host)
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
+  finish_cycle(a, rp, p, step, res_slot, best, nfeas, anyerr, glo, ghi, best ? rank2idx[key_rank(best)] : -1);
+}
+
+// Phase B of a PWR / PWR+FGD cycle (after k_step's phase A of the same step): the normalized PWR
+// score (pwr_score.go:104-141) with the replica's min / max raw score, the weighted sum with FGD
+// (framework.go:686-704, generic_scheduler.go:511-519), the packed argmax key, and the last
+// workgroup of the replica finishes the cycle as k_step does.
+__global__ __launch_bounds__(kBlock) void k_step_pwr(StepArgs a) {
+  const int r = a.rep_first + (int)blockIdx.x / a.bpr;
+  const int b = (int)blockIdx.x % a.bpr;
+  const int tid = (int)threadIdx.x;
+  const ReplicaDev rp = a.reps[r];
+  if (!is_pwr_policy(rp.policy)) return;
+  const int step = (a.base ? *a.base : 0) + a.step_off;
+  if (!a.pod_override && step >= rp.n_events) return;
+  const PodDev p = a.pod_override ? *a.pod_override : rp.ev[step];
+  if (p.flags & kPodDelete) return;
+  ResultDev* res_slot = a.res_override ? a.res_override : (rp.res + step);
+  Accum* ac = a.acc + r;
+  const int lo = __hip_atomic_load(&ac->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int hi = __hip_atomic_load(&ac->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ unsigned long long s_rkey[kBlock / 64];
+  const int n0 = b * a.NB;
+  const int nb = max(0, min(a.NB, a.N - n0));
+  unsigned long long key = 0ull;
+  if (tid < nb) {
+    const int2 v = rp.pws[n0 + tid];
+    if (v.x != INT_MIN) {
+      const int norm = pwr_normalize(v.x + kPwrBias, lo, hi);
+      const int pg = ((v.y >> 8) & 0xf) - 1, fg = ((v.y >> 12) & 0xf) - 1;
+      const int total = rp.policy == POL_PWR_FGD ? rp.w_pwr * norm + rp.w_fgd * (v.y & 0xff) : norm;
+      key = pack_key((unsigned)total, rp.nodes[n0 + tid].name_rank, rp.gpusel == SEL_PWR ? pg : fg);
+    }
+  }
+  key = wave_max_u64(key);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) s_rkey[w] = key;
+  __syncthreads();
+  if (tid != 0) return;
+  for (int i = 1; i < kBlock / 64; ++i) key = s_rkey[i] > key ? s_rkey[i] : key;
+  if (key) __hip_atomic_fetch_max(&ac->best, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the contribution performed before the ticket
+  const unsigned t = __hip_atomic_fetch_add(&ac->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != (unsigned)(a.bpr - 1)) return;
+  const unsigned long long best = __hip_atomic_exchange(&ac->best, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nfeas = __hip_atomic_exchange(&ac->nfeas, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int anyerr = __hip_atomic_exchange(&ac->err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int glo = __hip_atomic_exchange(&ac->lo, 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ghi = __hip_atomic_exchange(&ac->hi, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&ac->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)a.N * kTagStride);
   finish_cycle(a, rp, p, step, res_slot, best, nfeas, anyerr, glo, ghi, best ? rank2idx[key_rank(best)] : -1);
 }
@@ -1057,6 +1138,11 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
       }
     }
   }
+  if (rp.gpusel == SEL_PWR && is_share_pod(p) && p.milli > 0) {  // allocateGpuIdBasedOnPWRScore
+    bool perr = false;
+    (void)pwr_score(n, p, rp.cap[node], rp.cpum[node], *rp.pw, &fgd_gpu, &perr);
+    if (perr) fgd_gpu = -1;
+  }
   const int mask = select_gpus(n, p, rp.gpusel, fgd_gpu, rp.seed, step);
   *out_mask = mask;
   if (mask >= 0) apply_bind(nr, tg, p, mask, +1);
@@ -1133,10 +1219,16 @@ struct ksim_engine {
   bool mplan_ok = false;
   std::vector<int> mplan_reps;
   int mplan_max_ev = -1;
-  int last_memo = 0;  // replicas of the last run replayed by k_memo
+  int last_memo = 0;
+  bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
   int graph_R = -1;
+  bool graph_pwr = false;    // the graph carries k_step_pwr after every k_step
+  PowerDev* d_pw = nullptr;  // [R] PWR energy model
+  uint8_t* d_cpum = nullptr; // [R][N] CPU model id per node
+  int2* d_pws = nullptr;     // [R][N] PWR phase-A scratch
+  std::vector<char> pw_set;  // set_power_model called
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
@@ -1559,6 +1651,12 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
   KSIM_HIP(hipMalloc(&e->d_replist, sizeof(int) * (size_t)n_replicas));
   KSIM_HIP(hipMalloc(&e->d_cap, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_pw, sizeof(PowerDev) * (size_t)n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_cpum, (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_pws, sizeof(int2) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMemset(e->d_pw, 0, sizeof(PowerDev) * (size_t)n_replicas));
+  KSIM_HIP(hipMemset(e->d_cpum, 0, (size_t)n_nodes * n_replicas));
+  e->pw_set.assign(n_replicas, 0);
   KSIM_HIP(hipMalloc(&e->d_last, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMemset(e->d_cap, 0, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
@@ -1594,6 +1692,10 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     rp.cap = e->d_cap + (size_t)r * n_nodes;
     rp.init = e->d_nodes_init + (size_t)r * n_nodes;
     rp.last = e->d_last + (size_t)r * n_nodes;
+    rp.pw = e->d_pw + r;
+    rp.cpum = e->d_cpum + (size_t)r * n_nodes;
+    rp.pws = e->d_pws + (size_t)r * n_nodes;
+    rp.w_pwr = 1000;
   }
   KSIM_HIP(hipEventCreate(&e->ev0));
   KSIM_HIP(hipEventCreate(&e->ev1));
@@ -1617,7 +1719,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
-                  e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th};
+                  e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -1654,6 +1756,7 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
   if (!e || !nodes || replica < 0 || replica >= e->R) return KSIM_EINVAL;
   std::vector<NodeRec> h(e->N);
   std::vector<int32_t> cap(e->N);
+  std::vector<uint8_t> cpum(e->N);
   int64_t gpus = 0;
   std::vector<uint16_t> tags(e->tags_stride, 0);
   int* rank2idx = reinterpret_cast<int*>(tags.data() + (size_t)e->N * kTagStride);
@@ -1668,6 +1771,8 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     if (lr >= (uint32_t)e->N || seen[lr]) return KSIM_EINVAL;
     if (s.cpu_alloc_milli < 0 || s.cpu_alloc_milli > 0x3fffffff) return KSIM_ERANGE;
     cap[i] = (int32_t)s.cpu_alloc_milli;
+    if (s.cpu_model < 0 || s.cpu_model >= kMaxCpuModels) return KSIM_ERANGE;
+    cpum[i] = (uint8_t)s.cpu_model;
     gpus += s.gpu_count;
     seen[lr] = 1;
     const int64_t cpu_left = s.cpu_alloc_milli - s.cpu_used_milli;
@@ -1697,6 +1802,7 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
   KSIM_HIP(hipSetDevice(e->device));
   KSIM_HIP(hipMemcpyAsync(e->d_cap + (size_t)replica * e->N, cap.data(), sizeof(int32_t) * e->N, hipMemcpyHostToDevice,
                           e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_cpum + (size_t)replica * e->N, cpum.data(), e->N, hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemcpyAsync(e->reps[replica].nodes, h.data(), sizeof(NodeRec) * e->N, hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemcpyAsync(e->d_tags + (size_t)replica * e->tags_stride, tags.data(), sizeof(uint16_t) * e->tags_stride,
                           hipMemcpyHostToDevice, e->stream));
@@ -1750,7 +1856,16 @@ int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp,
 int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed) {
   if (e) e->mplan_dirty = true;
   if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
-  if (policy < POL_FGD || policy > POL_RANDOM || gpusel < SEL_BEST || gpusel > SEL_FGD) return KSIM_ENOTSUP;
+  if (policy < POL_FGD || policy > POL_PWR_FGD || gpusel < SEL_BEST || gpusel > SEL_PWR) return KSIM_ENOTSUP;
+  // allocateGpuIdFunc only holds the selectors of the enabled plugins (fgd_score.go:37, pwr_score.go:40)
+  if (gpusel == SEL_PWR && !is_pwr_policy(policy)) return KSIM_ENOTSUP;
+  if (policy == POL_PWR_FGD && e->reps[replica].policy != POL_PWR_FGD) {
+    e->reps[replica].w_pwr = 500;  // "PWR 500 FGD 500" (generate_run_scripts.py:40) until set_weights
+    e->reps[replica].w_fgd = 500;
+  } else if (policy == POL_PWR) {
+    e->reps[replica].w_pwr = 1000;
+    e->reps[replica].w_fgd = 0;
+  }
   e->reps[replica].policy = policy;
   e->reps[replica].gpusel = gpusel;
   e->reps[replica].seed = seed;
@@ -1759,6 +1874,38 @@ int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, 
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
   return KSIM_OK;
+}
+
+int ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t w_fgd) {
+  if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  if (e->reps[replica].policy != POL_PWR_FGD) return KSIM_ESTATE;
+  // framework weights are positive; the packed key holds w_pwr * 100 + w_fgd * 100 in 24 bits
+  if (w_pwr <= 0 || w_fgd <= 0 || w_pwr > 50000 || w_fgd > 50000) return KSIM_ERANGE;
+  e->reps[replica].w_pwr = w_pwr;
+  e->reps[replica].w_fgd = w_fgd;
+  KSIM_HIP(hipSetDevice(e->device));
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_set_power_model(ksim_engine* e, int replica, const ksim_power_model* pm) {
+  static_assert(sizeof(ksim_power_model) == sizeof(PowerDev), "ksim_power_model layout");
+  if (!e || !pm || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  for (int c = 0; c < kMaxCpuModels; ++c)
+    if (((pm->cpu_valid >> c) & 1u) && !(pm->cpu_cores[c] > 0)) return KSIM_ERANGE;
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(e->d_pw + replica, pm, sizeof(PowerDev), hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  e->pw_set[replica] = 1;
+  return KSIM_OK;
+}
+
+static bool any_pwr(const ksim_engine* e) {
+  for (int r = 0; r < e->R; ++r)
+    if (is_pwr_policy(e->reps[r].policy)) return true;
+  return false;
 }
 
 static StepArgs base_args(ksim_engine* e) {
@@ -1779,6 +1926,9 @@ int ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, i
   int rc = to_pod_dev(*pod, &p);
   if (rc) return rc;
   if (p.flags & kPodDelete) return KSIM_EINVAL;
+  // one plugin's Score per call: a weighted combination has two (query PWR and FGD replicas)
+  if (e->reps[replica].policy == POL_PWR_FGD) return KSIM_ENOTSUP;
+  if (is_pwr_policy(e->reps[replica].policy) && !e->pw_set[replica]) return KSIM_ESTATE;
   KSIM_HIP(hipSetDevice(e->device));
   KSIM_HIP(hipMemcpyAsync(e->d_pod, &p, sizeof p, hipMemcpyHostToDevice, e->stream));
   StepArgs a = base_args(e);
@@ -1813,7 +1963,10 @@ int ksim_engine_schedule(ksim_engine* e, int replica, const ksim_pod* pod, int32
   a.pod_override = e->d_pod;
   a.res_override = e->d_res1;
   a.mode = 0;
+  if (is_pwr_policy(e->reps[replica].policy) && !e->pw_set[replica]) return KSIM_ESTATE;
   hipLaunchKernelGGL(k_step, dim3(e->bpr), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
+  if (is_pwr_policy(e->reps[replica].policy))
+    hipLaunchKernelGGL(k_step_pwr, dim3(e->bpr), dim3(kBlock), 0, e->stream, a);
   KSIM_HIP(hipGetLastError());
   ResultDev r;
   KSIM_HIP(hipMemcpyAsync(&r, e->d_res1, sizeof r, hipMemcpyDeviceToHost, e->stream));
@@ -2058,7 +2211,8 @@ static int run_sharded(ksim_engine* e, int max_ev) {
 }
 
 static int build_graph(ksim_engine* e) {
-  if (e->graph && e->graph_R == e->R) return KSIM_OK;
+  const bool pwr = any_pwr(e);
+  if (e->graph && e->graph_R == e->R && e->graph_pwr == pwr) return KSIM_OK;
   if (e->graph) { (void)hipGraphExecDestroy(e->graph); e->graph = nullptr; }
   hipGraph_t g;
   KSIM_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
@@ -2068,12 +2222,14 @@ static int build_graph(ksim_engine* e) {
   for (int i = 0; i < e->K; ++i) {
     a.step_off = i;
     hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
+    if (pwr) hipLaunchKernelGGL(k_step_pwr, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
   }
   hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_base, e->K);
   KSIM_HIP(hipStreamEndCapture(e->stream, &g));
   KSIM_HIP(hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0));
   KSIM_HIP(hipGraphDestroy(g));
   e->graph_R = e->R;
+  e->graph_pwr = pwr;
   return KSIM_OK;
 }
 
@@ -2246,8 +2402,13 @@ int ksim_engine_run(ksim_engine* e) {
   rc = reset_state(e);
   if (rc) return rc;
   if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N * e->R, e->stream));
-  if (e->shard_world > 0) rc = run_sharded(e, max_ev);
-  else rc = e->run_mode == 1 ? run_graph(e, max_ev) : run_persistent(e, max_ev);
+  // PWR policies run on the per-pod path: NormalizeScore over the cluster sits between Score and
+  // selectHost (k_step + k_step_pwr per pod, hipGraph)
+  const bool step_path = e->run_mode == 1 || any_pwr(e);
+  for (int r = 0; r < e->R; ++r)
+    if (is_pwr_policy(e->reps[r].policy) && !e->pw_set[r]) return KSIM_ESTATE;
+  if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
+  else rc = step_path ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
   if (e->report) {
@@ -2262,7 +2423,8 @@ int ksim_engine_run(ksim_engine* e) {
   e->last_ms = ms;
   e->last_report_ms = e->report ? rms : 0.0;
   e->last_steps = max_ev;
-  if (e->run_mode != 1 && e->shard_world == 0) {
+  e->last_step_path = step_path;
+  if (!step_path && e->shard_world == 0) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
     if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
@@ -2416,7 +2578,7 @@ int ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica) {
 int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   if (!e || !path) return KSIM_EINVAL;
   if (e->shard_world > 0) *path = KSIM_PATH_SHARDED;
-  else if (e->run_mode == 1) *path = KSIM_PATH_STEP;
+  else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
   else if (e->last_memo == 0) *path = KSIM_PATH_REPLAY;
   else *path = e->last_memo == e->R ? KSIM_PATH_MEMO : KSIM_PATH_MIXED;
   return KSIM_OK;
@@ -2436,6 +2598,7 @@ int ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us) 
     a.step_off = i;
     KSIM_HIP(hipEventRecord(evs[2 * i], e->stream));
     hipLaunchKernelGGL(k_step, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a, (const TypDev*)e->d_tp);
+    if (any_pwr(e)) hipLaunchKernelGGL(k_step_pwr, dim3(e->bpr * e->R), dim3(kBlock), 0, e->stream, a);
     KSIM_HIP(hipEventRecord(evs[2 * i + 1], e->stream));
   }
   KSIM_HIP(hipStreamSynchronize(e->stream));

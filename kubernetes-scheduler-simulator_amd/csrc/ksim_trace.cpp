@@ -446,6 +446,34 @@ int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod*
   return KSIM_OK;
 }
 
+int ksim_trace_power_model(const ksim_trace* t, ksim_power_model* out) {
+  if (!t || !out) return KSIM_EINVAL;
+  std::memset(out, 0, sizeof *out);
+  // const.go:62-69 MapGpuTypeEnergyConsumption via const.go:115-124 MapGpuTypeModelEnergy
+  static const struct { const char* name; double idle, full; } kGpu[] = {
+      {"T4", 10, 70}, {"A10", 30, 150}, {"P100", 25, 250}, {"V100M16", 30, 300},
+      {"V100M32", 30, 300}, {"A100", 50, 400}, {"G2", 30, 150}, {"G3", 50, 400}};
+  // const.go:48-55 MapCpuTypeEnergyConsumption
+  static const struct { double idle, full, cores; } kCpu[] = {
+      {15, 120, 16}, {20, 205, 26}, {20, 165, 24}, {15, 120, 16}, {20, 185, 16}, {20, 270, 32}};
+  for (size_t v = 0; v < t->vocab.size() && v < (size_t)KSIM_MAX_TYPES; ++v) {
+    if (t->vocab[v].empty()) { out->gpu_unlabelled |= 1u << v; continue; }
+    for (const auto& g : kGpu)
+      if (t->vocab[v] == g.name) {
+        out->gpu_idle_w[v] = g.idle;
+        out->gpu_full_w[v] = g.full;
+        out->gpu_valid |= 1u << v;
+      }
+  }
+  for (int c = 0; c < (int)(sizeof kCpu / sizeof kCpu[0]); ++c) {
+    out->cpu_idle_w[c] = kCpu[c].idle;
+    out->cpu_full_w[c] = kCpu[c].full;
+    out->cpu_cores[c] = kCpu[c].cores;
+    out->cpu_valid |= 1u << c;
+  }
+  return KSIM_OK;
+}
+
 int ksim_go_rand(int64_t seed, int op, int64_t arg, int n, int64_t* out) {
   if (n < 0 || (n > 0 && !out)) return KSIM_EINVAL;
   if ((op == KSIM_GO_INTN || op == KSIM_GO_PERM) && arg <= 0) return KSIM_EINVAL;

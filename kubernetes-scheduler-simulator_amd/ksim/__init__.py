@@ -3,7 +3,8 @@
 A thin ctypes layer over the C ABI in include/ksim_engine.h and
 include/ksim_trace.h.  It mirrors the reference's plugin vocabulary
 (Filter / Score / Reserve / Unreserve / schedule cycle; FGDScore, BestFitScore,
-DotProductScore, GpuPackingScore, GpuClusteringScore, RandomScore) so tests and
+DotProductScore, GpuPackingScore, GpuClusteringScore, RandomScore, PWRScore and the weighted
+PWRScore + FGDScore combinations) so tests and
 bench.py read like the reference's own tests.
 
 There is no CPU fallback: compute calls raise KsimError(KSIM_ENODEV) when no
@@ -27,11 +28,22 @@ KSIM_TYPE_ANY = 0xFFFFFFFF
 MAX_GPU = 8
 NUM_TAGS = 9
 
-POLICY = {"FGD": 0, "BestFit": 1, "DotProd": 2, "GpuPacking": 3, "GpuClustering": 4, "Random": 5}
-GPUSEL = {"best": 0, "worst": 1, "random": 2, "FGD": 3}
-# experiments/run_scripts/expected_run_scripts_0511.sh: policy -> gpuSelMethod
+POLICY = {"FGD": 0, "BestFit": 1, "DotProd": 2, "GpuPacking": 3, "GpuClustering": 4, "Random": 5,
+          "PWR": 6, "PWR+FGD": 7}
+GPUSEL = {"best": 0, "worst": 1, "random": 2, "FGD": 3, "PWR": 4}
+# experiments/run_scripts/expected_run_scripts_0511.sh and generate_run_scripts.py:31-42:
+# policy -> gpuSelMethod
 DEFAULT_GPUSEL = {"FGD": "FGD", "BestFit": "best", "DotProd": "best", "GpuPacking": "best",
-                  "GpuClustering": "best", "Random": "random"}
+                  "GpuClustering": "best", "Random": "random", "PWR": "PWR", "PWR+FGD": "FGD"}
+
+
+def parse_policy(name):
+    """generate_run_scripts.py policy strings: "FGD", "PWR", "PWR 500 FGD 500", ... ->
+    (POLICY key, weights or None)."""
+    parts = name.split()
+    if len(parts) == 4 and parts[0] == "PWR" and parts[2] == "FGD":
+        return "PWR+FGD", (int(parts[1]), int(parts[3]))
+    return name, None
 SCHEDULED, UNSCHEDULABLE, ERROR, DELETED = 0, 1, 2, 3
 
 
@@ -47,7 +59,17 @@ class Node(C.Structure):
                 ("gpu_count", C.c_int32), ("gpu_type", C.c_int32), ("name_rank", C.c_uint32),
                 ("cpu_used_milli", C.c_int64), ("mem_used_mib", C.c_int64), ("pods_used", C.c_int32),
                 ("gpu_used_milli", C.c_int32 * MAX_GPU), ("tag_count", C.c_int32 * NUM_TAGS),
-                ("reserved", C.c_int32)]
+                ("cpu_model", C.c_int32)]
+
+
+MAX_CPU_MODELS = 8
+
+
+class PowerModel(C.Structure):
+    _fields_ = [("gpu_idle_w", C.c_double * 32), ("gpu_full_w", C.c_double * 32),
+                ("cpu_idle_w", C.c_double * MAX_CPU_MODELS), ("cpu_full_w", C.c_double * MAX_CPU_MODELS),
+                ("cpu_cores", C.c_double * MAX_CPU_MODELS), ("gpu_valid", C.c_uint32),
+                ("gpu_unlabelled", C.c_uint32), ("cpu_valid", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class Pod(C.Structure):
@@ -114,6 +136,9 @@ SIGNATURES = {
     "ksim_engine_set_nodes": (C.c_int, [_VP, C.c_int, _P(Node)]),
     "ksim_engine_set_typical": (C.c_int, [_VP, C.c_int, _P(Typical), C.c_int]),
     "ksim_engine_set_policy": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_uint64]),
+    "ksim_engine_set_power_model": (C.c_int, [_VP, C.c_int, _P(PowerModel)]),
+    "ksim_engine_set_weights": (C.c_int, [_VP, C.c_int, C.c_int32, C.c_int32]),
+    "ksim_trace_power_model": (C.c_int, [_VP, _P(PowerModel)]),
     "ksim_engine_filter_score": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int32, _P(C.c_uint8), _P(C.c_int32),
                                            _P(C.c_int32)]),
     "ksim_engine_reserve": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32, _P(C.c_int32)]),
@@ -254,6 +279,12 @@ class Trace:
                             num=p.gpu_count, mask=p.type_mask, spec=p.gpu_spec.decode()))
         return out
 
+    def power_model(self):
+        """The reference's PWR energy model for this trace's GPU models (const.go:41-124)."""
+        pm = PowerModel()
+        check(lib().ksim_trace_power_model(self.h, C.byref(pm)), "ksim_trace_power_model")
+        return pm
+
     def typical(self, threshold=95, step=1, involve_cpu=True, gpu_res_weight=0.0):
         """GetTypicalPods with the paper's TypicalPodsConfig (generate_config_and_run.py:59-62)."""
         cfg = TypicalCfg(1 if involve_cpu else 0, threshold, step, 0, gpu_res_weight)
@@ -320,8 +351,18 @@ class Engine:
         check(lib().ksim_engine_set_typical(self.h, r, tp, n), "set_typical")
 
     def set_policy(self, r, policy="FGD", gpusel=None, seed=0):
+        """policy: a POLICY key or a generate_run_scripts.py string such as "PWR 500 FGD 500"."""
+        policy, weights = parse_policy(policy)
         gs = gpusel or DEFAULT_GPUSEL[policy]
         check(lib().ksim_engine_set_policy(self.h, r, POLICY[policy], GPUSEL[gs], seed), "set_policy")
+        if weights:
+            self.set_weights(r, *weights)
+
+    def set_weights(self, r, w_pwr, w_fgd):
+        check(lib().ksim_engine_set_weights(self.h, r, w_pwr, w_fgd), "set_weights")
+
+    def set_power_model(self, r, pm):
+        check(lib().ksim_engine_set_power_model(self.h, r, C.byref(pm)), "set_power_model")
 
     # plugin-level entry points
     def filter_score(self, r, pod, step=0):

@@ -409,6 +409,101 @@ void orc_normalize_score(int64_t* s, int n) {
     for (int i = 0; i < n; i++) s[i] = oldRange == 0 ? 0 : ((s[i] - lo) * newRange / oldRange) + 0;
 }
 
+/* ---- PWR (pwr_score.go; energy model resource.go:536-563, const.go:41-124) ---- */
+
+/* const.go:48-55 MapCpuTypeEnergyConsumption: idle / full watts and cores per CPU */
+static const struct { const char* name; double idle, full, ncores; } CPU_ENERGY[] = {
+    {"", 15, 120, 16},
+    {"Intel-Xeon-8269CY", 20, 205, 26},
+    {"Intel-Xeon-8163", 20, 165, 24},
+    {"Intel-Xeon-ES-2682-V4", 15, 120, 16},
+    {"Intel-Xeon-6326", 20, 185, 16},
+    {"Intel-Xeon-8369B", 20, 270, 32},
+};
+/* const.go:62-69 MapGpuTypeEnergyConsumption through const.go:115-124 MapGpuTypeModelEnergy
+ * (G2 uses the A10 profile, G3 the A100 profile) */
+static const struct { const char* name; double idle, full; } GPU_ENERGY[] = {
+    {"T4", 10, 70}, {"A10", 30, 150}, {"P100", 25, 250}, {"V100M16", 30, 300},
+    {"V100M32", 30, 300}, {"A100", 50, 400}, {"G2", 30, 150}, {"G3", 50, 400},
+};
+
+/* resource.go:536-563 GetEnergyConsumptionNode */
+int orc_energy_node(const orc_node_resource* n, double* cpu_power, double* gpu_power) {
+    *cpu_power = 0;
+    *gpu_power = 0;
+    if (n->gpu_type[0] != '\0') {
+        int k = -1;
+        for (int i = 0; i < (int)(sizeof GPU_ENERGY / sizeof GPU_ENERGY[0]); i++)
+            if (strcmp(GPU_ENERGY[i].name, n->gpu_type) == 0) k = i;
+        if (k < 0) return -1;
+        int free_gpus = 0; /* GetFullyFreeGpuNum, resource.go:170-177 */
+        for (int g = 0; g < n->n_gpu_left; g++)
+            if (n->milli_gpu_left[g] == ORC_MILLI) free_gpus++;
+        double num_idle = (double)free_gpus;
+        double num_working = (double)n->gpu_number - num_idle;
+        *gpu_power = (GPU_ENERGY[k].idle * num_idle) + (GPU_ENERGY[k].full * num_working);
+    }
+    int c = -1;
+    for (int i = 0; i < (int)(sizeof CPU_ENERGY / sizeof CPU_ENERGY[0]); i++)
+        if (strcmp(CPU_ENERGY[i].name, n->cpu_type) == 0) c = i;
+    if (c < 0) return -2;
+    double real_cores = ceil((double)n->milli_cpu_capacity / ORC_MILLI / 2);
+    double idle_cores = floor((double)n->milli_cpu_left / ORC_MILLI / 2);
+    double working_cores = real_cores - idle_cores;
+    double ncores = CPU_ENERGY[c].ncores;
+    double num_cpus = ceil(real_cores / ncores);
+    double num_active = ceil(working_cores / ncores);
+    double num_idle_cpus = num_cpus - num_active;
+    *cpu_power = (CPU_ENERGY[c].idle * num_idle_cpus) + (CPU_ENERGY[c].full * num_active);
+    return 0;
+}
+
+/* pwr_score.go:143-212 calculatePWRShareExtendScore */
+int64_t orc_pwr_score(const orc_node_resource* n, const orc_pod_resource* p, int* gpu_mask, int* err) {
+    double oc, og, nc, ng;
+    *gpu_mask = 0;
+    *err = 0;
+    if (orc_energy_node(n, &oc, &og)) { *err = 1; return 0; }
+    double old_energy = oc + og;
+    if (p->gpu_number == 1 && p->milli_gpu < ORC_MILLI) {
+        int64_t score = INT64_MIN;
+        int gid = -1;
+        for (int i = 0; i < n->n_gpu_left; i++) {
+            if (n->milli_gpu_left[i] >= p->milli_gpu) {
+                orc_node_resource c = *n;
+                c.milli_cpu_left -= p->milli_cpu;
+                c.milli_gpu_left[i] -= p->milli_gpu;
+                (void)orc_energy_node(&c, &nc, &ng);
+                int64_t s = (int64_t)(old_energy - (nc + ng));
+                if (gid == -1 || s > score) { /* first fitting GPU, then strictly better */
+                    score = s;
+                    gid = i;
+                }
+            }
+        }
+        *gpu_mask = gid < 0 ? 0 : (1 << gid);
+        return score;
+    }
+    orc_node_resource c;
+    (void)orc_node_sub(n, p, &c); /* error ignored, as in the reference */
+    (void)orc_energy_node(&c, &nc, &ng);
+    int64_t s = (int64_t)(old_energy - (nc + ng));
+    int m = orc_allocate_exclusive_gpu_id(n, p);
+    *gpu_mask = m < 0 ? 0 : m;
+    return s;
+}
+
+/* pwr_score.go:104-141 NormalizeScore: all equal -> 100, else (s - min) * 100 / (max - min) */
+void orc_normalize_score_pwr(int64_t* s, int n) {
+    if (n <= 0) return;
+    int64_t lo = s[0], hi = s[0];
+    for (int i = 0; i < n; i++) {
+        if (s[i] < lo) lo = s[i];
+        if (s[i] > hi) hi = s[i];
+    }
+    for (int i = 0; i < n; i++) s[i] = lo == hi ? 100 : (s[i] - lo) * 100 / (hi - lo);
+}
+
 /* open_gpu_share.go:285-303 allocateGpuIdBasedOnBestFit */
 int orc_alloc_gpu_best_fit(const orc_node_resource* n, const orc_pod_resource* p) {
     if (p->milli_gpu < ORC_MILLI) {
@@ -551,6 +646,7 @@ static void node_res_of(const orc_node_spec* s, const node_dyn* d, orc_node_reso
     r->milli_cpu_capacity = s->cpu_alloc;
     r->gpu_number = s->gpu_count;
     strncpy(r->gpu_type, s->gpu_type, ORC_TYPE_LEN - 1);
+    strncpy(r->cpu_type, s->cpu_type, ORC_TYPE_LEN - 1);
     r->n_gpu_left = s->gpu_count > 0 ? s->gpu_count : 0; /* getGpuMilliLeftListOnNode: nil for non-GPU */
     for (int g = 0; g < r->n_gpu_left && g < 8; g++) r->milli_gpu_left[g] = ORC_MILLI - d->gpu_used[g];
 }
@@ -608,6 +704,7 @@ typedef struct {
     int64_t* raw;
     int32_t* gmask;
     int32_t* err;
+    int64_t* raw2;   /* ORC_POL_PWR_FGD: the FGD score (raw holds the PWR score) */
 } work_t;
 
 static int64_t score_one(const work_t* w, int i, int32_t* gm, int32_t* err) {
@@ -648,6 +745,17 @@ static int64_t score_one(const work_t* w, int i, int32_t* gm, int32_t* err) {
         int tag = pod_tag_of(w->e);
         if (tag == -2) { *err = 1; return 0; }
         return orc_clustering_score(&nr, &pr, tag, w->dyn[i].tag_counts);
+    }
+    case ORC_POL_PWR:
+    case ORC_POL_PWR_FGD: {
+        /* pwr_score.go:87-89: inaccessible -> error */
+        if (!accessible) { *err = 1; return 0; }
+        int m = 0, er = 0;
+        int64_t s = orc_pwr_score(&nr, &pr, &m, &er);
+        if (er) { *err = 1; return 0; }
+        *gm = m;
+        if (w->pol.policy == ORC_POL_PWR_FGD) w->raw2[i] = orc_fgd_score(&nr, &pr, w->tp, w->nt, NULL);
+        return s;
     }
     default:
         return 0; /* Random: handled by the pre-score pick */
@@ -697,6 +805,8 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
     int32_t* err = (int32_t*)calloc((size_t)n_nodes, sizeof(int32_t));
     int* fidx = (int*)calloc((size_t)n_nodes, sizeof(int));
     int64_t* fs = (int64_t*)calloc((size_t)n_nodes, sizeof(int64_t));
+    int64_t* raw2 = (int64_t*)calloc((size_t)n_nodes, sizeof(int64_t));
+    int64_t* fs2 = (int64_t*)calloc((size_t)n_nodes, sizeof(int64_t));
     uint32_t* rank = (uint32_t*)calloc((size_t)n_nodes, sizeof(uint32_t));
     int* order = (int*)calloc((size_t)n_nodes, sizeof(int));
     for (int i = 0; i < n_nodes; i++) order[i] = i;
@@ -739,7 +849,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
             int chunk = (n_nodes + threads - 1) / threads;
             for (int t = 0; t < threads; t++) {
                 w[t] = (work_t){nodes, dyn, tp, nt, pol, e, s, rank, t * chunk,
-                                (t + 1) * chunk < n_nodes ? (t + 1) * chunk : n_nodes, feas, raw, gm, err};
+                                (t + 1) * chunk < n_nodes ? (t + 1) * chunk : n_nodes, feas, raw, gm, err, raw2};
                 if (w[t].lo > w[t].hi) w[t].lo = w[t].hi;
                 if (threads > 1) pthread_create(&th[t], NULL, work_fn, &w[t]);
                 else work_fn(&w[t]);
@@ -760,6 +870,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                 int anyerr = 0;
                 for (int k = 0; k < nf; k++) {
                     fs[k] = raw[fidx[k]];
+                    fs2[k] = raw2[fidx[k]];
                     if (err[fidx[k]]) anyerr = 1;
                 }
                 if (pol.policy == ORC_POL_RANDOM) {
@@ -780,9 +891,17 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                     R->status = 2; /* framework.go:656-667: a Score error aborts the cycle */
                 } else {
                     if (pol.policy == ORC_POL_BESTFIT) orc_normalize_score(fs, nf);
+                    if (pol.policy == ORC_POL_PWR || pol.policy == ORC_POL_PWR_FGD) orc_normalize_score_pwr(fs, nf);
+                    /* framework.go:686-704: range check, then x plugin weight; prioritizeNodes sums the
+                     * plugins (generic_scheduler.go:511-519) */
+                    const int64_t w1 = pol.policy == ORC_POL_PWR_FGD ? pol.w_pwr : 1000;
                     for (int k = 0; k < nf; k++) {
-                        if (fs[k] > 100 || fs[k] < 0) anyerr = 1; /* framework.go:696-700 */
-                        fs[k] *= 1000;                            /* plugin weight (any weight > 0) */
+                        if (fs[k] > 100 || fs[k] < 0) anyerr = 1;
+                        fs[k] *= w1;
+                        if (pol.policy == ORC_POL_PWR_FGD) {
+                            if (fs2[k] > 100 || fs2[k] < 0) anyerr = 1;
+                            fs[k] += fs2[k] * pol.w_fgd;
+                        }
                     }
                     if (anyerr) R->status = 2;
                     else {
@@ -808,6 +927,12 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                         int m = 0;
                         (void)orc_fgd_score(&nr, &pr, tp, nt, &m);
                         mask = m == 0 ? -1 : m;
+                        break;
+                    }
+                    case ORC_SEL_PWR: { /* pwr_score.go:214-219 allocateGpuIdBasedOnPWRScore */
+                        int m = 0, er = 0;
+                        (void)orc_pwr_score(&nr, &pr, &m, &er);
+                        mask = (m == 0 || er) ? -1 : m;
                         break;
                     }
                     case ORC_SEL_WORST: mask = alloc_gpu_worst_fit(&nr, &pr); break;
@@ -885,7 +1010,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                 final_state[i].gpu_left[g] = g < nodes[i].gpu_count ? (int32_t)(ORC_MILLI - dyn[i].gpu_used[g]) : 0;
         }
     }
-    free(dyn); free(feas); free(raw); free(gm); free(err); free(fidx); free(fs); free(rank); free(order);
+    free(dyn); free(feas); free(raw); free(gm); free(err); free(fidx); free(fs); free(rank); free(order); free(raw2); free(fs2);
     return 0;
 }
 

@@ -11,7 +11,8 @@
  * tree; every function in fgd_oracle.c cites the file:line it follows):
  *   pkg/utils/frag.go                       (FGD fragmentation math)
  *   pkg/simulator/plugin/{fgd,...}_score.go         (FGD, BestFit, DotProduct, GpuPacking,
- *                                             GpuClustering, Random)
+ *                                             GpuClustering, Random, PWR)
+ *   pkg/type/open-gpu-share/utils/const.go   (PWR energy model constants)
  *   pkg/simulator/plugin/open_gpu_share.go   (Filter, Reserve, GPU selectors)
  *   pkg/type/resource.go                     (NodeResource/PodResource helpers)
  *   pkg/type/open-gpu-share/cache/gpunodeinfo.go (AllocateGpuId fit test)
@@ -62,6 +63,7 @@ typedef struct {
     int32_t n_gpu_left;                /* len(MilliGpuLeftList) */
     int32_t gpu_number;
     char    gpu_type[ORC_TYPE_LEN];
+    char    cpu_type[ORC_TYPE_LEN];    /* CpuType (alibabacloud.com/cpu-model label; "" when absent) */
 } orc_node_resource;
 
 /* resource.go:14-17 TargetPod */
@@ -105,6 +107,13 @@ int64_t orc_packing_score(const orc_node_resource* n, const orc_pod_resource* p,
 int64_t orc_clustering_score(const orc_node_resource* n, const orc_pod_resource* p, int pod_tag,
                              const int32_t* node_tag_counts);
 void    orc_normalize_score(int64_t* scores, int n);                                     /* plugin_utils.go:48-74 */
+/* resource.go:536-563 GetEnergyConsumptionNode; 0 ok, -1 GPU model without an energy model
+ * (the reference calls a nil func), -2 CPU model unknown (its map lookup yields NaN power) */
+int     orc_energy_node(const orc_node_resource* n, double* cpu_power, double* gpu_power);
+/* pwr_score.go:143-212 calculatePWRShareExtendScore: returns score; *gpu_mask = chosen GPU set;
+ * *err = 1 when orc_energy_node fails */
+int64_t orc_pwr_score(const orc_node_resource* n, const orc_pod_resource* p, int* gpu_mask, int* err);
+void    orc_normalize_score_pwr(int64_t* scores, int n);                                 /* pwr_score.go:104-141 */
 int     orc_alloc_gpu_best_fit(const orc_node_resource* n, const orc_pod_resource* p);   /* mask, -1 none */
 
 /* ---- typical pods (frag.go:285-380) ---- */
@@ -127,8 +136,10 @@ int orc_get_typical_pods(const orc_workload_pod* pods, int n, orc_typical_cfg cf
 
 /* ---- replay driver (scheduleOne semantics) ---- */
 enum { ORC_POL_FGD = 0, ORC_POL_BESTFIT = 1, ORC_POL_DOTPROD = 2, ORC_POL_PACKING = 3,
-       ORC_POL_CLUSTERING = 4, ORC_POL_RANDOM = 5 };
-enum { ORC_SEL_BEST = 0, ORC_SEL_WORST = 1, ORC_SEL_RANDOM = 2, ORC_SEL_FGD = 3 };
+       ORC_POL_CLUSTERING = 4, ORC_POL_RANDOM = 5,
+       ORC_POL_PWR = 6,       /* PWRScore alone */
+       ORC_POL_PWR_FGD = 7 }; /* PWRScore + FGDScore, weights orc_policy.w_pwr / w_fgd */
+enum { ORC_SEL_BEST = 0, ORC_SEL_WORST = 1, ORC_SEL_RANDOM = 2, ORC_SEL_FGD = 3, ORC_SEL_PWR = 4 };
 
 typedef struct {
     char    name[64];              /* full node name, e.g. "0042-openb-node-0001" (tie-break key) */
@@ -137,6 +148,7 @@ typedef struct {
     int32_t pods_alloc;
     int32_t gpu_count;
     char    gpu_type[ORC_TYPE_LEN];
+    char    cpu_type[ORC_TYPE_LEN];    /* alibabacloud.com/cpu-model ("" when absent) */
 } orc_node_spec;
 
 typedef struct {
@@ -171,6 +183,7 @@ typedef struct {
     int32_t gpu_sel;
     uint64_t seed;                 /* Random policy: see DESIGN.md "Random contract" */
     int32_t threads;               /* >1: parallelize.Until-style worker fan-out over nodes */
+    int32_t w_pwr, w_fgd;          /* ORC_POL_PWR_FGD plugin weights (scheduler config score weights) */
 } orc_policy;
 
 /* Replays n events on a fresh cluster.  results[n]; reports[n] may be NULL. */

@@ -12,8 +12,8 @@ _LIB = None
 
 MILLI = 1000
 Q1, Q2, Q3, Q4, XL, XR, NA = range(7)
-POL_FGD, POL_BESTFIT, POL_DOTPROD, POL_PACKING, POL_CLUSTERING, POL_RANDOM = range(6)
-SEL_BEST, SEL_WORST, SEL_RANDOM, SEL_FGD = range(4)
+POL_FGD, POL_BESTFIT, POL_DOTPROD, POL_PACKING, POL_CLUSTERING, POL_RANDOM, POL_PWR, POL_PWR_FGD = range(8)
+SEL_BEST, SEL_WORST, SEL_RANDOM, SEL_FGD, SEL_PWR = range(5)
 TYPE_LEN = 64
 MAX_GPU_LIST = 16
 
@@ -26,7 +26,7 @@ class PodResource(C.Structure):
 class NodeResource(C.Structure):
     _fields_ = [("milli_cpu_left", C.c_int64), ("milli_cpu_capacity", C.c_int64),
                 ("milli_gpu_left", C.c_int64 * MAX_GPU_LIST), ("n_gpu_left", C.c_int32),
-                ("gpu_number", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+                ("gpu_number", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN), ("cpu_type", C.c_char * TYPE_LEN)]
 
 
 class TargetPod(C.Structure):
@@ -45,7 +45,8 @@ class TypicalCfg(C.Structure):
 
 class NodeSpec(C.Structure):
     _fields_ = [("name", C.c_char * 64), ("cpu_alloc", C.c_int64), ("mem_alloc", C.c_int64),
-                ("pods_alloc", C.c_int32), ("gpu_count", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN)]
+                ("pods_alloc", C.c_int32), ("gpu_count", C.c_int32), ("gpu_type", C.c_char * TYPE_LEN),
+                ("cpu_type", C.c_char * TYPE_LEN)]
 
 
 class Event(C.Structure):
@@ -66,7 +67,8 @@ class Report(C.Structure):
 
 
 class Policy(C.Structure):
-    _fields_ = [("policy", C.c_int32), ("gpu_sel", C.c_int32), ("seed", C.c_uint64), ("threads", C.c_int32)]
+    _fields_ = [("policy", C.c_int32), ("gpu_sel", C.c_int32), ("seed", C.c_uint64), ("threads", C.c_int32),
+                ("w_pwr", C.c_int32), ("w_fgd", C.c_int32)]
 
 
 class NodeState(C.Structure):
@@ -116,6 +118,10 @@ def lib():
         L.orc_clustering_score.restype = C.c_int64
         L.orc_normalize_score.argtypes = [P(C.c_int64), C.c_int]
         L.orc_alloc_gpu_best_fit.argtypes = [P(NodeResource), P(PodResource)]
+        L.orc_energy_node.argtypes = [P(NodeResource), P(C.c_double), P(C.c_double)]
+        L.orc_pwr_score.argtypes = [P(NodeResource), P(PodResource), P(C.c_int), P(C.c_int)]
+        L.orc_pwr_score.restype = C.c_int64
+        L.orc_normalize_score_pwr.argtypes = [P(C.c_int64), C.c_int]
         L.orc_get_typical_pods.argtypes = [P(WorkloadPod), C.c_int, TypicalCfg, P(TargetPod), C.c_int]
         L.orc_run_events_state.argtypes = [P(NodeSpec), C.c_int, P(TargetPod), C.c_int, Policy, P(Event),
                                            C.c_int, P(Result), P(Report), P(NodeState)]
@@ -129,7 +135,27 @@ def _b(s):
     return s.encode() if isinstance(s, str) else s
 
 
-def node_res(cpu_left, gpu_left, gpu_number=None, gpu_type="", cpu_cap=0):
+def energy_node(node):
+    """(rc, cpu watts, gpu watts) of GetEnergyConsumptionNode (resource.go:536-563)"""
+    c, g = C.c_double(0), C.c_double(0)
+    rc = lib().orc_energy_node(C.byref(node), C.byref(c), C.byref(g))
+    return rc, c.value, g.value
+
+
+def pwr_score(node, pod):
+    """(score, gpu mask, err) of calculatePWRShareExtendScore (pwr_score.go:143-212)"""
+    m, e = C.c_int(0), C.c_int(0)
+    s = lib().orc_pwr_score(C.byref(node), C.byref(pod), C.byref(m), C.byref(e))
+    return s, m.value, e.value
+
+
+def normalize_pwr(scores):
+    arr = (C.c_int64 * max(1, len(scores)))(*scores)
+    lib().orc_normalize_score_pwr(arr, len(scores))
+    return list(arr[:len(scores)])
+
+
+def node_res(cpu_left, gpu_left, gpu_number=None, gpu_type="", cpu_cap=0, cpu_type=""):
     n = NodeResource()
     n.milli_cpu_left = cpu_left
     n.milli_cpu_capacity = cpu_cap
@@ -138,6 +164,7 @@ def node_res(cpu_left, gpu_left, gpu_number=None, gpu_type="", cpu_cap=0):
     n.n_gpu_left = len(gpu_left)
     n.gpu_number = len(gpu_left) if gpu_number is None else gpu_number
     n.gpu_type = _b(gpu_type)
+    n.cpu_type = _b(cpu_type)
     return n
 
 
@@ -191,7 +218,7 @@ def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_w
 
 
 def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
-               with_report=False):
+               with_report=False, w_pwr=0, w_fgd=0):
     """nodes: list of dicts {name,cpu,mem,pods,gpu,model}; events: list of dicts
     {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]"""
     nn = len(nodes)
@@ -201,6 +228,7 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
         ns[i].cpu_alloc, ns[i].mem_alloc = d["cpu"], d["mem"]
         ns[i].pods_alloc, ns[i].gpu_count = d.get("pods", 1001), d["gpu"]
         ns[i].gpu_type = _b(d.get("model", ""))
+        ns[i].cpu_type = _b(d.get("cpu_model", ""))
     tp, nt = typical(typical_list)
     ne = len(events)
     ev = (Event * max(1, ne))()
@@ -212,7 +240,7 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
     res = (Result * max(1, ne))()
     rep = (Report * max(1, ne))() if with_report else None
     st = (NodeState * nn)()
-    pol = Policy(policy, gpu_sel, seed, threads)
+    pol = Policy(policy, gpu_sel, seed, threads, w_pwr, w_fgd)
     rc = lib().orc_run_events_state(ns, nn, tp, nt, pol, ev, ne, res, rep, st)
     assert rc == 0
     results = [(res[i].node, res[i].gpu_mask, res[i].score, res[i].n_feasible, res[i].status) for i in range(ne)]

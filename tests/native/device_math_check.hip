@@ -168,4 +168,15 @@ int dm_exclusive(const int* gl8, int gpu_cnt, int milli, int num) {
   return exclusive_gpu_mask(mk(0, 0, gl8, gpu_cnt, 0, 1), pod(0, milli, num, ~0u));
 }
 
+// PWR (pwr_score.go:143-212) with a power model given as the ksim_power_model layout
+int dm_pwr_score(int cpu_left, int cap, int cpu_model, const int* gl8, int gpu_cnt, int type_id, int cpu, int milli,
+                 int num, const void* pm, int* gpu_out, int* err_out) {
+  const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, type_id, 1);
+  bool err = false;
+  const int s = pwr_score(n, pod(cpu, milli, num, ~0u), cap, cpu_model, *static_cast<const PowerDev*>(pm), gpu_out, &err);
+  *err_out = err ? 1 : 0;
+  return s;
+}
+int dm_pwr_normalize(int s, int lo, int hi) { return pwr_normalize(s, lo, hi); }
+
 }  // extern "C"

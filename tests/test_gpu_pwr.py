@@ -1,0 +1,128 @@
+"""GPU parity of PWRScore and the weighted PWRScore + FGDScore combinations
+(pkg/simulator/plugin/pwr_score.go; generate_run_scripts.py:31-42 "PWR", "PWR 500 FGD 500", ...).
+
+The engine runs PWR replicas on the per-pod path: k_step (Filter, raw PWR score, FGD candidates)
+then k_step_pwr (NormalizeScore with the cluster's min / max, weighted sum, selectHost, Reserve,
+Bind), one pair per pod in a hipGraph.  Bar: bit-exact against the oracle, event by event, and the
+same final cluster state.  Every test needs a gfx950 device.
+"""
+import pytest
+
+import helpers
+import ksim
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def default_trace():
+    return ksim.Trace.openb("default")
+
+
+def engine_run(trace, replay, keep, n_ev, policy, nodes=None):
+    nodes = helpers.subset_nodes(replay, keep) if keep is not None else replay.nodes
+    nn = len(keep) if keep is not None else trace.num_nodes
+    arr, n = trace.typical()
+    eng = ksim.Engine(nn, 1)
+    eng.set_nodes(0, nodes)
+    eng.set_typical(0, arr, n)
+    eng.set_policy(0, policy)
+    eng.set_power_model(0, trace.power_model())
+    eng.load_events(0, replay.events, n_ev)
+    eng.run()
+    path = eng.last_run_path()
+    res, state = eng.results(0), eng.nodes(0)
+    eng.close()
+    return res, state, path
+
+
+def oracle_run(trace, replay, keep, n_ev, policy, threads=16):
+    name, w = ksim.parse_policy(policy)
+    pol = O.POL_PWR if name == "PWR" else O.POL_PWR_FGD
+    sel = O.SEL_PWR if name == "PWR" else O.SEL_FGD
+    onodes = helpers.oracle_nodes(trace, replay)
+    if keep is not None:
+        onodes = [onodes[i] for i in keep]
+    w_pwr, w_fgd = w if w else (0, 0)
+    return O.run_events(onodes, helpers.oracle_typical(trace), helpers.oracle_events(trace, replay, n_ev),
+                        policy=pol, gpu_sel=sel, threads=threads, w_pwr=w_pwr, w_fgd=w_fgd)
+
+
+def assert_same(res, want, state, want_state):
+    bad = [i for i, (a, b) in enumerate(zip(res, want)) if a != b]
+    assert len(res) == len(want) and not bad, "first mismatch at event %d: gpu %s oracle %s" % (
+        bad[0], res[bad[0]], want[bad[0]])
+    for i, (cpu_left, mem_left, pods, gl) in enumerate(want_state):
+        s = state[i]
+        assert s.cpu_alloc_milli - s.cpu_used_milli == cpu_left and s.pods_used == pods
+        assert [1000 - s.gpu_used_milli[g] if g < s.gpu_count else 0 for g in range(8)] == gl
+
+
+@pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500", "PWR 100 FGD 900", "PWR 50 FGD 950"])
+def test_subset_replay(default_trace, policy):
+    rp = default_trace.replay(seed=42)
+    keep = list(range(3, default_trace.num_nodes, 7))  # 173 nodes, every GPU model
+    n_ev = 1500
+    res, state, path = engine_run(default_trace, rp, keep, n_ev, policy)
+    want, want_state, _ = oracle_run(default_trace, rp, keep, n_ev, policy)
+    assert path == "k_step"
+    assert_same(res, want, state, want_state)
+    assert sum(1 for r in res if r[0] >= 0) > 300 and any(r[4] == 1 for r in res)  # fills up, then fails
+
+
+@pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500"])
+def test_full_trace(default_trace, policy):
+    rp = default_trace.replay(seed=43)
+    res, state, _ = engine_run(default_trace, rp, None, rp.n, policy)
+    want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, policy)
+    assert_same(res, want, state, want_state)
+
+
+def test_plugin_level_score_and_reserve(default_trace):
+    # Score before NormalizeScore and the PWR GPU choice per node (the batch a Go PreScore shim
+    # would store), then Reserve with gpuSelMethod "PWRScore"
+    rp = default_trace.replay(seed=44)
+    keep = list(range(0, default_trace.num_nodes, 11))
+    eng = ksim.Engine(len(keep), 1)
+    eng.set_nodes(0, helpers.subset_nodes(rp, keep))
+    eng.set_policy(0, "PWR")
+    eng.set_power_model(0, default_trace.power_model())
+    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    evs = helpers.oracle_events(default_trace, rp, 200)
+    for k in range(0, 200, 17):
+        feas, score, gpu = eng.filter_score(0, rp.events[k], step=k)
+        e = evs[k]
+        pr = O.pod_res(e["cpu"], e["milli"], e["num"], e["type"])
+        for j, d in enumerate(onodes):
+            if not feas[j]:
+                continue
+            nr = O.node_res(d["cpu"], [1000] * d["gpu"], d["gpu"], d["model"], d["cpu"])
+            s, m, err = O.pwr_score(nr, pr)
+            assert err == 0 and score[j] == s
+            if e["num"] == 1 and e["milli"] < 1000:
+                assert gpu[j] == m
+    # Reserve on node 0 picks the PWR GPU; Unreserve restores the node
+    share = next(k for k, e in enumerate(evs) if e["num"] == 1 and 0 < e["milli"] < 1000)
+    mask = eng.reserve(0, rp.events[share], 0, step=share)
+    assert mask == 1  # fresh node: every GPU costs the same, the first is kept
+    eng.unreserve(0, rp.events[share], 0, mask)
+    assert all(g == 0 for g in eng.nodes(0)[0].gpu_used_milli)
+    eng.close()
+
+
+def test_errors(default_trace):
+    rp = default_trace.replay(seed=42)
+    eng = ksim.Engine(default_trace.num_nodes, 1)
+    eng.set_nodes(0, rp.nodes)
+    eng.set_policy(0, "PWR")
+    eng.load_events(0, rp.events, 10)
+    with pytest.raises(ksim.KsimError) as ei:
+        eng.run()  # no power model yet
+    assert ei.value.code == ksim.KSIM_ESTATE
+    with pytest.raises(ksim.KsimError):
+        eng.set_policy(0, "FGD", gpusel="PWR")  # allocateGpuIdFunc has no PWRScore without the plugin
+    eng.set_policy(0, "PWR 500 FGD 500")
+    with pytest.raises(ksim.KsimError):
+        eng.filter_score(0, rp.events[0])  # two plugins: no single plugin-level Score
+    eng.close()
