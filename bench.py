@@ -85,7 +85,8 @@ def main():
                     help="0 auto (FGD: k_memo), 1 k_step per pod, 2 k_replay only, 3 k_memo required")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | ...")
+    ap.add_argument("--policy", default="FGD", help="FGD (headline) | BestFit | DotProd | GpuPacking | GpuClustering | Random | PWR | "
+                         "'PWR 500 FGD 500' ...")
     ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"],
                     help="c2: openb x 10 seeds per GPU (headline); c4: the paper sweep, 17 traces x 6 policies "
                          "x 10 seeds split over the GPUs; c5: synthetic 100k nodes x 1M pods, one replica per GPU")
@@ -265,6 +266,8 @@ def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_m
         eng.set_nodes(r, rp.nodes)
         eng.set_typical(r, arr, n)
         eng.set_policy(r, policy)
+        if ksim.parse_policy(policy)[0] in ("PWR", "PWR+FGD"):
+            eng.set_power_model(r, trace.power_model())
         eng.load_events(r, rp.events, rp.n)
         total += rp.n
     eng.total_events = total

@@ -27,6 +27,11 @@ TRACES = ["openb_pod_list_cpu050", "openb_pod_list_cpu100", "openb_pod_list_cpu2
 # expected_results' sc_policy directories -> (score plugin, gpuSelMethod) (expected_run_scripts_0511.sh)
 POLICY_DIRS = {"01-Random": "Random", "02-DotProd": "DotProd", "03-GpuClustering": "GpuClustering",
                "04-GpuPacking": "GpuPacking", "05-BestFit": "BestFit", "06-FGD": "FGD"}
+# the fork's power-aware runs (generate_run_scripts.py:31-42; directory = id-policy with '_' for ' ',
+# get_dir_name_from_method :54-63).  No expected_results exist for them.
+PWR_POLICY_DIRS = {"07-PWR": "PWR", "08-PWR_500_FGD_500": "PWR 500 FGD 500",
+                   "11-PWR_100_FGD_900": "PWR 100 FGD 900", "12-PWR_50_FGD_950": "PWR 50 FGD 950"}
+ALL_POLICY_DIRS = {**POLICY_DIRS, **PWR_POLICY_DIRS}
 SEEDS = list(range(42, 52))
 
 
@@ -40,7 +45,9 @@ def shard(items, rank, world):
 
 
 class Sweep:
-    """All experiments of a plan as replicas of one engine on one device."""
+    """All experiments of a plan as replicas on one device: one engine for the persistent-kernel
+    policies (k_memo / k_replay) and, when the plan has PWR experiments, one for those (k_step +
+    k_step_pwr per pod)."""
 
     def __init__(self, experiments, device=0, report=True, wgs=0):
         self.exps = list(experiments)
@@ -50,33 +57,51 @@ class Sweep:
                 traces[t] = ksim.Trace.openb(t[len("openb_pod_list_"):] if t.startswith("openb_pod_list_") else t)
         n_nodes = {tr.num_nodes for tr in traces.values()}
         assert len(n_nodes) == 1, "every trace of a sweep must share the node list"
-        self.eng = ksim.Engine(n_nodes.pop(), len(self.exps), device=device, wgs_per_replica=wgs)
-        if report:
-            self.eng.set_report(True)
+        nn = n_nodes.pop()
         typ = {name: tr.typical() for name, tr in traces.items()}
+        pwr = [i for i, e in enumerate(self.exps) if e[1] in PWR_POLICY_DIRS]
+        rest = [i for i, e in enumerate(self.exps) if e[1] not in PWR_POLICY_DIRS]
+        self.groups = []
         self.total_events = 0
-        for r, (t, p, s, tune) in enumerate(self.exps):
-            rp = traces[t].replay(seed=s, tune_ratio=tune, shuffle=True)
-            self.eng.set_nodes(r, rp.nodes)
-            arr, n = typ[t]
-            self.eng.set_typical(r, arr, n)
-            self.eng.set_policy(r, POLICY_DIRS[p], seed=s)
-            self.eng.load_events(r, rp.events, rp.n)
-            self.total_events += rp.n
+        for idx in (rest, pwr):
+            if not idx:
+                continue
+            eng = ksim.Engine(nn, len(idx), device=device, wgs_per_replica=wgs)
+            if report:
+                eng.set_report(True)
+            for r, i in enumerate(idx):
+                t, p, s, tune = self.exps[i]
+                rp = traces[t].replay(seed=s, tune_ratio=tune, shuffle=True)
+                eng.set_nodes(r, rp.nodes)
+                arr, n = typ[t]
+                eng.set_typical(r, arr, n)
+                eng.set_policy(r, ALL_POLICY_DIRS[p], seed=s)
+                if p in PWR_POLICY_DIRS:
+                    eng.set_power_model(r, traces[t].power_model())
+                eng.load_events(r, rp.events, rp.n)
+                self.total_events += rp.n
+            self.groups.append((eng, idx))
+        self.eng = self.groups[0][0]  # the persistent-kernel engine (bench.py --config c4)
         self.report = report
 
     def run(self):
         t0 = time.perf_counter()
-        dev_ms = self.eng.run()
+        dev_ms = sum(eng.run() for eng, _ in self.groups)
         return dev_ms, time.perf_counter() - t0
 
     def curves(self):
         """{(trace, policy, seed): {"alloc": {arr%: val}, "frag": ..., "frag_ratio": ...}}"""
         assert self.report
-        return {(t, p, s): A.curves_arrays(self.eng.report_arrays(r)) for r, (t, p, s, _) in enumerate(self.exps)}
+        out = {}
+        for eng, idx in self.groups:
+            for r, i in enumerate(idx):
+                t, p, s, _ = self.exps[i]
+                out[(t, p, s)] = A.curves_arrays(eng.report_arrays(r))
+        return out
 
     def close(self):
-        self.eng.close()
+        for eng, _ in self.groups:
+            eng.close()
 
 
 def mean_curve(curves, trace, policy, kind="alloc"):

@@ -36,12 +36,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep"))
     ap.add_argument("--traces", default="all")
+    ap.add_argument("--pwr", action="store_true",
+                    help="also the fork's PWR runs (07-PWR, 08/11/12 PWR+FGD; no expected_results for them)")
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     traces = SW.TRACES if args.traces == "all" else args.traces.split(",")
-    exps = SW.shard(SW.plan(traces=traces), rank, world)
+    policies = tuple(SW.ALL_POLICY_DIRS) if args.pwr else tuple(SW.POLICY_DIRS)
+    exps = SW.shard(SW.plan(traces=traces, policies=policies), rank, world)
     t0 = time.perf_counter()
     sw = SW.Sweep(exps, device=local)
     t_setup = time.perf_counter() - t0

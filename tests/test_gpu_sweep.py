@@ -99,3 +99,23 @@ def test_full_paper_sweep_vs_expected_results():
     for kind in det:
         assert len(det[kind]) == 850
         assert all(not v for v in det[kind].values()), kind
+
+
+def test_sweep_with_pwr_runs():
+    # the fork's PWR experiments (generate_run_scripts.py:31-42) next to FGD in one sweep: two
+    # engines (persistent kernels / per-pod PWR path); FGD stays row-identical to the reference
+    pols = ("06-FGD",) + tuple(SW.PWR_POLICY_DIRS)
+    sw = SW.Sweep(SW.plan(traces=["openb_pod_list_default"], policies=pols, seeds=[42, 43]))
+    assert len(sw.groups) == 2
+    dev_ms, _ = sw.run()
+    curves = sw.curves()
+    sw.close()
+    assert len(curves) == 10
+    for (t, p, s), c in curves.items():
+        assert len(c["alloc"]) == 131 and len(c["frag"]) == 131, (p, s)
+        assert c["alloc"][130] > 85.0, (p, s, c["alloc"][130])
+    for kind, csv in (("alloc", ALLO), ("frag", FRAG)):
+        mm = SW.row_mismatches({k: v for k, v in curves.items() if k[1] == "06-FGD"}, kind, SW.expected_rows(csv))
+        assert len(mm) == 2 and not any(mm.values())
+    print("PWR sweep: %.0f ms device time; alloc at 130%%:" % dev_ms,
+          {(p, s): c["alloc"][130] for (t, p, s), c in sorted(curves.items())})
