@@ -1565,10 +1565,13 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     }
     double cyc = 0, tick = 0;
     for (int b = 0; b < nb; ++b) { cyc += (double)h[(size_t)b * P + 10]; tick += (double)h[(size_t)b * P + 11]; }
-    for (int ph = 12; ph < 14; ++ph) {
+    for (int ph = 12; ph < 20; ++ph) {
       double sum = 0;
       for (int b = 0; b < nb; ++b) sum += (double)h[(size_t)b * P + ph] / 100.0 / std::max(max_ev, 1);
-      std::fprintf(stderr, " %s %.3f;", ph == 12 ? "listwave-A" : "listwave-C", sum / nb);
+      static const char* extra[] = {"listwave-A", "listwave-C", "step-start loads", "owner A per step",
+                                    "owner: own F done", "crit F all done", "keys", "published"};
+      // owner phases: summed over the K workgroups of a replica (one owner per step)
+      std::fprintf(stderr, " %s %.3f;", extra[ph - 12], ph >= 15 ? sum / std::max(nb / pl.K, 1) : sum / nb);
     }
     if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nb / 1e5);
     std::fprintf(stderr, "\n");

@@ -39,7 +39,11 @@ constexpr int kMWaves = kMBlock / 64;
 constexpr int kMaxCw = 64;                 // class slots per workgroup (one wave-0 lane each)
 constexpr int kMaxItems = 1 + 8 * kMaxCw;  // F evaluations per refresh: current + 8 per request
 constexpr int kFoldRows = 6;               // Q1, Q2 (+Q3 frag), Q4, XL, XR, NA
-constexpr int kFoldBuf = kFoldRows * 64;   // doubles per evaluating wave
+// fold-buffer rows 66 doubles apart: lanes 0-5 fold rows 0-5 with ds_read_b128, whose bank is
+// (a/4) % 64; a 64-double (2 x 256 B) stride put all six rows on the same banks (6-way conflict),
+// 66 puts row b on banks 4b..4b+3
+constexpr int kFoldStride = 66;
+constexpr int kFoldBuf = kFoldRows * kFoldStride;  // doubles per evaluating wave
 constexpr int kEvBuf = 128;
 constexpr unsigned kSpinLimit = 1u << 22;
 
@@ -63,7 +67,8 @@ struct MemoArgs {
   unsigned long long* trace; // optional [R*K][trace_steps][2] (KSIM_PROFILE=2): step start, publish / receive
   int trace_steps;
 };
-constexpr int kProfPhases = 16;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C
+constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
+                                 // 14 step-start loads, 15 owner's A, 16-19 owner's A split (wave 0)
 
 struct __align__(16) MemoShared {
   PodDev ev[kEvBuf];
@@ -274,14 +279,14 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
     const double y = fr * (double)(int)frag;  // Q3: frag part to Q2
     const double val = (!is_cpu && acc_ok && cpu_ok && gpu_ok) ? y : x;
 #pragma unroll
-    for (int b = 0; b < kFoldRows; ++b) buf[b * 64 + lane] = row == b ? val : 0.0;
+    for (int b = 0; b < kFoldRows; ++b) buf[b * kFoldStride + lane] = row == b ? val : 0.0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // lane b < 6 folds row b in typical-pod order; columns past the chunk's last typical pod hold
     // +0.0, so the uniform 8-pair batches only ever add exact zeros beyond it
     const int np = (min(64, nt - t0) + 1) >> 1;
     if (lane < kFoldRows) {
-      const double2* rw = reinterpret_cast<const double2*>(buf + lane * 64);
+      const double2* rw = reinterpret_cast<const double2*>(buf + lane * kFoldStride);
       for (int k0 = 0; k0 < np; k0 += 8) {
         double2 v[8];
 #pragma unroll
@@ -460,6 +465,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     const bool own = oc >= 0 && (oc >> 16) == w;
     const int oslot = own ? (oc & 0xff) : -1;
     const int crep = own ? ((oc >> 8) & 0xff) : -1;
+    const unsigned long long t_loaded = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (prof && tid == 0) sh.prof[14] += t_loaded - t_last;  // step start: the event / d loads
 
     // ---- A: the step's own class on d (owner, waves 0-8) | the list of d's other requests (list wave)
     if (d >= 0) {
@@ -477,6 +484,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
                                   s_fold + (size_t)wv * kFoldBuf);
           if (lane == 0) sh.Fc[wv] = F;
         }
+        if (prof && tid == 0) sh.prof[16] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (wv > 0 && lane == 0) {  // hand the candidate's F to wave 0 without a workgroup barrier
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __hip_atomic_fetch_add(&sh.crit_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -528,6 +536,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8)
             __builtin_amdgcn_s_sleep(0);
           sh.crit_done = 0;
+          if (prof) sh.prof[17] += __builtin_amdgcn_s_memrealtime() - t_loaded;
           if (a.trace && step < a.trace_steps)
             a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 3] = __builtin_amdgcn_s_memrealtime();
         }
@@ -546,6 +555,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         const PodDev oq = ksim_replay::uniform_pod(&sh.cls[oslot]);
         fresh = filter_node(dn, oq) ? gk_crit : 0u;
         old_own = s_keys[(size_t)oslot * N + d];
+        if (prof && tid == 0) sh.prof[18] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (a.trace && lane == 0 && step < a.trace_steps)
           a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
       }
@@ -576,6 +586,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
         gput(rp.res + step, out);
         sh.pay = pay;
+        if (prof) sh.prof[19] += __builtin_amdgcn_s_memrealtime() - t_loaded;
       }
       if (d >= 0) {  // every class of the step's score group on d (its own included)
         const int j = lane;
@@ -589,6 +600,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         }
       }
     }
+    if (prof && tid == 0 && own) sh.prof[15] += __builtin_amdgcn_s_memrealtime() - t_loaded;  // owner's A
     mark(1);
     __syncthreads();
     mark(2);
