@@ -1339,7 +1339,7 @@ static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPl
     }
     int nfw = 0;
     if (Cw <= kMaxCw)
-      for (int f : {16, 12, 8, 4})
+      for (int f : {16, 12})  // waves 1..9 need fold buffers on the critical path
         if (memo_lds(e->N, Cw, f) <= 160 * 1024) { nfw = f; break; }
     if (nfw > 0) {
       pl.K = K;
@@ -1565,11 +1565,12 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     }
     double cyc = 0, tick = 0;
     for (int b = 0; b < nb; ++b) { cyc += (double)h[(size_t)b * P + 10]; tick += (double)h[(size_t)b * P + 11]; }
-    for (int ph = 12; ph < 20; ++ph) {
+    for (int ph = 12; ph < 21; ++ph) {
       double sum = 0;
       for (int b = 0; b < nb; ++b) sum += (double)h[(size_t)b * P + ph] / 100.0 / std::max(max_ev, 1);
       static const char* extra[] = {"listwave-A", "listwave-C", "step-start loads", "owner A per step",
-                                    "owner: own F done", "crit F all done", "keys", "published"};
+                                    "owner: prefetch done", "crit F all done", "keys", "result written",
+                                    "granule stored"};
       // owner phases: summed over the K workgroups of a replica (one owner per step)
       std::fprintf(stderr, " %s %.3f;", extra[ph - 12], ph >= 15 ? sum / std::max(nb / pl.K, 1) : sum / nb);
     }

@@ -39,6 +39,7 @@ constexpr int kMWaves = kMBlock / 64;
 constexpr int kMaxCw = 64;                 // class slots per workgroup (one wave-0 lane each)
 constexpr int kMaxItems = 1 + 8 * kMaxCw;  // F evaluations per refresh: current + 8 per request
 constexpr int kFoldRows = 6;               // Q1, Q2 (+Q3 frag), Q4, XL, XR, NA
+constexpr int kCritWaves = 9;              // owner: waves 1..9 evaluate the step's class on d
 // fold-buffer rows 66 doubles apart: lanes 0-5 fold rows 0-5 with ds_read_b128, whose bank is
 // (a/4) % 64; a 64-double (2 x 256 B) stride put all six rows on the same banks (6-way conflict),
 // 66 puts row b on banks 4b..4b+3
@@ -68,7 +69,7 @@ struct MemoArgs {
   int trace_steps;
 };
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
-                                 // 14 step-start loads, 15 owner's A, 16-19 owner's A split (wave 0)
+                                 // 14 step-start loads, 15 owner's A, 16-20 owner's A split (wave 0)
 
 struct __align__(16) MemoShared {
   PodDev ev[kEvBuf];
@@ -92,7 +93,7 @@ struct __align__(16) MemoShared {
   unsigned wtop[kMWaves][2];
   unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
   int nitems;
-  int crit_done;      // owner: critical F evaluations finished (waves 1-8 count up, wave 0 waits)
+  int crit_done;      // owner: critical F evaluations finished (waves 1-9 count up, wave 0 waits)
   int dirty;          // node (rank) changed by the previous event, -1 none
   int stop;
   unsigned pay;       // this step's granule (its owner)
@@ -470,22 +471,25 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
 
     // ---- A: the step's own class on d (owner, waves 0-8) | the list of d's other requests (list wave)
     if (d >= 0) {
-      if (own && wv <= 8) {
+      if (own && wv >= 1 && wv <= kCritWaves) {
+        // wave 1 + c evaluates candidate c of d for the step's class: 0 = d's current state,
+        // 1..8 = the share pod on GPU c-1 (first GPU of its milli-left value), 1 = the Sub state
+        // otherwise.  Nine waves over four SIMDs; wave 0 is left to the owner's bookkeeping.
         const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
+        const int c = wv - 1;
         int code = -1;
-        if (wv == 0) code = 0;
-        else if (is_share_pod(cp)) code = (((dfirst & ge_mask(dn, cp.milli)) >> (wv - 1)) & 1u) ? wv : -1;
-        else if (wv == 1) code = 9;
+        if (c == 0) code = 0;
+        else if (is_share_pod(cp)) code = (((dfirst & ge_mask(dn, cp.milli)) >> (c - 1)) & 1u) ? c : -1;
+        else if (c == 1) code = 9;
         if (code >= 0) {
           int cpuL, total;
           uint32_t gs[4];
           ksim_replay::fgd_candidate(dn, code, cp, &cpuL, gs, &total);
           const double F = wave_F(cpuL, gs, total, 1u << dn.gpu_type(), rp.typed != 0, sh.tp, rp.ncpu, rp.nt, lane,
                                   s_fold + (size_t)wv * kFoldBuf);
-          if (lane == 0) sh.Fc[wv] = F;
+          if (lane == 0) sh.Fc[c] = F;
         }
-        if (prof && tid == 0) sh.prof[16] += __builtin_amdgcn_s_memrealtime() - t_loaded;
-        if (wv > 0 && lane == 0) {  // hand the candidate's F to wave 0 without a workgroup barrier
+        if (lane == 0) {  // hand the candidate's F to wave 0 without a workgroup barrier
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __hip_atomic_fetch_add(&sh.crit_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -528,12 +532,33 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         }
       }
     }
-    // ---- the owner publishes the step's winner (wave 0, as soon as waves 1-8 have their F)
+    // ---- the owner publishes the step's winner (wave 0, as soon as waves 1-9 have their F).
+    // Everything that does not depend on this step's F values -- the precomputed best of the other
+    // nodes (ex) and Reserve's GPU choice on it, the class requests, d's feasibility and old key --
+    // is loaded while waves 1-9 evaluate F; after the wait only d's key, the max and the granule store
+    // remain before the winner is out.
+    unsigned gk_crit = 0u;
     if (own && wv == 0) {
-      unsigned fresh = 0u, old_own = 0u, gk_crit = 0u;
+      const unsigned t2a = sh.t2a, t2b = sh.t2b;
+      const unsigned ex = (d >= 0 && t2a != 0u && key32_rank(t2a) == d) ? t2b : t2a;
+      const int cnt_o = sh.cnt[oslot];
+      unsigned old_own = 0u, fresh = 0u;
+      bool ofeas = false;
+      PodDev cp{};
       if (d >= 0) {
-        if (lane == 0) {  // wait for waves 1-8 (LDS counter; every one of them arrives)
-          while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8)
+        old_own = s_keys[(size_t)oslot * N + d];
+        cp = ksim_replay::uniform_pod(&sh.cls[crep]);
+        ofeas = filter_node(dn, ksim_replay::uniform_pod(&sh.cls[oslot]));
+      }
+      const int mask_ex =
+          ex != 0u ? select_gpus(load_node(&s_nodes[key32_rank(ex)]), p, rp.gpusel, key32_gpu(ex), rp.seed, step) : -1;
+      // Reserve on d: only the FGD / PWR selectors of a share pod depend on the key's GPU
+      const bool d_gpu_from_key = is_share_pod(p) && p.milli > 0 && (rp.gpusel == SEL_FGD || rp.gpusel == SEL_PWR);
+      const int mask_d_pre = d >= 0 && !d_gpu_from_key ? select_gpus(dn, p, rp.gpusel, -1, rp.seed, step) : -1;
+      if (prof && tid == 0) sh.prof[16] += __builtin_amdgcn_s_memrealtime() - t_loaded;
+      if (d >= 0) {
+        if (lane == 0) {  // wait for waves 1-9 (LDS counter; every one of them arrives)
+          while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kCritWaves)
             __builtin_amdgcn_s_sleep(0);
           sh.crit_done = 0;
           if (prof) sh.prof[17] += __builtin_amdgcn_s_memrealtime() - t_loaded;
@@ -542,48 +567,43 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
-        const PodDev cp = ksim_replay::uniform_pod(&sh.cls[crep]);
         const bool cshare = is_share_pod(cp);
         const unsigned fm = cshare ? (dfirst & ge_mask(dn, cp.milli)) : 0u;
         const bool has = lane >= 1 && lane <= 8 && (cshare ? ((fm >> (lane - 1)) & 1u) != 0u : lane == 1);
         int k = 0;
         if (has) k = (int)pack_key32(score_of(sh.Fc[0] - sh.Fc[lane]), d, cshare ? 15 - (lane - 1) : 0);
-        unsigned gk = (unsigned)ksim_replay::wave_max_dpp(k);
+        const unsigned gk = (unsigned)ksim_replay::wave_max_dpp(k);
         const unsigned z = pack_key32(0, d, 0);  // feasible with no fitting GPU
         gk_crit = gk > z ? gk : z;
-        // the step's own class first (the rest of its group after the granule is out)
-        const PodDev oq = ksim_replay::uniform_pod(&sh.cls[oslot]);
-        fresh = filter_node(dn, oq) ? gk_crit : 0u;
-        old_own = s_keys[(size_t)oslot * N + d];
+        fresh = ofeas ? gk_crit : 0u;
         if (prof && tid == 0) sh.prof[18] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (a.trace && lane == 0 && step < a.trace_steps)
           a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
       }
-      const unsigned t2a = sh.t2a, t2b = sh.t2b;
-      const unsigned ex = (d >= 0 && t2a != 0u && key32_rank(t2a) == d) ? t2b : t2a;
       const unsigned W = fresh > ex ? fresh : ex;
-      const int nfeas = sh.cnt[oslot] + (d >= 0 ? (fresh != 0u ? 1 : 0) - (old_own != 0u ? 1 : 0) : 0);
+      const int rk = W != 0u ? key32_rank(W) : -1;
+      // Reserve (open_gpu_share.go:178-205) on the winner: d's record is in registers
+      const int gW = key32_gpu(W);
+      const int mask = W == 0u ? -1 : (W == ex ? mask_ex : (d_gpu_from_key ? (gW < 0 ? -1 : 1 << gW) : mask_d_pre));
+      const unsigned pay = (W != 0u && mask >= 0) ? pack_pay(rk, mask) : 1u;
       if (lane == 0) {
-        ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
-        unsigned pay = 1u;
-        if (W != 0u) {
-          out.status = ST_OK;
-          out.score = result_score(rp, nfeas, key32_score(W), 0, 0);
-          const int rk = key32_rank(W);
-          const int mask = select_gpus(load_node(&s_nodes[rk]), p, rp.gpusel, key32_gpu(W), rp.seed, step);
-          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
-            out.status = ST_ERROR;
-            out.score = 0;
-          } else {
-            out.node = rk;  // name rank; k_memo_finish maps it to the node index
-            out.gpu_mask = mask;
-            pay = pack_pay(rk, mask);
-          }
-        }
         gstore32(win + step, pay);
         asm volatile("" ::: "memory");
+        if (prof) sh.prof[20] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (a.trace && step < a.trace_steps)
           a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        const int nfeas = cnt_o + (d >= 0 ? (fresh != 0u ? 1 : 0) - (old_own != 0u ? 1 : 0) : 0);
+        ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+        if (W != 0u) {
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+          } else {
+            out.status = ST_OK;
+            out.score = result_score(rp, nfeas, key32_score(W), 0, 0);
+            out.node = rk;  // name rank; k_memo_finish maps it to the node index
+            out.gpu_mask = mask;
+          }
+        }
         gput(rp.res + step, out);
         sh.pay = pay;
         if (prof) sh.prof[19] += __builtin_amdgcn_s_memrealtime() - t_loaded;
