@@ -183,7 +183,9 @@ typedef struct {
     int32_t wgs_per_replica;       /* k_replay: workgroups per replica (0 = CUs / replicas, <= 64) */
     int32_t run_mode;              /* ksim_engine_run: 0 = auto (FGD: memoised k_memo when the cluster and its pod
                                       classes fit in LDS, else k_replay), 1 = k_step per pod (hipGraph),
-                                      2 = k_replay only, 3 = k_memo required for FGD (KSIM_ENOTSUP otherwise) */
+                                      2 = k_replay only, 3 = k_memo required for FGD (KSIM_ENOTSUP otherwise),
+                                      4 = k_memo in decider mode (workgroup 0 decides every event from the
+                                      class owners' top lists; KSIM_ENOTSUP if it does not fit) */
     int32_t reserved[3];
 } ksim_config;
 

@@ -1212,6 +1212,9 @@ struct ksim_engine {
   unsigned long long* d_m_wggrp = nullptr;
   unsigned* d_win = nullptr;
   int* d_m_evo = nullptr;
+  int* d_m_evcls = nullptr;     // decider mode: class of each event
+  unsigned* d_topg = nullptr;   // decider mode: top granules
+  size_t m_cap2[2] = {0, 0};
   double* d_th = nullptr;       // FGD score steps (build_score_thresholds), null if unusable
   size_t m_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   struct MemoPlan* mplan = nullptr;  // the FGD replicas' k_memo plan, uploaded before the timed run
@@ -1280,6 +1283,7 @@ static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_repla
 // ---- k_memo planning (memoised FGD replay, ksim_memo.hpp) ----
 struct MemoPlan {
   int K = 0, Cw = 0, nfw = 0, Cmax = 1;
+  bool decider = false;  // workgroup 0 decides, 1..K-1 own the classes
   size_t lds = 0;
   std::vector<PodDev> pod;                  // [Rg][Cmax]
   std::vector<int> owner;                   // [Rg][Cmax]
@@ -1329,11 +1333,19 @@ static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPl
   if (K < 1 || Rg * K > e->cus) return false;
   for (;;) {
     // slots per workgroup: the smallest Cw every replica's classes pack into
-    int Cw = std::max(1, (pl.Cmax + K - 1) / K);
+    int Cw = std::max(1, (pl.Cmax + K - 1 - (pl.decider ? 1 : 0)) / std::max(1, K - (pl.decider ? 1 : 0)));
     std::vector<std::vector<int>> sc(Rg), ow(Rg);
+    const int d0 = pl.decider ? 1 : 0;  // decider mode: classes on workgroups 1..K-1
     for (;;) {
-      bool ok = Cw <= kMaxCw;
-      for (int i = 0; ok && i < Rg; ++i) ok = memo_assign(e->h_cls[reps[i]], K, Cw, sc[i], ow[i]);
+      bool ok = Cw <= kMaxCw && K > d0;
+      for (int i = 0; ok && i < Rg; ++i) {
+        std::vector<int> s1;
+        ok = memo_assign(e->h_cls[reps[i]], K - d0, Cw, s1, ow[i]);
+        if (!ok) break;
+        sc[i].assign((size_t)K * Cw, -1);
+        std::copy(s1.begin(), s1.end(), sc[i].begin() + (size_t)d0 * Cw);
+        for (int& o : ow[i]) o += d0 << 8;
+      }
       if (ok || Cw > kMaxCw) break;
       ++Cw;
     }
@@ -1415,6 +1427,9 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   if (reps.empty()) return KSIM_OK;
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
+  // run_mode 4 (or KSIM_MEMO_DECIDER=1 with run_mode 0): the decider variant of k_memo
+  const char* dv = std::getenv("KSIM_MEMO_DECIDER");
+  pl.decider = e->run_mode == 4 || (e->run_mode == 0 && dv && dv[0] == '1');
   if (!memo_plan(e, reps, pl)) return KSIM_OK;
   const int Rg = (int)reps.size();
   int rc;
@@ -1426,6 +1441,13 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   const int stride = std::max(max_ev, 1);
   if ((rc = ensure_buf(e->d_win, e->m_cap[5], (size_t)Rg * stride))) return rc;
   if ((rc = ensure_buf(e->d_m_evo, e->m_cap[6], (size_t)Rg * stride))) return rc;
+  if ((rc = ensure_buf(e->d_m_evcls, e->m_cap2[0], (size_t)Rg * stride))) return rc;
+  if ((rc = ensure_buf(e->d_topg, e->m_cap2[1], (size_t)Rg * stride * ksim_memo::kTopWords))) return rc;
+  std::vector<int> evcls((size_t)Rg * stride, -1);
+  for (int gi = 0; gi < Rg; ++gi) {
+    const std::vector<int>& ec = e->h_ev_cls[reps[gi]];
+    for (size_t i = 0; i < ec.size(); ++i) evcls[(size_t)gi * stride + i] = ec[i];
+  }
   // owner code of every event: workgroup << 16 | first slot of its score group << 8 | slot; -1 delete
   std::vector<int> evo((size_t)Rg * stride, -1);
   for (int gi = 0; gi < Rg; ++gi) {
@@ -1440,6 +1462,7 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   }
   hipStream_t st = e->stream;
   KSIM_HIP(hipMemcpyAsync(e->d_m_evo, evo.data(), sizeof(int) * evo.size(), hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_m_evcls, evcls.data(), sizeof(int) * evcls.size(), hipMemcpyHostToDevice, st));
   KSIM_HIP(hipMemcpyAsync(e->d_m_pod, pl.pod.data(), sizeof(PodDev) * pl.pod.size(), hipMemcpyHostToDevice, st));
   KSIM_HIP(hipMemcpyAsync(e->d_m_owner, pl.owner.data(), sizeof(int) * pl.owner.size(), hipMemcpyHostToDevice, st));
   KSIM_HIP(hipMemcpyAsync(e->d_m_wgcls, pl.wgcls.data(), sizeof(int) * pl.wgcls.size(), hipMemcpyHostToDevice, st));
@@ -1460,6 +1483,8 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   hipStream_t st = e->stream;
   const int stride = std::max(max_ev, 1);
   KSIM_HIP(hipMemsetAsync(e->d_win, 0, sizeof(unsigned) * (size_t)Rg * stride, st));
+  if (pl.decider)
+    KSIM_HIP(hipMemsetAsync(e->d_topg, 0, sizeof(unsigned) * (size_t)Rg * stride * ksim_memo::kTopWords, st));
   ksim_memo::MemoArgs ma;
   ma.reps = e->d_reps;
   ma.rep_list = e->d_replist + first;
@@ -1481,6 +1506,9 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ma.prof = nullptr;
   ma.trace = nullptr;
   ma.trace_steps = 0;
+  ma.decider = pl.decider ? 1 : 0;
+  ma.ev_cls = e->d_m_evcls;
+  ma.topg = e->d_topg;
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   const bool tracing = pe && pe[0] == '2';
@@ -1497,8 +1525,17 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
     ma.prof = e->d_prof;
   }
-  KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
-  hipLaunchKernelGGL(ksim_memo::k_memo, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma, (const TypDev*)e->d_tp);
+  if (pl.decider) {
+    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)pl.lds));
+    hipLaunchKernelGGL(ksim_memo::k_memo<true>, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
+                       (const TypDev*)e->d_tp);
+  } else {
+    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)pl.lds));
+    hipLaunchKernelGGL(ksim_memo::k_memo<false>, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
+                       (const TypDev*)e->d_tp);
+  }
   KSIM_HIP(hipGetLastError());
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
@@ -1573,6 +1610,15 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
                                     "granule stored"};
       // owner phases: summed over the K workgroups of a replica (one owner per step)
       std::fprintf(stderr, " %s %.3f;", extra[ph - 12], ph >= 15 ? sum / std::max(nb / pl.K, 1) : sum / nb);
+    }
+    if (pl.decider) {  // the deciders' own phases (workgroup 0 of each replica)
+      static const char* dn[] = {"list + top wait", "F", "decide + bind", "end barrier"};
+      std::fprintf(stderr, " | decider:");
+      for (int ph = 20; ph < 24; ++ph) {
+        double sum = 0;
+        for (int b = 0; b < nb; b += pl.K) sum += (double)h[(size_t)b * P + ph] / 100.0 / std::max(max_ev, 1);
+        std::fprintf(stderr, " %s %.3f;", dn[ph - 20], sum / std::max(nb / pl.K, 1));
+      }
     }
     if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nb / 1e5);
     std::fprintf(stderr, "\n");
@@ -1723,7 +1769,8 @@ void ksim_engine_destroy(ksim_engine* e) {
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
-                  e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws};
+                  e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
+                  e->d_m_evcls, e->d_topg};
   for (void* p : bufs) (void)hipFree(p);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -2316,11 +2363,11 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         e->last_groups = (int)groups.size();
         e->last_memo += Rg;
         first += Rg;
-        if (profile) std::fprintf(stderr, "ksim memo: %d replicas, K=%d, Cw=%d, F waves %d, LDS %zu B\n", Rg, pl.K, pl.Cw,
-                                  pl.nfw, pl.lds);
+        if (profile) std::fprintf(stderr, "ksim memo%s: %d replicas, K=%d, Cw=%d, F waves %d, LDS %zu B\n",
+                                  pl.decider ? " (decider)" : "", Rg, pl.K, pl.Cw, pl.nfw, pl.lds);
         continue;
       }
-      if (e->run_mode == 3) return KSIM_ENOTSUP;
+      if (e->run_mode == 3 || e->run_mode == 4) return KSIM_ENOTSUP;
     }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;

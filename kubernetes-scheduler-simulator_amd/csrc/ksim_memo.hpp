@@ -47,6 +47,13 @@ constexpr int kFoldStride = 66;
 constexpr int kFoldBuf = kFoldRows * kFoldStride;  // doubles per evaluating wave
 constexpr int kEvBuf = 128;
 constexpr unsigned kSpinLimit = 1u << 22;
+// Decider mode (MemoArgs::decider): class owners publish, for event s, the top kTopN keys of its
+// class and its feasible count as of kLag events earlier; the decider adds the <= kLag nodes
+// changed since.
+constexpr int kLag = 3;
+constexpr int kTopN = kLag + 1;
+constexpr int kTopWords = 8;  // per event: kTopN keys | 1, (count << 8) | 1 (nonzero once written)
+constexpr int kDItems = kLag * 9;
 
 struct MemoArgs {
   ReplicaDev* reps;
@@ -67,13 +74,17 @@ struct MemoArgs {
   unsigned long long* prof;  // optional [R*K][kProfPhases] (KSIM_PROFILE=1)
   unsigned long long* trace; // optional [R*K][trace_steps][2] (KSIM_PROFILE=2): step start, publish / receive
   int trace_steps;
+  // decider mode: workgroup 0 decides every event, workgroups 1..K-1 own the classes
+  int decider;
+  const int* ev_cls;         // [launch replica][win_stride] class of each event, -1 delete
+  unsigned* topg;            // [launch replica][win_stride][kTopWords] top granules, zeroed before launch
 };
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
                                  // 14 step-start loads, 15 owner's A, 16-20 owner's A split (wave 0)
 
 struct __align__(16) MemoShared {
   PodDev ev[kEvBuf];
-  int evo[kEvBuf + 4];  // owner code of each staged event (+ the next window's first): workgroup << 16 |
+  int evo[kEvBuf + 8];  // owner code of each staged event (+ the next window's first): workgroup << 16 |
                         // first slot of its group << 8 | slot; -1 delete
   PodDev cls[kMaxCw];
   TypDev tp[kMaxTypical];
@@ -91,6 +102,7 @@ struct __align__(16) MemoShared {
   uint8_t item_code[kMaxItems + 7];
   uint8_t item_slot[kMaxItems + 7];
   unsigned wtop[kMWaves][2];
+  unsigned wtop4[kMWaves][kTopN];  // decider mode: per-wave top keys of an upcoming event's class
   unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
   int nitems;
   int crit_done;      // owner: critical F evaluations finished (waves 1-9 count up, wave 0 waits)
@@ -314,6 +326,368 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
 }
 
 // ---------------------------------------------------------------------------
+// Decider mode.  Workgroup 0 of a replica owns no class: it keeps the cluster and, per event,
+// decides the winner itself instead of waiting for a class owner to publish it:
+//   W = max( top kTopN keys of the event's class as its owner saw them after event s-1-kLag, minus
+//            the nodes changed since,  fresh keys of those <= kLag changed nodes )
+// (the snapshot's top list holds the best unchanged node because at most kLag entries are
+// removed), n_feasible = snapshot count - their snapshot feasibility + their current one.  The
+// owners (workgroups 1..K-1) refresh their keys behind it and publish each top list kLag events
+// ahead, so the decider's chain per event is its own F evaluations, no cross-CU hand-off.
+// ---------------------------------------------------------------------------
+constexpr int kRing = 16;  // top lists the prefetch wave may hold ahead of the coordinator
+
+struct __align__(16) DeciderScratch {
+  PodDev cq[kEvBuf];      // class request (Filter + Score) of each staged create event
+  PodDev cp;              // this create event's class request, for the F waves
+  NodeRec xcur[kLag];     // this event's changed nodes: current records
+  NodeRec hprev[kLag], hafter[kLag];  // event t's change (slot t % kLag): record before / after
+  int hnode[kLag];                    // node (rank) event t changed, -1 none
+  double F[kDItems + 1];
+  unsigned ring[kRing][kTopWords];
+  int ring_tag[kRing];    // step + 1 once the slot holds that step's top list
+  int xn, nitems;
+  int cflag;              // create events whose work list is posted (monotonic)
+  int fdone;              // F-wave completions (monotonic)
+  int consumed;           // last step the coordinator finished
+  int finished;
+  uint8_t item_x[kDItems + 5], item_code[kDItems + 5];
+};
+
+__device__ __forceinline__ int lds_load(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Hand-offs between the decider's waves go through LDS only.  A wave's LDS operations execute in
+// issue order, so the data stores before a flag store are seen by a wave that has seen the flag;
+// the release only drains the wave's LDS queue (a workgroup-scope fence would also wait for every
+// outstanding global store -- the previous event's result and granule -- about a microsecond).
+__device__ __forceinline__ void lds_release() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_acquire() { asm volatile("" ::: "memory"); }
+
+// A bounded LDS wait: past the limit the replica stops with a failure (no silent hang).
+__device__ __forceinline__ bool lds_spin(unsigned& spins, int* stop, int* fail) {
+  if (++spins > 4 * kSpinLimit) {
+    __hip_atomic_store(stop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    atomicOr(fail, 1);
+    return false;
+  }
+  __builtin_amdgcn_s_sleep(0);
+  return true;
+}
+__device__ __forceinline__ NodeV sel3(int j, const NodeV& a0, const NodeV& a1, const NodeV& a2) {
+  return j == 0 ? a0 : (j == 1 ? a1 : a2);
+}
+
+// The decider workgroup.  No workgroup barrier inside the event loop: three roles hand work over
+// through LDS counters (release / acquire at workgroup scope), so the prefetch wave can run ahead.
+//   wave 0        coordinator: the changed nodes and their F work list (history kept in
+//                 registers), then the keys, the winner, Reserve, the granule, the result, Bind;
+//   waves 1..nF   F evaluations of the posted work list;
+//   wave 15       prefetch: polls each create event's top list (global memory, published kLag
+//                 events ahead by the class owner) into an LDS ring.
+__device__ void memo_decider(const MemoArgs& a, const ReplicaDev& rp, MemoShared& sh, NodeRec* s_nodes,
+                             DeciderScratch& ds, double* s_fold, int* s_last, int gi, int tid) {
+  const int lane = tid & 63, wv = tid >> 6;
+  const size_t gbase = (size_t)gi * a.win_stride;
+  unsigned* win = a.win + gbase;
+  const int E = rp.n_events;
+  constexpr int kPW = kMWaves - 1;
+  const int nfw = min(a.nfw, kPW);  // waves with a fold buffer, the prefetch wave excluded
+  const int nF = nfw - 1;           // F waves 1 .. nfw-1
+  if (tid == 0) { ds.cflag = 0; ds.fdone = 0; ds.consumed = -1; ds.finished = 0; }
+  for (int i = tid; i < kRing; i += kMBlock) ds.ring_tag[i] = 0;
+  for (int i = tid; i < kLag; i += kMBlock) ds.hnode[i] = -1;
+  __syncthreads();
+  // KSIM_PROFILE=1 (coordinator): prof[20] work list, [21] top-list wait, [22] F wait, [23] decision + bind
+  const bool prof = a.prof != nullptr && tid == 0;
+  unsigned long long tp0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  auto dmark = [&](int ph) {
+    if (prof) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - tp0;
+      tp0 = t;
+    }
+  };
+
+  if (wv == 0) {
+    // ---------------- coordinator
+    const PodDev* cls_pod = a.cls_pod + (size_t)gi * a.Cmax;
+    const bool use_th = a.th != nullptr;
+    auto score_of = [&](double delta) { return use_th ? score_lookup_dev(delta, sh.th) : fgd_score_of_delta(delta); };
+    // the last kLag events' changes, newest first: node (rank, -1 none), record before, record after
+    static_assert(kLag == 3, "the history registers are unrolled for kLag == 3");
+    // (the records before live in the LDS ring ds.hprev, slot = event % kLag)
+    int hn0 = -1, hn1 = -1, hn2 = -1;
+    NodeV ha0{}, ha1{}, ha2{};
+    unsigned hf0 = 0u, hf1 = 0u, hf2 = 0u;  // first_of_class(after, 0), lane-parallel at Bind time
+    int ncreate = 0;
+    for (int step = 0; step < E; ++step) {
+      const int eb = step & (kEvBuf - 1);
+      if (eb == 0) {
+        const int ne = min(kEvBuf, E - step);
+        const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+        for (int i = lane; i < ne * 2; i += 64) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
+        for (int i = lane; i < ne; i += 64) {
+          const int c = gget(a.ev_cls + gbase + step + i);
+          ds.cq[i] = c >= 0 ? gget(cls_pod + c) : PodDev{};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
+      const bool del = (p.flags & kPodDelete) != 0u;
+      int rk = -1;
+      NodeV before{}, after{};
+      if (!del) {
+        const PodDev cp = ksim_replay::uniform_pod(&ds.cq[eb]);
+        const bool share = is_share_pod(cp);
+        // changed nodes X from the register history, oldest change first (the snapshot state of a
+        // node changed twice is the one before its first change; its current state the one after
+        // its last)
+        int xn = 0, x0 = -1, x1 = -1, x2 = -1;
+        bool s0 = false, s1 = false, s2 = false;
+        NodeV c0{}, c1{}, c2{};
+        unsigned f0 = 0u, f1 = 0u, f2 = 0u;
+#define KSIM_XADD(R, PRE, POST, FM)                         \
+        if ((R) >= 0) {                                     \
+          if ((R) == x0) {                                  \
+            c0 = (POST); f0 = (FM);                         \
+          } else if ((R) == x1) {                           \
+            c1 = (POST); f1 = (FM);                         \
+          } else {                                          \
+            const bool f_ = filter_node((PRE), cp);         \
+            if (xn == 0) { x0 = (R); s0 = f_; c0 = (POST); f0 = (FM); } \
+            else if (xn == 1) { x1 = (R); s1 = f_; c1 = (POST); f1 = (FM); } \
+            else { x2 = (R); s2 = f_; c2 = (POST); f2 = (FM); } \
+            ++xn;                                           \
+          }                                                 \
+        }
+        KSIM_XADD(hn2, ksim_replay::uniform_node(&ds.hprev[(step + 0) % kLag]), ha2, hf2)  // event step-3
+        KSIM_XADD(hn1, ksim_replay::uniform_node(&ds.hprev[(step + 1) % kLag]), ha1, hf1)  // event step-2
+        KSIM_XADD(hn0, ksim_replay::uniform_node(&ds.hprev[(step + 2) % kLag]), ha0, hf0)  // event step-1
+#undef KSIM_XADD
+        // F work list: per changed node its current state, then one candidate per GPU value class
+        // (share pod) or the Sub state; written lane-parallel.  first_of_class(c, m) ==
+        // first_of_class(c, 0) & ge_mask(c, m): packed compares instead of 64 scalar ones
+        const unsigned cm0 = xn > 0 && share ? (f0 & ge_mask(c0, cp.milli)) : 0u;
+        const unsigned cm1 = xn > 1 && share ? (f1 & ge_mask(c1, cp.milli)) : 0u;
+        const unsigned cm2 = xn > 2 && share ? (f2 & ge_mask(c2, cp.milli)) : 0u;
+        const int n0 = xn > 0 ? 1 + (share ? __popc(cm0) : 1) : 0;
+        const int n1 = xn > 1 ? 1 + (share ? __popc(cm1) : 1) : 0;
+        const int n2 = xn > 2 ? 1 + (share ? __popc(cm2) : 1) : 0;
+        const int xf1 = n0, xf2 = n0 + n1, nit = n0 + n1 + n2;
+        if (lane < nit) {
+          const int j = lane < xf1 ? 0 : (lane < xf2 ? 1 : 2);
+          const int k = lane - (j == 0 ? 0 : (j == 1 ? xf1 : xf2));
+          unsigned m = j == 0 ? cm0 : (j == 1 ? cm1 : cm2);
+          for (int q = 1; q < k; ++q) m &= m - 1u;
+          ds.item_x[lane] = (uint8_t)j;
+          ds.item_code[lane] = (uint8_t)(k == 0 ? 0 : (share ? 1 + __builtin_ctz(m) : 9));
+        }
+        if (lane < xn) store_node(&ds.xcur[lane], sel3(lane, c0, c1, c2));
+        if (lane == 0) {
+          ds.cp = cp;
+          ds.nitems = nit;
+        }
+        lds_release();
+        ++ncreate;
+        if (lane == 0) lds_store(&ds.cflag, ncreate);
+        dmark(20);
+        // the class owner's top list (the prefetch wave's LDS ring; the words before the tag)
+        const int slot = step % kRing;
+        unsigned rw = 0u, spins = 0;
+        for (;;) {
+          const int tg = lds_load(&ds.ring_tag[slot]);
+          rw = lane <= kTopN ? ds.ring[slot][lane] : 0u;
+          if (tg == step + 1) break;
+          if (lds_load(&sh.stop) || !lds_spin(spins, &sh.stop, a.fail)) break;
+        }
+        dmark(21);
+        // the F values
+        spins = 0;
+        while (lds_load(&ds.fdone) < nF * ncreate) {
+          if (lds_load(&sh.stop) || !lds_spin(spins, &sh.stop, a.fail)) break;
+        }
+        lds_acquire();
+        if (lds_load(&sh.stop)) break;
+        dmark(22);
+        // fresh key of changed node j on lane j (memo_key_scalar's key from the F values)
+        unsigned fresh = 0u;
+        bool fnow = false, fsnap = false;
+        const int xr = lane == 0 ? x0 : (lane == 1 ? x1 : x2);
+        if (lane < xn) {
+          const NodeV cur = sel3(lane, c0, c1, c2);
+          fsnap = lane == 0 ? s0 : (lane == 1 ? s1 : s2);
+          if (filter_node(cur, cp)) {
+            fnow = true;
+            const int nj = lane == 0 ? n0 : (lane == 1 ? n1 : n2);
+            const int xfj = lane == 0 ? 0 : (lane == 1 ? xf1 : xf2);
+            double Fv[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Fv[k] = k < nj ? ds.F[xfj + k] : 0.0;
+            unsigned bk = pack_key32(0, xr, 0);
+            if (share) {
+              unsigned m = lane == 0 ? cm0 : (lane == 1 ? cm1 : cm2);
+#pragma unroll
+              for (int k = 1; k < 9; ++k) {
+                if (m) {
+                  const int g = __builtin_ctz(m);
+                  m &= m - 1u;
+                  const unsigned key = pack_key32(score_of(Fv[0] - Fv[k]), xr, 15 - g);
+                  bk = key > bk ? key : bk;
+                }
+              }
+            } else {
+              const unsigned key = pack_key32(score_of(Fv[0] - Fv[1]), xr, 0);
+              bk = key > bk ? key : bk;
+            }
+            fresh = bk;
+          }
+        }
+        unsigned tk = 0u;
+        if (lane < kTopN) {
+          const unsigned k = rw & ~0xffu;
+          const int kr = key32_rank(k);
+          const bool inx = k != 0u && ((xn > 0 && kr == x0) || (xn > 1 && kr == x1) || (xn > 2 && kr == x2));
+          tk = inx ? 0u : k;
+        }
+        const unsigned W = (unsigned)ksim_replay::wave_max_dpp((int)(fresh > tk ? fresh : tk));
+        const int cnt = (int)((unsigned)__builtin_amdgcn_readlane((int)rw, kTopN) >> 8);
+        const int nfeas = cnt + __popcll(__ballot(fnow)) - __popcll(__ballot(lane < xn && fsnap));
+        if (lane == 0) lds_store(&ds.consumed, step);
+        ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+        unsigned pay = 1u;
+        if (W != 0u) {
+          const int wr = key32_rank(W);
+          const NodeV wn = wr == x0 ? c0 : (wr == x1 ? c1 : (wr == x2 ? c2 : ksim_replay::uniform_node(&s_nodes[wr])));
+          const int mask = select_gpus(wn, p, rp.gpusel, key32_gpu(W), rp.seed, step);
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+          } else {
+            out.status = ST_OK;
+            out.score = result_score(rp, nfeas, key32_score(W), 0, 0);
+            out.node = wr;  // name rank; k_memo_finish maps it to the node index
+            out.gpu_mask = mask;
+            pay = pack_pay(wr, mask);
+            rk = wr;
+            before = wn;
+            after = wn;
+            bind_node(after, p, mask, +1);
+          }
+        }
+        if (lane == 0) {
+          gstore32(win + step, pay);
+          gput(rp.res + step, out);
+        }
+      } else {
+        // simulator.go:416-422 deletePod: undo the creation's Bind (the coordinator wrote its granule)
+        unsigned pay = 0u;
+        PodDev bp = p;
+        if (p.ref >= 0 && p.ref < step) {
+          pay = __builtin_amdgcn_readfirstlane(gload32(win + p.ref));
+          const uint4* q = reinterpret_cast<const uint4*>(rp.ev + p.ref);
+          uint4 u0 = gget(q), u1 = gget(q + 1);
+          uint32_t* o = reinterpret_cast<uint32_t*>(&bp);
+          o[0] = __builtin_amdgcn_readfirstlane(u0.x); o[1] = __builtin_amdgcn_readfirstlane(u0.y);
+          o[2] = __builtin_amdgcn_readfirstlane(u0.z); o[3] = __builtin_amdgcn_readfirstlane(u0.w);
+          o[4] = __builtin_amdgcn_readfirstlane(u1.x); o[5] = __builtin_amdgcn_readfirstlane(u1.y);
+          o[6] = __builtin_amdgcn_readfirstlane(u1.z); o[7] = __builtin_amdgcn_readfirstlane(u1.w);
+        }
+        const int wr = (int)((pay >> 8) & 0xffffu) - 1;
+        const int mask = (int)(pay >> 24);
+        if (wr >= 0) {
+          rk = wr;
+          before = ksim_replay::uniform_node(&s_nodes[wr]);
+          after = before;
+          bind_node(after, bp, mask, -1);
+        }
+        if (lane == 0) gput(rp.res + step, ResultDev{wr, wr >= 0 ? mask : 0, 0, 0, ST_DELETED});
+        if (lane == 0) lds_store(&ds.consumed, step);
+      }
+      if (rk >= 0) {
+        if (lane == 0) store_node(&s_nodes[rk], after);
+        if (rp.snap && lane == 0) {  // cluster report: the state this event left
+          gput_node(rp.snap + step, after);
+          gput(rp.prev + step, s_last[rk]);
+        }
+        if (lane == 0) s_last[rk] = step;
+      }
+      if (rk >= 0 && lane == 0) store_node(&ds.hprev[step % kLag], before);
+      const unsigned fa = rk >= 0 ? first_mask_lanes(after, lane) : 0u;
+      hn2 = hn1; ha2 = ha1; hf2 = hf1;
+      hn1 = hn0; ha1 = ha0; hf1 = hf0;
+      hn0 = rk; ha0 = after; hf0 = fa;
+      dmark(23);
+    }
+    if (lane == 0) lds_store(&ds.finished, 1);
+  } else if (wv == kPW) {
+    // ---------------- prefetch wave: the top list of every create event, in order, kRing ahead
+    int chunk = 0, my_cls = -1;
+    for (int step = 0; step < E; ++step) {
+      if (step == 0 || step - chunk >= 64) {
+        chunk = step;
+        my_cls = step + lane < E ? gget(a.ev_cls + gbase + step + lane) : -1;
+      }
+      if (__builtin_amdgcn_readlane(my_cls, step - chunk) < 0) continue;  // deletes: no top list
+      unsigned cspins = 0;
+      while (lds_load(&ds.consumed) < step - kRing) {
+        if (lds_load(&sh.stop) || lds_load(&ds.finished) || !lds_spin(cspins, &sh.stop, a.fail)) break;
+      }
+      if (lds_load(&sh.stop) || lds_load(&ds.finished)) break;
+      unsigned v = 0u;
+      bool ok = true;
+      if (lane <= kTopN) {
+        const unsigned* tw = a.topg + (gbase + step) * kTopWords;
+        unsigned spins = 0;
+        while ((v = gload32(tw + lane)) == 0u) {
+          if (++spins > kSpinLimit || lds_load(&sh.stop)) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (__ballot(!ok) != 0ull) {
+        if (lane == 0) { lds_store(&sh.stop, 1); atomicOr(a.fail, 1); }
+        break;
+      }
+      const int slot = step % kRing;
+      if (lane <= kTopN) ds.ring[slot][lane] = v;
+      lds_release();
+      if (lane == 0) lds_store(&ds.ring_tag[slot], step + 1);
+    }
+  } else if (wv <= nF) {
+    // ---------------- F waves: the posted work list of each create event
+    int seen = 0;
+    for (;;) {
+      int cf;
+      unsigned spins = 0;
+      while ((cf = lds_load(&ds.cflag)) == seen) {  // (backs off: 14 polling waves would crowd the LDS)
+        if (lds_load(&ds.finished) || lds_load(&sh.stop) || !lds_spin(spins, &sh.stop, a.fail)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (cf == seen) break;
+      seen = cf;
+      lds_acquire();
+      const int nit = __builtin_amdgcn_readfirstlane(ds.nitems);
+      const PodDev cp = ksim_replay::uniform_pod(&ds.cp);
+      for (int it = wv - 1; it < nit; it += nF) {
+        const NodeV cur = ksim_replay::uniform_node(&ds.xcur[ds.item_x[it]]);
+        int cpuL, total;
+        uint32_t gs[4];
+        ksim_replay::fgd_candidate(cur, ds.item_code[it], cp, &cpuL, gs, &total);
+        const double F = wave_F(cpuL, gs, total, 1u << cur.gpu_type(), rp.typed != 0, sh.tp, rp.ncpu, rp.nt, lane,
+                                s_fold + (size_t)wv * kFoldBuf);
+        if (lane == 0) ds.F[it] = F;
+      }
+      lds_release();
+      if (lane == 0) __hip_atomic_fetch_add(&ds.fdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // k_memo.  Dynamic LDS: MemoShared | NodeRec nodes[N] (slot = name rank) | u32 keys[Cw][N] |
 // f64 fold buffers [nfw][6][64] (the initial F of every node at start-up) | i32 last[N] (cluster
 // report: the last event that changed each node).
@@ -326,6 +700,9 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
 //   C  list wave: the listed requests' keys; then (next step's owner) top-2; then wave 0 reads
 //      the step's granule and applies the Bind.
 // ---------------------------------------------------------------------------
+// kDecider: decider mode (MemoArgs::decider), a separate instantiation so that the classic
+// kernel's register allocation does not carry the decider's code.
+template <bool kDecider>
 __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __restrict__ tp_all) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MemoShared& sh = *reinterpret_cast<MemoShared*>(smem);
@@ -340,7 +717,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(MemoShared));
   unsigned* s_keys = reinterpret_cast<unsigned*>(s_nodes + N);
-  double* s_fold = reinterpret_cast<double*>(reinterpret_cast<char*>(s_keys) + (((size_t)Cw * N * 4 + 15) & ~(size_t)15));
+  double* s_fold = reinterpret_cast<double*>(reinterpret_cast<char*>(s_keys) +
+                                             ((std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15));
   int* s_last = reinterpret_cast<int*>(reinterpret_cast<char*>(s_fold) +
                                        std::max((size_t)a.nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15));
   const PodDev* cls_pod = a.cls_pod + (size_t)gi * a.Cmax;
@@ -417,8 +795,48 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   const bool use_th = a.th != nullptr;
   if (use_th)
     for (int i = tid; i < 102; i += kMBlock) sh.th[i] = a.th[i];
-  // the first create event's class
-  {
+  // decider mode: the top kTopN keys of class slot `slot` and its feasible count, published for
+  // event sp (every thread of the workgroup calls it)
+  const size_t gbase = (size_t)gi * a.win_stride;
+  auto publish_top = [&](int slot, int sp) {
+    const unsigned* kr = s_keys + (size_t)slot * N;
+    unsigned k4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k4[q] = tid + q * kMBlock < N ? kr[tid + q * kMBlock] : 0u;
+    unsigned prev = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < kTopN; ++r) {  // keys are distinct (they carry the rank): next smaller each round
+      unsigned c = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c = (k4[q] < prev && k4[q] > c) ? k4[q] : c;
+      const unsigned m = (unsigned)ksim_replay::wave_max_dpp((int)c);
+      if (lane == 0) sh.wtop4[wv][r] = m;
+      prev = m;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const unsigned v = lane < kMWaves * kTopN ? sh.wtop4[lane / kTopN][lane % kTopN] : 0u;
+      unsigned pv = 0xFFFFFFFFu, out = 0u;
+#pragma unroll
+      for (int r = 0; r < kTopN; ++r) {
+        const unsigned m = (unsigned)ksim_replay::wave_max_dpp((int)(v < pv ? v : 0u));
+        out = lane == r ? m : out;
+        pv = m;
+      }
+      unsigned* tw = a.topg + (gbase + sp) * kTopWords;
+      if (lane < kTopN) gstore32(tw + lane, out | 1u);
+      else if (lane == kTopN) gstore32(tw + lane, ((unsigned)sh.cnt[slot] << 8) | 1u);
+    }
+  };
+  if constexpr (kDecider) {
+    // the first kLag events see the initial state
+    for (int sp = 0; sp < kLag && sp < rp.n_events; ++sp) {
+      const int o = evo[sp];
+      __syncthreads();
+      if (o >= 0 && (o >> 16) == w) publish_top(o & 0xff, sp);
+    }
+  } else {
+    // the first create event's class
     int s0 = 0;
     while (s0 < rp.n_events && evo[s0] < 0) ++s0;
     __syncthreads();
@@ -445,13 +863,16 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   bool r_feas = false, r_need = false, r_skip = false;
   int r_base = 0, r_ni = 0;
 
-  for (int step = 0; step < rp.n_events; ++step) {
+  const bool decider = kDecider && w == 0;
+  if constexpr (kDecider)
+    if (decider) memo_decider(a, rp, sh, s_nodes, *reinterpret_cast<DeciderScratch*>(s_keys), s_fold, s_last, gi, tid);
+  for (int step = 0; step < (decider ? 0 : rp.n_events); ++step) {
     const int eb = step & (kEvBuf - 1);
     if (eb == 0) {
       const int ne = min(kEvBuf, rp.n_events - step);
       const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
       for (int i = tid; i < ne * 2; i += kMBlock) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
-      for (int i = tid; i <= ne; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
+      for (int i = tid; i <= ne + kLag; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
       __syncthreads();
     }
     if (a.trace && tid == 0 && step < a.trace_steps)
@@ -463,7 +884,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     const NodeV dn = ksim_replay::uniform_node(&sh.dnode);
     const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
     const bool del = (p.flags & kPodDelete) != 0u;
-    const bool own = oc >= 0 && (oc >> 16) == w;
+    const bool own = !kDecider && oc >= 0 && (oc >> 16) == w;  // decider mode: workgroup 0 decides
     const int oslot = own ? (oc & 0xff) : -1;
     const int crep = own ? ((oc >> 8) & 0xff) : -1;
     const unsigned long long t_loaded = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -670,8 +1091,17 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       if (prof && lane == 0) sh.prof[13] += __builtin_amdgcn_s_memrealtime() - tl0;
     }
     mark(6);
-    // ---- top-2 of the next create event's class (its owner), on keys fresh but for this step's node
-    if (step + 1 < rp.n_events) {
+    // ---- top-2 of the next create event's class (its owner), on keys fresh but for this step's node;
+    // decider mode: the top list of event step + kLag on keys fresh up to event step - 1
+    if constexpr (kDecider) {
+      if (step + kLag < rp.n_events) {
+        const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + kLag]);
+        if (ocn >= 0 && (ocn >> 16) == w) {
+          __syncthreads();
+          publish_top(ocn & 0xff, step + kLag);
+        }
+      }
+    } else if (step + 1 < rp.n_events) {
       const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + 1]);
       if (ocn >= 0 && (ocn >> 16) == w) {
         __syncthreads();
@@ -788,7 +1218,7 @@ __global__ void k_memo_finish(ReplicaDev* reps, const int* rep_list, int N) {
 
 // LDS bytes of k_memo's dynamic region (must match the carving in the kernel).
 inline size_t memo_lds(int N, int Cw, int nfw) {
-  const size_t keys = ((size_t)Cw * N * 4 + 15) & ~(size_t)15;
+  const size_t keys = (std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15;
   const size_t fold = std::max((size_t)nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15);
   return sizeof(MemoShared) + (size_t)N * sizeof(NodeRec) + keys + fold + (size_t)N * 4;
 }

@@ -2,7 +2,8 @@
 scanning replay (k_replay, run_mode 2).
 
 k_memo keeps the key of every (pod class, node) pair and recomputes only the node the previous
-event changed; the bar is the same as every other path: bit-exact (node, GPU set, score, feasible
+event changed; in decider mode (run_mode 4) workgroup 0 decides every event from the class owners'
+top lists, kLag events old, plus the fresh keys of the nodes changed since; the bar is the same as every other path: bit-exact (node, GPU set, score, feasible
 count, status) per event and the same final cluster state.  Every test needs a gfx950 device.
 """
 import pytest
@@ -14,7 +15,8 @@ from test_gpu_parity import assert_same, engine_run, oracle_run
 
 pytestmark = pytest.mark.gpu
 
-MEMO, SCAN = 3, 2
+MEMO, SCAN, DECIDER = 3, 2, 4
+MODES = pytest.mark.parametrize("mode", [MEMO, DECIDER], ids=["memo", "decider"])
 
 
 @pytest.fixture(scope="module")
@@ -22,43 +24,47 @@ def default_trace():
     return ksim.Trace.openb("default")
 
 
-def test_memo_full_openb_fgd(default_trace):
+@MODES
+def test_memo_full_openb_fgd(default_trace, mode):
     # C2 at one seed: 10 953 events on 1213 nodes, memo == oracle == k_replay
     rp = default_trace.replay(seed=42)
-    res, state = engine_run(default_trace, rp, None, rp.n, "FGD", run_mode=MEMO)
+    res, state = engine_run(default_trace, rp, None, rp.n, "FGD", run_mode=mode)
     want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, O.POL_FGD, O.SEL_FGD)
     assert_same(res, want, state, want_state, None)
     scan, _ = engine_run(default_trace, rp, None, rp.n, "FGD", run_mode=SCAN)
     assert res == scan
 
 
+@MODES
 @pytest.mark.parametrize("wgs", [3, 4, 8, 25, 64])
-def test_memo_workgroups_invariance(default_trace, wgs):
+def test_memo_workgroups_invariance(default_trace, wgs, mode):
     # any number of class-owning workgroups per replica gives the same decisions
     rp = default_trace.replay(seed=6)
     keep = list(range(0, default_trace.num_nodes, 3))
-    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", run_mode=MEMO, wgs=wgs)
+    res, state = engine_run(default_trace, rp, keep, 1500, "FGD", run_mode=mode, wgs=wgs)
     want, want_state, _ = oracle_run(default_trace, rp, keep, 1500, O.POL_FGD, O.SEL_FGD)
     assert_same(res, want, state, want_state, keep)
 
 
+@MODES
 @pytest.mark.parametrize("trace_name", ["gpuspec33", "multigpu50", "gpushare100", "cpu250"])
-def test_memo_other_traces(trace_name):
+def test_memo_other_traces(trace_name, mode):
     # gpuspec33: 457 pod classes and typed typical pods (the NA bin)
     t = ksim.Trace.openb(trace_name)
     rp = t.replay(seed=43)
     keep = list(range(1, t.num_nodes, 3))
     n_ev = min(rp.n, 2500)
-    res, state = engine_run(t, rp, keep, n_ev, "FGD", run_mode=MEMO)
+    res, state = engine_run(t, rp, keep, n_ev, "FGD", run_mode=mode)
     want, want_state, _ = oracle_run(t, rp, keep, n_ev, O.POL_FGD, O.SEL_FGD)
     assert_same(res, want, state, want_state, keep)
 
 
-def test_memo_ten_replicas_ragged(default_trace):
+@pytest.mark.parametrize("memo_mode", [MEMO, DECIDER], ids=["memo", "decider"])
+def test_memo_ten_replicas_ragged(default_trace, memo_mode):
     # the C2 layout (10 seeds, one engine) with ragged stream lengths: memo == k_replay
     arr, n = default_trace.typical()
     outs = {}
-    for mode in (MEMO, SCAN):
+    for mode in (memo_mode, SCAN):
         eng = ksim.Engine(default_trace.num_nodes, 10, run_mode=mode)
         for r in range(10):
             rp = default_trace.replay(seed=42 + r)
@@ -68,11 +74,11 @@ def test_memo_ten_replicas_ragged(default_trace):
             eng.load_events(r, rp.events, rp.n - 97 * r)
         eng.run()
         outs[mode] = [eng.results(r) for r in range(10)]
-        if mode == MEMO:
-            assert eng.last_run_wgs() >= 8
+        if mode == memo_mode:
+            assert eng.last_run_wgs() >= 8 and eng.last_run_path() == "k_memo"
         eng.close()
     for r in range(10):
-        assert outs[MEMO][r] == outs[SCAN][r], "replica %d" % r
+        assert outs[memo_mode][r] == outs[SCAN][r], "replica %d" % r
 
 
 def test_memo_mixed_policies(default_trace):
@@ -97,12 +103,13 @@ def test_memo_mixed_policies(default_trace):
     eng.close()
 
 
-def test_memo_deletions(default_trace):
+@MODES
+def test_memo_deletions(default_trace, mode):
     rp = default_trace.replay(seed=9)
     keep = list(range(0, default_trace.num_nodes, 9))
     evs, oev = helpers.delete_stream(default_trace, rp, 900, 0.3, seed=0)
     arr, n = default_trace.typical()
-    eng = ksim.Engine(len(keep), 1, run_mode=MEMO, wgs_per_replica=6)
+    eng = ksim.Engine(len(keep), 1, run_mode=mode, wgs_per_replica=6)
     eng.set_nodes(0, helpers.subset_nodes(rp, keep))
     eng.set_typical(0, arr, n)
     eng.set_policy(0, "FGD")
@@ -117,21 +124,23 @@ def test_memo_deletions(default_trace):
     eng.close()
 
 
-def test_memo_tiny_cluster(default_trace):
+@MODES
+def test_memo_tiny_cluster(default_trace, mode):
     # 3 nodes, more workgroups than classes and nodes; the cluster fills up and pods fail
     rp = default_trace.replay(seed=3)
     keep = [5, 600, 1100]
-    res, state = engine_run(default_trace, rp, keep, 400, "FGD", run_mode=MEMO, wgs=16)
+    res, state = engine_run(default_trace, rp, keep, 400, "FGD", run_mode=mode, wgs=16)
     want, want_state, _ = oracle_run(default_trace, rp, keep, 400, O.POL_FGD, O.SEL_FGD)
     assert_same(res, want, state, want_state, keep)
     assert any(r[4] == ksim.UNSCHEDULABLE for r in res)
 
 
-def test_memo_rerun_same_results(default_trace):
+@MODES
+def test_memo_rerun_same_results(default_trace, mode):
     # run() restarts from the set_nodes state: two runs of one engine agree
     rp = default_trace.replay(seed=44)
     arr, n = default_trace.typical()
-    eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=MEMO)
+    eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=mode)
     eng.set_nodes(0, rp.nodes)
     eng.set_typical(0, arr, n)
     eng.set_policy(0, "FGD")
