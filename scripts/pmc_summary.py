@@ -20,7 +20,7 @@ def rows(pattern):
 
 def main(d):
     def kernel_of(name):  # demangled or mangled names
-        if "k_memo(" in name or "k_memoENS" in name:
+        if "k_memo(" in name or "k_memoENS" in name or "k_memo<" in name or "k_memoILb" in name:
             return "k_memo"
         return "k_replay" if "k_replay" in name else name
 
