@@ -1007,7 +1007,9 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
       int gc = 0, ge = 0, gl = 0, gh = 0;
       if (pend) {
         W = exchange(pg, &gc, &ge, &gl, &gh, &ok);
-        owner = W != 0ull && W == p_key;
+        // b's post-Bind version only if the pending step binds: a Score error (framework.go:650-656,
+        // e.g. BestFit's -1 on a node with less CPU left than the non-zero request) aborts the cycle
+        owner = W != 0ull && W == p_key && !(gc > 1 && ge);
       }
       mark(5);
       // add b back: post-Bind if this workgroup owned the pending winner, else as it was

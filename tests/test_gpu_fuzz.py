@@ -1,0 +1,93 @@
+"""Parity fuzz on adversarial synthetic clusters (tests/fuzz_cases.py): every policy through every
+execution path -- auto (k_memo for FGD, k_replay for the rest), k_replay forced, k_step per pod
+(hipGraph), k_memo forced for FGD -- bit-exact against the oracle per event (node, GPU set, score,
+feasible count, status) and in the final cluster state.  Every test needs a gfx950 device.
+"""
+import pytest
+
+import ksim
+import pyoracle as O
+from fuzz_cases import make_case
+from test_gpu_parity import POLICIES
+
+pytestmark = pytest.mark.gpu
+
+# (seed, nodes, creations, delete probability)
+CASES = [(1, 40, 500, 0.0), (2, 97, 900, 0.25), (3, 250, 1200, 0.1), (4, 7, 300, 0.4), (5, 1, 60, 0.3),
+         (6, 600, 2000, 0.0)]
+PATHS = [(0, "auto"), (2, "replay"), (1, "step")]
+
+
+def run_engine(case, policy, run_mode, seed=5, wgs=0):
+    nn = len(case["onodes"])
+    eng = ksim.Engine(nn, 1, run_mode=run_mode, wgs_per_replica=wgs)
+    try:
+        eng.set_nodes(0, case["nodes"])
+        eng.set_typical(0, case["typical"], case["typical_n"])
+        eng.set_policy(0, policy, seed=seed)
+        eng.load_events(0, case["events"], case["n_events"])
+        eng.run()
+        return eng.results(0), eng.nodes(0)
+    finally:
+        eng.close()
+
+
+def check_state(state, want_state):
+    for i, (cpu_left, mem_left, pods, gl) in enumerate(want_state):
+        s = state[i]
+        assert (s.cpu_alloc_milli - s.cpu_used_milli, s.mem_alloc_mib - s.mem_used_mib, s.pods_used) == \
+            (cpu_left, mem_left, pods), "node %d" % i
+        assert [1000 - s.gpu_used_milli[g] if g < s.gpu_count else 0 for g in range(8)] == gl, "node %d" % i
+
+
+@pytest.fixture(scope="module", params=CASES, ids=["s%d-n%d-e%d-d%g" % c for c in CASES])
+def case(request):
+    seed, n, e, pdel = request.param
+    return make_case(seed, n, e, pdel)
+
+
+@pytest.mark.parametrize("name,pol,sel", POLICIES, ids=[p[0] for p in POLICIES])
+def test_fuzz_all_paths_vs_oracle(case, name, pol, sel):
+    want, want_state, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=pol, gpu_sel=sel,
+                                       seed=5, threads=16)
+    for mode, label in PATHS:
+        got, state = run_engine(case, name, mode)
+        bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+        assert len(got) == len(want) and not bad, \
+            "%s/%s: first mismatch at event %d: gpu %s oracle %s" % (name, label, bad[0], got[bad[0]], want[bad[0]])
+        check_state(state, want_state)
+
+
+def test_fuzz_memo_forced_fgd(case):
+    # k_memo (run_mode 3) where its classes fit in LDS; it refuses loudly otherwise
+    want, want_state, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=O.POL_FGD,
+                                       gpu_sel=O.SEL_FGD, threads=16)
+    try:
+        got, state = run_engine(case, "FGD", 3)
+    except ksim.KsimError:
+        pytest.skip("k_memo does not fit this case")
+    assert got == want
+    check_state(state, want_state)
+
+
+def test_fuzz_empty_event_stream():
+    case = make_case(7, 30, 0)
+    for mode, _ in PATHS:
+        got, state = run_engine(case, "FGD", mode)
+        assert got == []
+        assert all(state[i].cpu_used_milli == 0 and state[i].pods_used == 0 for i in range(30))
+
+
+def test_typical_table_over_engine_limit_is_loud():
+    # the target-workload table lives in LDS, at most 256 entries (the reference traces: <= 127)
+    tp = (ksim.Typical * 257)()
+    for i in range(257):
+        tp[i].cpu_milli, tp[i].gpu_milli, tp[i].gpu_count = 1000 + i, 100, 1
+        tp[i].type_mask, tp[i].freq = ksim.KSIM_TYPE_ANY, 1.0 / 257
+    eng = ksim.Engine(4, 1)
+    try:
+        with pytest.raises(ksim.KsimError):
+            eng.set_typical(0, tp, 257)
+        eng.set_typical(0, tp, 256)
+    finally:
+        eng.close()
