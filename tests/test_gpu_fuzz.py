@@ -91,3 +91,73 @@ def test_typical_table_over_engine_limit_is_loud():
         eng.set_typical(0, tp, 256)
     finally:
         eng.close()
+
+
+REPORT_KEYS = ["used_nodes", "used_gpus", "used_gpu_milli", "total_gpus", "arrived_gpu_milli", "used_cpu_milli",
+               "arrived_cpu_milli"]
+
+
+@pytest.mark.parametrize("name,pol,sel", POLICIES[:2] + POLICIES[4:5], ids=["FGD", "BestFit", "GpuClustering"])
+def test_fuzz_cluster_report(case, name, pol, sel):
+    # the per-event cluster report (analysis.go:59-119) on every path: the oracle's exact sums
+    want_res, _, want = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=pol, gpu_sel=sel,
+                                     seed=5, threads=16, with_report=True)
+    for mode, label in PATHS:
+        eng = ksim.Engine(len(case["onodes"]), 1, run_mode=mode)
+        try:
+            eng.set_nodes(0, case["nodes"])
+            eng.set_typical(0, case["typical"], case["typical_n"])
+            eng.set_policy(0, name, seed=5)
+            eng.set_report(True)
+            eng.load_events(0, case["events"], case["n_events"])
+            eng.run()
+            assert eng.results(0) == want_res, label
+            got = eng.reports(0)
+        finally:
+            eng.close()
+        assert len(got) == len(want)
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert g["frag_bins"] == w["frag_bins_exact"], (label, i)
+            assert [g[k] for k in REPORT_KEYS] == [w[k] for k in REPORT_KEYS], (label, i)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+@pytest.mark.parametrize("name,pol,sel", POLICIES, ids=[p[0] for p in POLICIES])
+def test_fuzz_node_sharded_group(case, world, name, pol, sel):
+    # one cluster split over `world` shard engines (in-process group, the multi-GPU exchange's protocol)
+    import ksim.shard as SH
+    n = len(case["onodes"])
+    if n < world:
+        pytest.skip("fewer nodes than shards")
+    want, _, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=pol, gpu_sel=sel, seed=5,
+                              threads=16)
+    g = SH.ShardGroup(case["nodes"], (case["typical"], case["typical_n"]), world, policy=name, seed=5)
+    try:
+        g.load_events(case["events"], case["n_events"])
+        g.run()
+        got = g.results()
+    finally:
+        g.close()
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert len(got) == len(want) and not bad, "first mismatch at %d: %s vs %s" % (bad[0], got[bad[0]], want[bad[0]])
+
+
+def test_fuzz_multi_replica_mixed_policies():
+    # six replicas of one node set, one per policy, ragged event streams from different seeds, one run
+    cases = [make_case(20 + r, 150, 300 + 150 * r, 0.2) for r in range(len(POLICIES))]
+    eng = ksim.Engine(150, len(POLICIES))
+    try:
+        for r, (name, _, _) in enumerate(POLICIES):
+            eng.set_nodes(r, cases[r]["nodes"])
+            eng.set_typical(r, cases[r]["typical"], cases[r]["typical_n"])
+            eng.set_policy(r, name, seed=5)
+            eng.load_events(r, cases[r]["events"], cases[r]["n_events"])
+        eng.run()
+        for r, (name, pol, sel) in enumerate(POLICIES):
+            c = cases[r]
+            want, want_state, _ = O.run_events(c["onodes"], c["otypical"], c["oevents"], policy=pol, gpu_sel=sel,
+                                               seed=5, threads=16)
+            assert eng.results(r) == want, name
+            check_state(eng.nodes(r), want_state)
+    finally:
+        eng.close()
