@@ -19,18 +19,23 @@ UNKNOWN = "H100"  # a model no node has: its bit never matches
 VOCAB = MODELS + [UNKNOWN]
 
 
-def _mask(spec):
+def _mask(spec, vocab=VOCAB):
     if not spec:
         return ksim.KSIM_TYPE_ANY
     m = 0
     for s in spec.split("|"):
-        m |= 1 << VOCAB.index(s)
+        m |= 1 << vocab.index(s)
     return m
 
 
-def make_case(seed, n_nodes, n_create, p_delete=0.0):
-    """-> dict(nodes, events, n_events, typical, typical_n, onodes, oevents, otypical)"""
+def make_case(seed, n_nodes, n_create, p_delete=0.0, models=None):
+    """-> dict(nodes, events, n_events, typical, typical_n, onodes, oevents, otypical)
+    models: the GPU model vocabulary (model id = index; default MODELS), e.g. a trace's type_names()
+    so that its PWR power model applies."""
     import pyoracle as O
+
+    MODELS_ = list(models) if models is not None else MODELS
+    VOCAB_ = MODELS_ + [UNKNOWN]
 
     rnd = np.random.default_rng(seed)
     # node names: "%04d-" + name from a permutation (simulator.go:584-588); rank = byte order
@@ -44,14 +49,14 @@ def make_case(seed, n_nodes, n_create, p_delete=0.0):
     onodes = []
     for i in range(n_nodes):
         gpu = int(rnd.choice([0, 1, 2, 3, 4, 5, 6, 7, 8], p=[.12, .1, .15, .05, .15, .03, .05, .05, .3]))
-        model = int(rnd.integers(len(MODELS))) if gpu > 0 else 0
+        model = int(rnd.integers(len(MODELS_))) if gpu > 0 else 0
         cpu = int(rnd.choice([2000, 8000, 32000, 64000, 96000, 128000]))
         mem = int(rnd.choice([4096, 16384, 65536, 262144, 786432]))
         pods = int(rnd.choice([1, 2, 3, 8, 110], p=[.05, .1, .1, .25, .5]))
         n = nodes[i]
         n.cpu_alloc_milli, n.mem_alloc_mib, n.pods_alloc = cpu, mem, pods
         n.gpu_count, n.gpu_type, n.name_rank = gpu, model, rank[i]
-        onodes.append(dict(name=names[i], cpu=cpu, mem=mem, pods=pods, gpu=gpu, model=MODELS[model] if gpu else ""))
+        onodes.append(dict(name=names[i], cpu=cpu, mem=mem, pods=pods, gpu=gpu, model=MODELS_[model] if gpu else ""))
     creates = []
     for _ in range(n_create):
         kind = rnd.choice(["cpu", "share", "whole"], p=[.2, .45, .35])
@@ -68,13 +73,13 @@ def make_case(seed, n_nodes, n_create, p_delete=0.0):
         spec = ""
         if num > 0 and rnd.random() < 0.2:
             k = int(rnd.integers(1, 3))
-            spec = "|".join(rnd.choice(VOCAB, size=k, replace=False))
+            spec = "|".join(rnd.choice(VOCAB_, size=k, replace=False))
         creates.append((cpu, mem, milli, num, spec))
     # event stream: creations, each followed with probability p_delete by the deletion of a random
     # live earlier creation
     evs, oev, live = [], [], []
     for cpu, mem, milli, num, spec in creates:
-        e = ksim.make_pod(cpu, milli, num, mem, _mask(spec), cpu_nz=cpu if cpu > 0 else 100)
+        e = ksim.make_pod(cpu, milli, num, mem, _mask(spec, VOCAB_), cpu_nz=cpu if cpu > 0 else 100)
         evs.append(e)
         oev.append(dict(cpu=cpu, cpu_nz=cpu if cpu > 0 else 100, mem=mem, milli=milli, num=num, type=spec))
         live.append(len(evs) - 1)
@@ -93,6 +98,6 @@ def make_case(seed, n_nodes, n_create, p_delete=0.0):
     typ = (ksim.Typical * max(1, len(otyp)))()
     for i, (cpu, milli, num, spec, freq) in enumerate(otyp):
         typ[i].cpu_milli, typ[i].gpu_milli, typ[i].gpu_count = cpu, milli, num
-        typ[i].type_mask, typ[i].freq = _mask(spec), freq
+        typ[i].type_mask, typ[i].freq = _mask(spec, VOCAB_), freq
     return dict(nodes=nodes, events=(ksim.Pod * max(1, len(evs)))(*evs), n_events=len(evs), typical=typ,
                 typical_n=len(otyp), onodes=onodes, oevents=oev, otypical=otyp)

@@ -161,3 +161,31 @@ def test_fuzz_multi_replica_mixed_policies():
             check_state(eng.nodes(r), want_state)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500", "PWR 100 FGD 900"])
+@pytest.mark.parametrize("seed,n,e,pdel", [(31, 60, 700, 0.2), (32, 300, 1200, 0.0)])
+def test_fuzz_pwr(policy, seed, n, e, pdel):
+    # PWRScore and the weighted PWR + FGD sums (k_step + k_step_pwr), on the openb model vocabulary
+    # so that the reference's energy tables (const.go:41-124) apply
+    t = ksim.Trace.openb("default")
+    c = make_case(seed, n, e, pdel, models=t.type_names())
+    name, w = ksim.parse_policy(policy)
+    pol, sel = (O.POL_PWR, O.SEL_PWR) if name == "PWR" and not w else (O.POL_PWR_FGD, O.SEL_FGD)
+    w_pwr, w_fgd = w if w else (0, 0)
+    want, want_state, _ = O.run_events(c["onodes"], c["otypical"], c["oevents"], policy=pol, gpu_sel=sel,
+                                       threads=16, w_pwr=w_pwr, w_fgd=w_fgd)
+    eng = ksim.Engine(n, 1)
+    try:
+        eng.set_nodes(0, c["nodes"])
+        eng.set_typical(0, c["typical"], c["typical_n"])
+        eng.set_policy(0, policy)
+        eng.set_power_model(0, t.power_model())
+        eng.load_events(0, c["events"], c["n_events"])
+        eng.run()
+        got, state = eng.results(0), eng.nodes(0)
+    finally:
+        eng.close()
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert len(got) == len(want) and not bad, "first mismatch at %d: %s vs %s" % (bad[0], got[bad[0]], want[bad[0]])
+    check_state(state, want_state)
