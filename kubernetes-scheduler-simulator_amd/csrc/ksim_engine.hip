@@ -1528,14 +1528,19 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     ma.prof = e->d_prof;
   }
   if (pl.decider) {
-    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)pl.lds));
-    hipLaunchKernelGGL(ksim_memo::k_memo<true>, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
+    hipLaunchKernelGGL((ksim_memo::k_memo<true, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
+                       (const TypDev*)e->d_tp);
+  } else if (profile || tracing) {
+    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)pl.lds));
+    hipLaunchKernelGGL((ksim_memo::k_memo<false, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
                        (const TypDev*)e->d_tp);
   } else {
-    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)pl.lds));
-    hipLaunchKernelGGL(ksim_memo::k_memo<false>, dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
+    hipLaunchKernelGGL((ksim_memo::k_memo<false, false>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
                        (const TypDev*)e->d_tp);
   }
   KSIM_HIP(hipGetLastError());

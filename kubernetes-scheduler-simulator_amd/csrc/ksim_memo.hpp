@@ -702,7 +702,9 @@ __device__ void memo_decider(const MemoArgs& a, const ReplicaDev& rp, MemoShared
 // ---------------------------------------------------------------------------
 // kDecider: decider mode (MemoArgs::decider), a separate instantiation so that the classic
 // kernel's register allocation does not carry the decider's code.
-template <bool kDecider>
+// kProf: the KSIM_PROFILE phase timers and step trace; the production instantiation compiles them out
+// (this kernel's critical path is sensitive to code size and scalar-register pressure).
+template <bool kDecider, bool kProf>
 __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __restrict__ tp_all) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MemoShared& sh = *reinterpret_cast<MemoShared*>(smem);
@@ -745,7 +747,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; sh.crit_done = 0; }
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
-  const bool prof = a.prof != nullptr;
+  const bool prof = kProf && a.prof != nullptr;
+  unsigned long long* const trace = kProf ? a.trace : nullptr;
   if (prof && tid < kProfPhases) sh.prof[tid] = 0ull;
   unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -875,8 +878,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       for (int i = tid; i <= ne + kLag; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
       __syncthreads();
     }
-    if (a.trace && tid == 0 && step < a.trace_steps)
-      a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4] = __builtin_amdgcn_s_memrealtime();
+    if (trace && tid == 0 && step < a.trace_steps)
+      trace[((size_t)blockIdx.x * a.trace_steps + step) * 4] = __builtin_amdgcn_s_memrealtime();
     // one LDS round trip: the event, its owner code, d and d's record
     const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
     const int oc = __builtin_amdgcn_readfirstlane(sh.evo[eb]);
@@ -983,8 +986,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
             __builtin_amdgcn_s_sleep(0);
           sh.crit_done = 0;
           if (prof) sh.prof[17] += __builtin_amdgcn_s_memrealtime() - t_loaded;
-          if (a.trace && step < a.trace_steps)
-            a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+          if (trace && step < a.trace_steps)
+            trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 3] = __builtin_amdgcn_s_memrealtime();
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -998,8 +1001,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         gk_crit = gk > z ? gk : z;
         fresh = ofeas ? gk_crit : 0u;
         if (prof && tid == 0) sh.prof[18] += __builtin_amdgcn_s_memrealtime() - t_loaded;
-        if (a.trace && lane == 0 && step < a.trace_steps)
-          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+        if (trace && lane == 0 && step < a.trace_steps)
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
       }
       const unsigned W = fresh > ex ? fresh : ex;
       const int rk = W != 0u ? key32_rank(W) : -1;
@@ -1011,8 +1014,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         gstore32(win + step, pay);
         asm volatile("" ::: "memory");
         if (prof) sh.prof[20] += __builtin_amdgcn_s_memrealtime() - t_loaded;
-        if (a.trace && step < a.trace_steps)
-          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        if (trace && step < a.trace_steps)
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
         const int nfeas = cnt_o + (d >= 0 ? (fresh != 0u ? 1 : 0) - (old_own != 0u ? 1 : 0) : 0);
         ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
         if (W != 0u) {
@@ -1132,8 +1135,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           if (++spins > kSpinLimit) { ok = false; break; }
           __builtin_amdgcn_s_sleep(1);
         }
-        if (a.trace && step < a.trace_steps)
-          a.trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+        if (trace && step < a.trace_steps)
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
       }
       int nd = -1;
       if (!ok) {
