@@ -1532,7 +1532,9 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
                                  (int)pl.lds));
     hipLaunchKernelGGL((ksim_memo::k_memo<true, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
                        (const TypDev*)e->d_tp);
-  } else if (profile || tracing || e->report || !e->d_th) {  // the general instantiation
+  } else if (profile || tracing || e->report || !e->d_th ||
+             std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; })) {
+    // the general instantiation
     KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)pl.lds));
     hipLaunchKernelGGL((ksim_memo::k_memo<false, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,

@@ -702,9 +702,10 @@ __device__ void memo_decider(const MemoArgs& a, const ReplicaDev& rp, MemoShared
 // ---------------------------------------------------------------------------
 // kDecider: decider mode (MemoArgs::decider), a separate instantiation so that the classic
 // kernel's register allocation does not carry the decider's code.
-// kGeneral: the KSIM_PROFILE phase timers and step trace, the per-event cluster report stores and
-// the direct sigmoid expression when the host has no score table.  The lean instantiation
-// (kGeneral = false: no profile, no report, score table present -- the bench and the sweeps)
+// kGeneral: the KSIM_PROFILE phase timers and step trace, the per-event cluster report stores,
+// delete events and the direct sigmoid expression when the host has no score table.  The lean
+// instantiation (kGeneral = false: no profile, no report, no delete event, score table present --
+// the bench and the paper sweeps)
 // compiles them out of the step loop: this kernel's critical path is sensitive to code size and
 // scalar-register pressure (39.1 -> 35.8 ms per C2 launch for the profile hooks alone).
 template <bool kDecider, bool kGeneral>
@@ -889,7 +890,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     const int d = __builtin_amdgcn_readfirstlane(sh.dirty);
     const NodeV dn = ksim_replay::uniform_node(&sh.dnode);
     const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
-    const bool del = (p.flags & kPodDelete) != 0u;
+    const bool del = kGeneral && (p.flags & kPodDelete) != 0u;  // lean: launched on create-only streams
     const bool own = !kDecider && oc >= 0 && (oc >> 16) == w;  // decider mode: workgroup 0 decides
     const int oslot = own ? (oc & 0xff) : -1;
     const int crep = own ? ((oc >> 8) & 0xff) : -1;
