@@ -643,7 +643,10 @@ struct GranV {
 };
 
 // kSub = ceil(K / 64): 1 for K <= 64, 4 for K <= 256 (one wave-0 lane polls kSub workgroups).
-template <int kPol, int kSub>
+// kGeneral: the KSIM_PROFILE timers, the cluster-report stores and delete events (bind history);
+// the lean instantiation (none of them: the bench, the paper sweeps, C5) compiles them out of the
+// step loop, as k_memo's does.
+template <int kPol, int kSub, bool kGeneral>
 __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
                                                                  const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
@@ -669,7 +672,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   int* s_last = reinterpret_cast<int*>(s_F0 + S1);
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   // (null when no replica of the launch has a delete event: nothing ever reads it)
-  int2* hist = a.hist ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
+  int2* hist = (kGeneral && a.hist) ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
+  NodeRec* const snap = kGeneral ? rp.snap : nullptr;
   unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * 4;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
@@ -695,7 +699,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   int p_st0 = 0, p_st1 = 0, p_st2 = 0, p_st3 = 0;  // K == 1: the step's own totals
 
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
-  const bool prof = a.prof != nullptr;
+  const bool prof = kGeneral && a.prof != nullptr;
   if (prof && tid < kProfPhases) sh.prof[tid] = 0ull;
   unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -797,8 +801,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
               reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
                   reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
-            else if (lane == 7 && rp.snap) {  // cluster report: the post-Bind record (the virtual slot)
-              store_node(rp.snap + p_step, load_node(&s_nodes[ns]));
+            else if (lane == 7 && snap) {  // cluster report: the post-Bind record (the virtual slot)
+              store_node(snap + p_step, load_node(&s_nodes[ns]));
               rp.prev[p_step] = s_last[p_b];
               s_last[p_b] = p_step;
             }
@@ -846,7 +850,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     const PodDev p = uniform_pod(&sh.ev[eb]);
     const int2 pvb = *reinterpret_cast<const int2*>(&sh.pend_valid);
     const bool pend = __builtin_amdgcn_readfirstlane(pvb.x) != 0;
-    if (p.flags & kPodDelete) {
+    if (kGeneral && (p.flags & kPodDelete)) {  // lean: launched on create-only streams
       if (pend) finish_pending();
       if (sh.stop) break;
       // removePod on the owner of the creation (every workgroup recorded its view of it)
@@ -857,8 +861,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
           const int loc = h.x - n_lo;
           apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
-          if (rp.snap) {
-            store_node(rp.snap + step, load_node(&s_nodes[loc]));
+          if (snap) {
+            store_node(snap + step, load_node(&s_nodes[loc]));
             rp.prev[step] = s_last[loc];
             s_last[loc] = step;
           }
@@ -1271,15 +1275,22 @@ static int upload_reps(ksim_engine* e) {
   return KSIM_OK;
 }
 
-template <int P>
-static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp) {
+template <int P, bool G>
+static void launch_replay_g(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp) {
   if (ra.K <= 64) {
-    (void)hipFuncSetAttribute((const void*)k_replay<P, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_replay<P, 1>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+    (void)hipFuncSetAttribute((const void*)k_replay<P, 1, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_replay<P, 1, G>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
   } else {
-    (void)hipFuncSetAttribute((const void*)k_replay<P, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_replay<P, 4>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+    (void)hipFuncSetAttribute((const void*)k_replay<P, 4, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_replay<P, 4, G>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
   }
+}
+// general: profile timers, report stores or delete events needed; else the lean instantiation
+template <int P>
+static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp,
+                          bool general) {
+  if (general) launch_replay_g<P, true>(grid, lds, st, ra, tp);
+  else launch_replay_g<P, false>(grid, lds, st, ra, tp);
 }
 
 // ---- k_memo planning (memoised FGD replay, ksim_memo.hpp) ----
@@ -2418,13 +2429,14 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                             e->stream));
     const int grid = Rg * K;
     const TypDev* tp = e->d_tp;
+    const bool general = profile || e->report || any_delete;
     switch (gp.first) {
-      case POL_FGD: launch_replay<POL_FGD>(grid, lds, e->stream, ra, tp); break;
-      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, e->stream, ra, tp); break;
-      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, e->stream, ra, tp); break;
-      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, e->stream, ra, tp); break;
-      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, e->stream, ra, tp); break;
-      default: launch_replay<POL_RANDOM>(grid, lds, e->stream, ra, tp); break;
+      case POL_FGD: launch_replay<POL_FGD>(grid, lds, e->stream, ra, tp, general); break;
+      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, e->stream, ra, tp, general); break;
+      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, e->stream, ra, tp, general); break;
+      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, e->stream, ra, tp, general); break;
+      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, e->stream, ra, tp, general); break;
+      default: launch_replay<POL_RANDOM>(grid, lds, e->stream, ra, tp, general); break;
     }
     KSIM_HIP(hipGetLastError());
     e->last_K = K;
