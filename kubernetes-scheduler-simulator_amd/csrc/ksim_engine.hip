@@ -1239,6 +1239,11 @@ struct ksim_engine {
   int2* d_pws = nullptr;     // [R][N] PWR phase-A scratch
   std::vector<char> pw_set;  // set_power_model called
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_mid = nullptr;
+  // side streams for concurrent single-workgroup k_replay groups (created on first use)
+  static constexpr int kSide = 6;
+  hipStream_t side[kSide] = {};
+  hipEvent_t side_ev[kSide] = {};
+  hipEvent_t ev_fork = nullptr;
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
   bool report = false;
@@ -1792,6 +1797,11 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg};
   for (void* p : bufs) (void)hipFree(p);
+  for (int i = 0; i < ksim_engine::kSide; ++i) {
+    if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
+    if (e->side_ev[i]) (void)hipEventDestroy(e->side_ev[i]);
+  }
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
@@ -2371,8 +2381,40 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   const bool profile = pe && pe[0] == '1';
   int first = 0;
   e->last_memo = 0;
+  // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
+  // co-residency needed) run concurrently on side streams: a paper-sweep group fills 170 of 256 CUs,
+  // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
+  // profile timers) keeps the launches back to back on the engine stream.
+  bool concurrent = !profile && groups.size() >= 2;
+  for (const auto& gp : groups) {
+    if (!concurrent) break;
+    if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
+    int K = choose_wgs(e, gp.second);
+    int S = (e->N + K - 1) / K;
+    while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && gp.second * (K + 1) <= e->cus) {
+      ++K;
+      S = (e->N + K - 1) / K;
+    }
+    concurrent = K == 1;
+  }
+  int gidx = 0;
+  if (concurrent) {
+    if (!e->ev_fork) KSIM_HIP(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+    KSIM_HIP(hipEventRecord(e->ev_fork, e->stream));
+  }
   for (const auto& gp : groups) {
     const int Rg = gp.second;
+    hipStream_t gs = e->stream;
+    if (concurrent) {
+      const int i = gidx % ksim_engine::kSide;
+      if (!e->side[i]) {
+        KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
+        KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
+      }
+      gs = e->side[i];
+      if (gidx < ksim_engine::kSide) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));
+    }
+    ++gidx;
     // FGD: the memoised replay when the cluster and the classes fit (run_mode 0 / 3)
     if (gp.first == POL_FGD && e->run_mode != 2) {
       if (e->mplan_ok) {  // prepared by prepare_memo (the FGD replicas are the first group of `order`)
@@ -2424,19 +2466,20 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * words, e->stream));
       ra.prof = e->d_prof;
     }
-    // re-initialise every polled word before the launch (granule tags restart at step 1)
-    KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
-                            e->stream));
+    // re-initialise every polled word before the launch (granule tags restart at step 1; K = 1 polls none)
+    if (K > 1)
+      KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
+                              e->stream));
     const int grid = Rg * K;
     const TypDev* tp = e->d_tp;
     const bool general = profile || e->report || any_delete;
     switch (gp.first) {
-      case POL_FGD: launch_replay<POL_FGD>(grid, lds, e->stream, ra, tp, general); break;
-      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, e->stream, ra, tp, general); break;
-      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, e->stream, ra, tp, general); break;
-      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, e->stream, ra, tp, general); break;
-      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, e->stream, ra, tp, general); break;
-      default: launch_replay<POL_RANDOM>(grid, lds, e->stream, ra, tp, general); break;
+      case POL_FGD: launch_replay<POL_FGD>(grid, lds, gs, ra, tp, general); break;
+      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, gs, ra, tp, general); break;
+      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, gs, ra, tp, general); break;
+      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, gs, ra, tp, general); break;
+      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, gs, ra, tp, general); break;
+      default: launch_replay<POL_RANDOM>(grid, lds, gs, ra, tp, general); break;
     }
     KSIM_HIP(hipGetLastError());
     e->last_K = K;
@@ -2448,6 +2491,11 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       print_replay_profile(e, Rg, K, max_ev);
     }
   }
+  if (concurrent)  // join: the engine stream waits for every side stream used
+    for (int i = 0; i < std::min(gidx, (int)ksim_engine::kSide); ++i) {
+      KSIM_HIP(hipEventRecord(e->side_ev[i], e->side[i]));
+      KSIM_HIP(hipStreamWaitEvent(e->stream, e->side_ev[i], 0));
+    }
   return KSIM_OK;
 }
 
