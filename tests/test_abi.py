@@ -73,3 +73,9 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")):
                 txt = open(os.path.join(root, f)).read()
                 assert "pyoracle" not in txt and "liboracle" not in txt, f
+
+
+def test_integration_names_every_entry_point():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    missing = sorted(n for n in declared_functions() if "`" + n + "`" not in doc and "C." + n not in doc)
+    assert not missing, missing
