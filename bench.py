@@ -33,7 +33,7 @@ BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # HBM bytes per launch of the dominant kernel of this default workload from the PMC passes of
 # scripts/profile_round.sh (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section)
-PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("lean", "final", "gorand", "memo", "round_end")]
+PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("head_check", "lean", "final", "gorand", "memo", "round_end")]
 
 
 def cpu_baseline(trace, seed, threads):
