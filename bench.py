@@ -176,6 +176,19 @@ def main():
                 traffic = pmc["hbm_bytes_per_dispatch"]
                 traffic_src = os.path.relpath(pf, ROOT)
                 break
+    # FGD is VALU-bound, so the VALU issue fraction is reported beside the HBM one. The
+    # instruction count per launch comes from a PMC pass (scripts/profile_valu.sh -> profiles/ summary);
+    # the rate uses this run's live kernel time.
+    valu = None
+    vf = os.path.join(ROOT, "profiles", "r01", "head_check", "valu.json")
+    if default_cfg and os.path.exists(vf):
+        with open(vf) as f:
+            v = json.load(f)
+        if v.get("kernel") == kernel:
+            rate = v["valu_insts_per_dispatch"] / (kern_us * 1e-6)
+            valu = {"bound": "valu", "achieved": rate, "peak": v["peak_valu_insts_per_s"], "unit": "wave-instr/s",
+                    "frac": rate / v["peak_valu_insts_per_s"], "insts_per_launch": v["valu_insts_per_dispatch"],
+                    "source": os.path.relpath(vf, ROOT)}
     line = {
         "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
         "value": value,
@@ -199,6 +212,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kernel, "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
                      "wgs_per_replica": eng.last_run_wgs()},
+        "valu_roofline": valu,
     }
     if args.config == "c4":
         line["data"] = "Alibaba openb traces (data/openb: 17 pod lists), the reference's own event order (Go math/rand replay)"
