@@ -49,11 +49,30 @@ def cpu_baseline(trace, seed, threads):
     t0 = time.perf_counter()
     O.run_events(nodes, tp, ev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=threads)
     dt = time.perf_counter() - t0
+    # one thread too, on a bounded prefix of the same stream (the first 1500 events)
+    nodes1 = helpers.oracle_nodes(trace, rp)
+    t1 = time.perf_counter()
+    O.run_events(nodes1, tp, ev[:1500], policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=1)
+    one = 1500 / (time.perf_counter() - t1)
     return dict(value=len(ev) / dt, unit="pods/s", cores=threads, kind="port",
                 node_evals_per_s=len(ev) * trace.num_nodes / dt,
+                single_thread={"value": one, "unit": "pods/s", "cores": 1,
+                               "sample": "the first 1500 events of the same stream"},
                 sample="openb default, seed %d, full replay (%d events x %d nodes), FGD, %d worker threads "
-                       "(parallelize.Until fan-out); host nproc=%d" % (seed, len(ev), trace.num_nodes, threads,
-                                                                        os.cpu_count()))
+                       "(parallelize.Until fan-out); host nproc=%d, cpu %s" % (seed, len(ev), trace.num_nodes, threads,
+                                                                               os.cpu_count(), cpu_model()))
+
+
+def cpu_model():
+    """Host CPU model name (SURVEY §8(d) asks for it beside the thread count)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def seeds_for_rank(rank, replicas, base=42):
