@@ -49,7 +49,7 @@ class Sweep:
     policies (k_memo / k_replay) and, when the plan has PWR experiments, one for those (k_step +
     k_step_pwr per pod)."""
 
-    def __init__(self, experiments, device=0, report=True, wgs=0):
+    def __init__(self, experiments, device=0, report=True, wgs=0, fgd_batch=0):
         self.exps = list(experiments)
         traces = {}
         for (t, _, _, _) in self.exps:
@@ -63,7 +63,12 @@ class Sweep:
         rest = [i for i, e in enumerate(self.exps) if e[1] not in PWR_POLICY_DIRS]
         self.groups = []
         self.total_events = 0
-        for idx in (rest, pwr):
+        parts = [rest, pwr]
+        if fgd_batch > 0:  # FGD experiments as separate engines of fgd_batch replicas (k_memo where they fit)
+            fgd = [i for i in rest if self.exps[i][1] == "06-FGD"]
+            parts = [[i for i in rest if i not in set(fgd)], pwr] + \
+                [fgd[k:k + fgd_batch] for k in range(0, len(fgd), fgd_batch)]
+        for idx in parts:
             if not idx:
                 continue
             eng = ksim.Engine(nn, len(idx), device=device, wgs_per_replica=wgs)

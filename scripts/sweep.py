@@ -36,6 +36,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep"))
     ap.add_argument("--traces", default="all")
+    ap.add_argument("--fgd-batch", type=int, default=0,
+                    help="run the FGD experiments as engines of this many replicas (0: one engine for all)")
     ap.add_argument("--pwr", action="store_true",
                     help="also the fork's PWR runs (07-PWR, 08/11/12 PWR+FGD; no expected_results for them)")
     args = ap.parse_args()
@@ -46,7 +48,7 @@ def main():
     policies = tuple(SW.ALL_POLICY_DIRS) if args.pwr else tuple(SW.POLICY_DIRS)
     exps = SW.shard(SW.plan(traces=traces, policies=policies), rank, world)
     t0 = time.perf_counter()
-    sw = SW.Sweep(exps, device=local)
+    sw = SW.Sweep(exps, device=local, fgd_batch=args.fgd_batch)
     t_setup = time.perf_counter() - t0
     dev_ms, wall = sw.run()
     t1 = time.perf_counter()
