@@ -182,10 +182,12 @@ typedef struct {
     int32_t steps_per_graph;       /* k_step: pod steps captured per hipGraph (default 256) */
     int32_t wgs_per_replica;       /* k_replay: workgroups per replica (0 = CUs / replicas, <= 64) */
     int32_t run_mode;              /* ksim_engine_run: 0 = auto (FGD: memoised k_memo when the cluster and its pod
-                                      classes fit in LDS, else k_replay), 1 = k_step per pod (hipGraph),
-                                      2 = k_replay only, 3 = k_memo required for FGD (KSIM_ENOTSUP otherwise),
-                                      4 = k_memo in decider mode (workgroup 0 decides every event from the
-                                      class owners' top lists; KSIM_ENOTSUP if it does not fit) */
+                                      classes fit in LDS, else k_hmemo when it fits, else k_replay),
+                                      1 = k_step per pod (hipGraph), 2 = k_replay only, 3 = k_memo required
+                                      for FGD (KSIM_ENOTSUP otherwise), 4 = k_memo in decider mode (workgroup 0
+                                      decides every event from the class owners' top lists; KSIM_ENOTSUP if it
+                                      does not fit), 5 = k_hmemo required for FGD (one workgroup per replica,
+                                      keys in HBM; KSIM_ENOTSUP if it does not fit) */
     int32_t reserved[3];
 } ksim_config;
 
@@ -268,13 +270,15 @@ int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
 /* Workgroups per replica used by the last run. */
 int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 /* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),
- * KSIM_PATH_MEMO (k_memo, memoised FGD keys), KSIM_PATH_MIXED (k_memo for the FGD replicas, k_replay
- * for the others), KSIM_PATH_STEP (k_step per pod, hipGraph), KSIM_PATH_SHARDED (node-sharded). */
+ * KSIM_PATH_MEMO (k_memo, memoised FGD keys), KSIM_PATH_MIXED (a memoised kernel for the FGD replicas,
+ * k_replay for the others), KSIM_PATH_STEP (k_step per pod, hipGraph), KSIM_PATH_SHARDED (node-sharded),
+ * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica). */
 #define KSIM_PATH_REPLAY  0
 #define KSIM_PATH_MEMO    1
 #define KSIM_PATH_MIXED   2
 #define KSIM_PATH_STEP    3
 #define KSIM_PATH_SHARDED 4
+#define KSIM_PATH_HMEMO   5
 int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus

@@ -29,6 +29,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
+#include <numeric>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -627,6 +630,7 @@ __global__ void k_shard_gather(unsigned long long* const* sends, unsigned long l
 #include "ksim_replay.hpp"
 #include "ksim_report.hpp"
 #include "ksim_memo.hpp"
+#include "ksim_hmemo.hpp"
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
@@ -1229,6 +1233,25 @@ struct ksim_engine {
   std::vector<int> mplan_reps;
   int mplan_max_ev = -1;
   int last_memo = 0;
+  // k_hmemo (memoised FGD replay, keys in HBM): the plan and its device tables
+  struct HPlan* hplan = nullptr;
+  bool hplan_ok = false;
+  int* d_h_cg = nullptr;
+  PodDev* d_h_cls = nullptr;
+  uint16_t* d_h_cgrp = nullptr;
+  PodDev* d_h_gpod = nullptr;
+  int* d_h_evc = nullptr;
+  NodeRec* d_h_st = nullptr;
+  int* d_h_ns = nullptr;
+  int* d_h_nstate = nullptr;
+  unsigned* d_h_gsc = nullptr;
+  unsigned* d_h_keys = nullptr;
+  unsigned* d_h_l1 = nullptr;
+  int* d_h_cnt = nullptr;
+  unsigned long long* d_h_prof = nullptr;
+  size_t h_cap[13] = {};
+  int last_hmemo = 0;
+  std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
   bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
@@ -1430,6 +1453,134 @@ static const double* score_table() {
   return ok ? th : nullptr;
 }
 
+// ---- k_hmemo planning (memoised FGD replay with the keys in HBM, ksim_hmemo.hpp) ----
+struct HPlan {
+  int Cmax = 1, Gmax = 1, Smax = 1, Npad = 0, nb = 0;
+  size_t lds = 0;
+  std::vector<int> cg;            // [Rg][2] classes, groups
+  std::vector<PodDev> cls, gpod;  // [Rg][Cmax] (sorted by group), [Rg][Gmax]
+  std::vector<uint16_t> cgrp;     // [Rg][Cmax]
+  std::vector<int> evc;           // [Rg][stride] class slot of each event, -1 delete
+  std::vector<NodeRec> st;        // [Rg][Smax] distinct initial node states
+  std::vector<int> ns;            // [Rg]
+  std::vector<int> nstate;        // [Rg][Npad] state of each rank, -1 padding
+};
+
+// Classes of each replica grouped by score request (cpu_nz, milli, num: the candidate states of
+// fgd_score.go:99-149 depend on nothing else), and the distinct initial node states (the keys
+// before the first event depend on the state, the class and the rank only).
+static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int stride, HPlan& pl) {
+  using namespace ksim_hmemo;
+  const int Rg = (int)reps.size();
+  if (Rg == 0 || e->N > kMaxNb * kFan || e->N > kHRankMax || !score_table()) return false;
+  pl.Npad = (e->N + kFan - 1) / kFan * kFan;
+  pl.nb = pl.Npad / kFan;
+  std::vector<std::vector<int>> ord(Rg), gof(Rg), slot(Rg), gfirst(Rg), sof(Rg);
+  std::vector<std::vector<NodeRec>> sts(Rg);
+  pl.Cmax = pl.Gmax = pl.Smax = 1;
+  for (int i = 0; i < Rg; ++i) {
+    const int r = reps[i];
+    const std::vector<PodDev>& cls = e->h_cls[r];
+    std::vector<std::array<int, 3>> gk;
+    gof[i].resize(cls.size());
+    for (size_t c = 0; c < cls.size(); ++c) {
+      const std::array<int, 3> k{cls[c].cpu_nz, cls[c].milli, cls[c].num};
+      const auto it = std::find(gk.begin(), gk.end(), k);
+      gof[i][c] = (int)(it - gk.begin());
+      if (it == gk.end()) { gk.push_back(k); gfirst[i].push_back((int)c); }
+    }
+    if ((int)cls.size() > kMaxClasses || (int)gk.size() > kMaxGroups) return false;
+    ord[i].resize(cls.size());
+    std::iota(ord[i].begin(), ord[i].end(), 0);
+    std::stable_sort(ord[i].begin(), ord[i].end(), [&](int a, int b) { return gof[i][a] < gof[i][b]; });
+    slot[i].assign(cls.size(), -1);
+    for (size_t k = 0; k < ord[i].size(); ++k) slot[i][ord[i][k]] = (int)k;
+    pl.Cmax = std::max(pl.Cmax, (int)cls.size());
+    pl.Gmax = std::max(pl.Gmax, (int)gk.size());
+    // distinct initial states (every field but the rank)
+    if (e->h_rec[r].size() != (size_t)e->N) return false;
+    std::map<std::array<uint32_t, 7>, int> sid;
+    sof[i].assign(pl.Npad, -1);
+    for (int j = 0; j < e->N; ++j) {
+      const NodeRec& n = e->h_rec[r][j];
+      std::array<uint32_t, 7> k;
+      std::memcpy(k.data(), &n, sizeof k);
+      auto it = sid.find(k);
+      if (it == sid.end()) {
+        it = sid.emplace(k, (int)sts[i].size()).first;
+        sts[i].push_back(n);
+      }
+      sof[i][(int)(n.name_rank - (uint32_t)e->node_off)] = it->second;
+    }
+    pl.Smax = std::max(pl.Smax, (int)sts[i].size());
+  }
+  pl.lds = hmemo_layout(e->N, pl.Cmax, pl.Gmax, pl.nb).total;
+  if (pl.lds > 160 * 1024) return false;
+  pl.cg.assign((size_t)Rg * 2, 0);
+  pl.cls.assign((size_t)Rg * pl.Cmax, PodDev{});
+  pl.cgrp.assign((size_t)Rg * pl.Cmax, 0);
+  pl.gpod.assign((size_t)Rg * pl.Gmax, PodDev{});
+  pl.evc.assign((size_t)Rg * stride, -1);
+  pl.st.assign((size_t)Rg * pl.Smax, NodeRec{});
+  pl.ns.assign(Rg, 0);
+  pl.nstate.assign((size_t)Rg * pl.Npad, -1);
+  for (int i = 0; i < Rg; ++i) {
+    const int r = reps[i];
+    const std::vector<PodDev>& cls = e->h_cls[r];
+    pl.cg[2 * i] = (int)cls.size();
+    pl.cg[2 * i + 1] = (int)gfirst[i].size();
+    for (size_t k = 0; k < ord[i].size(); ++k) {
+      pl.cls[(size_t)i * pl.Cmax + k] = cls[ord[i][k]];
+      pl.cgrp[(size_t)i * pl.Cmax + k] = (uint16_t)gof[i][ord[i][k]];
+    }
+    for (size_t g = 0; g < gfirst[i].size(); ++g) pl.gpod[(size_t)i * pl.Gmax + g] = cls[gfirst[i][g]];
+    const std::vector<int>& ec = e->h_ev_cls[r];
+    for (size_t k = 0; k < ec.size(); ++k) pl.evc[(size_t)i * stride + k] = ec[k] < 0 ? -1 : slot[i][ec[k]];
+    std::copy(sts[i].begin(), sts[i].end(), pl.st.begin() + (size_t)i * pl.Smax);
+    pl.ns[i] = (int)sts[i].size();
+    std::copy(sof[i].begin(), sof[i].end(), pl.nstate.begin() + (size_t)i * pl.Npad);
+  }
+  return true;
+}
+
+template <typename T>
+static int upload_vec(T*& p, size_t& cap, const std::vector<T>& v, hipStream_t st) {
+  int rc = ensure_buf(p, cap, v.size());
+  if (rc) return rc;
+  KSIM_HIP(hipMemcpyAsync(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
+  return KSIM_OK;
+}
+
+static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev) {
+  e->hplan_ok = false;
+  if (!e->hplan) e->hplan = new HPlan();
+  HPlan& pl = *e->hplan;
+  const int stride = std::max(max_ev, 1);
+  if (!hmemo_plan(e, reps, stride, pl)) return KSIM_OK;
+  const int Rg = (int)reps.size();
+  hipStream_t st = e->stream;
+  int rc;
+  if ((rc = upload_vec(e->d_h_cg, e->h_cap[0], pl.cg, st))) return rc;
+  if ((rc = upload_vec(e->d_h_cls, e->h_cap[1], pl.cls, st))) return rc;
+  if ((rc = upload_vec(e->d_h_cgrp, e->h_cap[2], pl.cgrp, st))) return rc;
+  if ((rc = upload_vec(e->d_h_gpod, e->h_cap[3], pl.gpod, st))) return rc;
+  if ((rc = upload_vec(e->d_h_evc, e->h_cap[4], pl.evc, st))) return rc;
+  if ((rc = upload_vec(e->d_h_st, e->h_cap[5], pl.st, st))) return rc;
+  if ((rc = upload_vec(e->d_h_ns, e->h_cap[6], pl.ns, st))) return rc;
+  if ((rc = upload_vec(e->d_h_nstate, e->h_cap[7], pl.nstate, st))) return rc;
+  if ((rc = ensure_buf(e->d_h_gsc, e->h_cap[8], (size_t)Rg * pl.Gmax * pl.Smax))) return rc;
+  if ((rc = ensure_buf(e->d_h_keys, e->h_cap[9], (size_t)Rg * pl.Cmax * pl.Npad))) return rc;
+  if ((rc = ensure_buf(e->d_h_l1, e->h_cap[10], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
+  if ((rc = ensure_buf(e->d_h_cnt, e->h_cap[11], (size_t)Rg * pl.Cmax))) return rc;
+  if (!e->d_th) {
+    KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
+    KSIM_HIP(hipMemcpyAsync(e->d_th, score_table(), sizeof(double) * 102, hipMemcpyHostToDevice, st));
+  }
+  KSIM_HIP(hipStreamSynchronize(st));  // the host vectors are pageable
+  e->hplan_ok = true;
+  return KSIM_OK;
+}
+
 // Plan and upload the k_memo launch of the FGD replicas (before the timed region of a run; cached
 // until events or policies change).
 static int prepare_memo(ksim_engine* e, int max_ev) {
@@ -1442,13 +1593,15 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   e->mplan_reps = reps;
   e->mplan_max_ev = max_ev;
   e->mplan_ok = false;
+  e->hplan_ok = false;
   if (reps.empty()) return KSIM_OK;
+  if (e->run_mode == 5) return prepare_hmemo(e, reps, max_ev);  // k_hmemo required
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
   // run_mode 4 (or KSIM_MEMO_DECIDER=1 with run_mode 0): the decider variant of k_memo
   const char* dv = std::getenv("KSIM_MEMO_DECIDER");
   pl.decider = e->run_mode == 4 || (e->run_mode == 0 && dv && dv[0] == '1');
-  if (!memo_plan(e, reps, pl)) return KSIM_OK;
+  if (!memo_plan(e, reps, pl)) return e->run_mode == 0 ? prepare_hmemo(e, reps, max_ev) : KSIM_OK;
   const int Rg = (int)reps.size();
   int rc;
   if ((rc = ensure_buf(e->d_m_pod, e->m_cap[0], pl.pod.size()))) return rc;
@@ -1651,6 +1804,103 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   return KSIM_OK;
 }
 
+// k_hmemo launch: the initial keys (k_hinit_gk, k_hinit_keys), the replay, the result map.
+static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
+  using namespace ksim_hmemo;
+  const HPlan& pl = *e->hplan;
+  const int stride = std::max(max_ev, 1);
+  HInitArgs ia;
+  ia.reps = e->d_reps;
+  ia.rep_list = e->d_replist + first;
+  ia.N = e->N;
+  ia.Npad = pl.Npad;
+  ia.nb = pl.nb;
+  ia.Cmax = pl.Cmax;
+  ia.Gmax = pl.Gmax;
+  ia.Smax = pl.Smax;
+  ia.cg = e->d_h_cg;
+  ia.cls = e->d_h_cls;
+  ia.cgrp = e->d_h_cgrp;
+  ia.gpod = e->d_h_gpod;
+  ia.st = e->d_h_st;
+  ia.ns = e->d_h_ns;
+  ia.nstate = e->d_h_nstate;
+  ia.gsc = e->d_h_gsc;
+  ia.keys = e->d_h_keys;
+  ia.l1 = e->d_h_l1;
+  ia.cnt = e->d_h_cnt;
+  ia.th = e->d_th;
+  KSIM_HIP(hipMemsetAsync(e->d_h_cnt, 0, sizeof(int) * (size_t)Rg * pl.Cmax, st));
+  hipLaunchKernelGGL(k_hinit_gk, dim3((unsigned)((pl.Smax + 255) / 256), (unsigned)pl.Gmax, (unsigned)Rg), dim3(256), 0,
+                     st, ia, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_hinit_keys, dim3((unsigned)((pl.Npad + 255) / 256), (unsigned)pl.Cmax, (unsigned)Rg), dim3(256), 0,
+                     st, ia);
+  KSIM_HIP(hipGetLastError());
+  HMemoArgs ma;
+  ma.reps = e->d_reps;
+  ma.rep_list = e->d_replist + first;
+  ma.N = e->N;
+  ma.Npad = pl.Npad;
+  ma.nb = pl.nb;
+  ma.Cmax = pl.Cmax;
+  ma.Gmax = pl.Gmax;
+  ma.cg = e->d_h_cg;
+  ma.cls = e->d_h_cls;
+  ma.cgrp = e->d_h_cgrp;
+  ma.gpod = e->d_h_gpod;
+  ma.evc = e->d_h_evc;
+  ma.stride = stride;
+  ma.keys = e->d_h_keys;
+  ma.l1 = e->d_h_l1;
+  ma.cnt0 = e->d_h_cnt;
+  ma.th = e->d_th;
+  ma.prof = nullptr;
+  const char* pe = std::getenv("KSIM_PROFILE");
+  const bool profile = pe && pe[0] == '1';
+  if (profile) {
+    int rc = ensure_buf(e->d_h_prof, e->h_cap[12], (size_t)Rg * kHProf);
+    if (rc) return rc;
+    KSIM_HIP(hipMemsetAsync(e->d_h_prof, 0, sizeof(unsigned long long) * (size_t)Rg * kHProf, st));
+    ma.prof = e->d_h_prof;
+  }
+  KSIM_HIP(hipFuncSetAttribute((const void*)k_hmemo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
+  hipLaunchKernelGGL(k_hmemo, dim3((unsigned)Rg), dim3(kHBlock), pl.lds, st, ma, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
+                     e->d_reps, (const int*)(e->d_replist + first), e->N);
+  KSIM_HIP(hipGetLastError());
+  if (profile) {
+    KSIM_HIP(hipStreamSynchronize(st));
+    std::vector<unsigned long long> h((size_t)Rg * kHProf);
+    KSIM_HIP(hipMemcpy(h.data(), e->d_h_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    static const char* names[] = {"class pass", "list+loads", "F eval", "blocks+group keys", "class update", "decide+bind"};
+    std::fprintf(stderr, "ksim hmemo profile: %d replicas, LDS %zu B, Cmax %d Gmax %d Smax %d; us/step mean [max]:", Rg,
+                 pl.lds, pl.Cmax, pl.Gmax, pl.Smax);
+    for (int ph = 0; ph < 6; ++ph) {
+      double sum = 0, mx = 0;
+      for (int b = 0; b < Rg; ++b) {
+        const double us = (double)h[(size_t)b * kHProf + ph] / 100.0 / std::max(max_ev, 1);
+        sum += us;
+        mx = std::max(mx, us);
+      }
+      std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / Rg, mx);
+    }
+    double it = 0, fl = 0, rs = 0, cyc = 0, tick = 0;
+    for (int b = 0; b < Rg; ++b) {
+      it += (double)h[(size_t)b * kHProf + 7];
+      fl += (double)h[(size_t)b * kHProf + 8];
+      rs += (double)h[(size_t)b * kHProf + 9];
+      cyc += (double)h[(size_t)b * kHProf + 10];
+      tick += (double)h[(size_t)b * kHProf + 11];
+    }
+    if (rs > 0) std::fprintf(stderr, " F items/refresh %.1f, flagged classes/refresh %.1f;", it / rs, fl / rs);
+    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / Rg / 1e5);
+    std::fprintf(stderr, "\n");
+  }
+  return KSIM_OK;
+}
+
 extern "C" {
 
 const char* ksim_strerror(int code) {
@@ -1744,6 +1994,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMemcpy(e->d_acc, acc.data(), sizeof(Accum) * n_replicas, hipMemcpyHostToDevice));
   e->reps.resize(n_replicas);
   e->h_nodes.resize(n_replicas);
+  e->h_rec.resize(n_replicas);
   e->d_ev.assign(n_replicas, nullptr);
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
@@ -1795,7 +2046,8 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
-                  e->d_m_evcls, e->d_topg};
+                  e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
+                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -1808,6 +2060,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   if (e->comm) destroy_comm(e->comm);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e->mplan;
+  delete e->hplan;
   delete e;
 }
 
@@ -1879,6 +2132,8 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     rank2idx[lr] = i;
   }
   e->h_nodes[replica].assign(nodes, nodes + e->N);
+  e->h_rec[replica] = h;
+  e->mplan_dirty = true;  // k_hmemo's plan holds the distinct initial node states
   e->total_gpus[replica] = gpus;
   KSIM_HIP(hipSetDevice(e->device));
   KSIM_HIP(hipMemcpyAsync(e->d_cap + (size_t)replica * e->N, cap.data(), sizeof(int32_t) * e->N, hipMemcpyHostToDevice,
@@ -2381,6 +2636,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   const bool profile = pe && pe[0] == '1';
   int first = 0;
   e->last_memo = 0;
+  e->last_hmemo = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
   // co-residency needed) run concurrently on side streams: a paper-sweep group fills 170 of 256 CUs,
   // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
@@ -2389,6 +2645,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   for (const auto& gp : groups) {
     if (!concurrent) break;
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
+    if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) continue;  // one workgroup per replica
     int K = choose_wgs(e, gp.second);
     int S = (e->N + K - 1) / K;
     while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && gp.second * (K + 1) <= e->cus) {
@@ -2429,7 +2686,16 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                                   pl.decider ? " (decider)" : "", Rg, pl.K, pl.Cw, pl.nfw, pl.lds);
         continue;
       }
-      if (e->run_mode == 3 || e->run_mode == 4) return KSIM_ENOTSUP;
+      if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
+        const int rc = launch_hmemo(e, Rg, first, max_ev, gs);
+        if (rc) return rc;
+        e->last_K = 1;
+        e->last_groups = (int)groups.size();
+        e->last_hmemo += Rg;
+        first += Rg;
+        continue;
+      }
+      if (e->run_mode == 3 || e->run_mode == 4 || e->run_mode == 5) return KSIM_ENOTSUP;
     }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
@@ -2699,8 +2965,10 @@ int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   if (!e || !path) return KSIM_EINVAL;
   if (e->shard_world > 0) *path = KSIM_PATH_SHARDED;
   else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
-  else if (e->last_memo == 0) *path = KSIM_PATH_REPLAY;
-  else *path = e->last_memo == e->R ? KSIM_PATH_MEMO : KSIM_PATH_MIXED;
+  else if (e->last_memo == 0 && e->last_hmemo == 0) *path = KSIM_PATH_REPLAY;
+  else if (e->last_memo == e->R) *path = KSIM_PATH_MEMO;
+  else if (e->last_hmemo == e->R) *path = KSIM_PATH_HMEMO;
+  else *path = KSIM_PATH_MIXED;
   return KSIM_OK;
 }
 

@@ -1,0 +1,517 @@
+// ksim_hmemo.hpp -- memoised FGD replay with the (pod class, node) keys in HBM (k_hmemo).
+//
+// k_memo (ksim_memo.hpp) keeps every (class, node) key of a replica in LDS, spread over K
+// co-resident workgroups, so it only fits when the replica's classes x nodes fit K x 160 KB and
+// K x replicas <= CUs.  The paper sweep's 170 FGD replicas (one workgroup each) and the 100k-node
+// C5 cluster do not, and fell back to k_replay, which re-scores every node per pod.
+//
+// k_hmemo runs ONE workgroup per replica (no cross-workgroup exchange, hence no co-residency
+// requirement) and keeps:
+//   HBM   key[c][rank]            the packed key of every (class, node) pair (hkey below)
+//   LDS   L1[c][b] = max key[c][64b .. 64b+63]    (a max tree of fan-out 64, one level: N <= 4096)
+//         the cluster (node slot = name rank), the class table, the typical table.
+// Per pod step, with d = the node changed by the previous event (its Bind or a delete):
+//   1. class pass (one thread per class): Filter on d's new and old records (feasible counts),
+//      which score groups (same cpu_nz, milli, num: same candidate states, fgd_score.go:99-149)
+//      some class finds feasible, and which classes had d as the max of d's block (flagged);
+//   2. wave 0 lists the F evaluations: d's current state + each feasible group's candidates (one
+//      per distinct milli-left value among the fitting GPUs, or the NodeResource.Sub state); every
+//      quarter-wave issues the HBM load of one flagged class's 64-key block (held in registers);
+//   3. every quad of lanes evaluates one state's F (frag_F_quad, bit-exact with frag.go);
+//   4. the flagged blocks' maxima without d (quarter-wave DPP), the groups' keys on d;
+//   5. class pass: key[c][d] (HBM store) and L1[c][d/64] (max with the new key, or the block max
+//      without d when d was the block max);
+//   6. wave 0: the winner of the event's class = max over L1[class][*] (selectHost: max score, ties
+//      to the smallest name), Reserve's GPU selector on it, the Bind in LDS, the result.
+// Every key of every class is fresh at step 6, so the decision is the one k_replay / k_step / the
+// oracle make (same device functions: filter_node, fgd_candidate + frag_F_quad, the score table).
+//
+// Keys are produced before the run by k_hinit_gk / k_hinit_keys: one evaluation per (group,
+// distinct initial node state), then key = Filter ? that score with the node's rank : 0.
+#pragma once
+
+namespace ksim_hmemo {
+
+using namespace ksim;
+
+constexpr int kHBlock = 1024;
+constexpr int kHWaves = kHBlock / 64;
+constexpr int kFan = 64;              // keys per L1 block (one wave / one quarter-wave dwordx4 row)
+constexpr int kMaxNb = 64;            // L1 blocks per class (N <= 4096)
+constexpr int kMaxClasses = 1024;     // one class-pass thread each
+constexpr int kMaxGroups = 128;
+constexpr int kMaxItems = 1 + 8 * kMaxGroups;
+constexpr int kEvBuf = 128;
+constexpr int kQuarters = kHBlock / 16;
+
+// Packed key of (class, node): [30:24] score + 1 | [23:4] kHRankMax - rank | [3:0] gpu field
+// (15 - g for a share pod placed on GPU g, 0 otherwise).  0 = infeasible.  Max key = max score,
+// ties to the smallest name (selectHost, generic_scheduler.go:187-212); over one node's candidates
+// the max keeps the lowest GPU index reaching the max (fgd_score.go:128).  Non-negative as int32.
+constexpr int kHRankMax = (1 << 20) - 1;
+KSIM_HD unsigned hkey(int score, int rank, int gf) {
+  return ((unsigned)(score + 1) << 24) | ((unsigned)(kHRankMax - rank) << 4) | (unsigned)gf;
+}
+// The key without its rank field (k_hinit_gk); hkey(s, r, g) == hkey_norank(s, g) | hkey_rankbits(r).
+KSIM_HD unsigned hkey_norank(int score, int gf) { return ((unsigned)(score + 1) << 24) | (unsigned)gf; }
+KSIM_HD unsigned hkey_rankbits(int rank) { return (unsigned)(kHRankMax - rank) << 4; }
+KSIM_HD int hkey_score(unsigned k) { return (int)(k >> 24) - 1; }
+KSIM_HD int hkey_rank(unsigned k) { return kHRankMax - (int)((k >> 4) & (unsigned)kHRankMax); }
+KSIM_HD int hkey_gpu(unsigned k) {
+  const int gf = (int)(k & 15u);
+  return gf ? 15 - gf : -1;
+}
+
+struct HMemoArgs {
+  ReplicaDev* reps;
+  const int* rep_list;      // replica of each launch workgroup
+  int N, Npad, nb;          // nodes, padded to kFan, L1 blocks per class
+  int Cmax, Gmax;           // class / group table strides
+  const int* cg;            // [Rg][2] classes, groups
+  const PodDev* cls;        // [Rg][Cmax] class requests, sorted by group
+  const uint16_t* cgrp;     // [Rg][Cmax] group of each class
+  const PodDev* gpod;       // [Rg][Gmax] a request of each group (the score part is the group's)
+  const int* evc;           // [Rg][stride] class of each event, -1 delete
+  int stride;
+  unsigned* keys;           // [Rg][Cmax][Npad]
+  const unsigned* l1;       // [Rg][Cmax][nb] initial L1 (k_hinit_keys)
+  const int* cnt0;          // [Rg][Cmax] initial feasible counts
+  const double* th;         // [102] FGD score steps
+  unsigned long long* prof; // optional [Rg][kHProf] (KSIM_PROFILE=1)
+};
+constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
+
+struct __align__(16) HShared {
+  PodDev ev[kEvBuf];
+  int evc[kEvBuf];
+  TypDev tp[kMaxTypical];
+  double th[104];
+  NodeRec dold, dnew;  // the node the previous event changed: record before / after
+  int d;               // its rank, -1 none
+  unsigned dfirst;     // first_of_class(dnew, 0)
+  int nitems, nflag;
+  unsigned long long prof[kHProf];
+};
+static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned");
+
+// Dynamic LDS after HShared (16-B aligned regions).
+struct HLayout {
+  size_t cls, gpod, F, l1, nodes, last, cnt, bx, cgrp, flist, code, igrp, fnew, fold, gfeas, gbase, gkey, total;
+};
+KSIM_HD size_t halign(size_t x) { return (x + 15) & ~(size_t)15; }
+KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
+  HLayout L;
+  size_t o = sizeof(HShared);
+  L.cls = o;   o = halign(o + (size_t)Cmax * sizeof(PodDev));
+  L.gpod = o;  o = halign(o + (size_t)Gmax * sizeof(PodDev));
+  L.F = o;     o = halign(o + (size_t)kMaxItems * sizeof(double));
+  L.l1 = o;    o = halign(o + (size_t)Cmax * nb * 4);
+  L.nodes = o; o = halign(o + (size_t)N * sizeof(NodeRec));
+  L.last = o;  o = halign(o + (size_t)N * 4);
+  L.cnt = o;   o = halign(o + (size_t)Cmax * 4);
+  L.bx = o;    o = halign(o + (size_t)Cmax * 4);
+  L.cgrp = o;  o = halign(o + (size_t)Cmax * 2);
+  L.flist = o; o = halign(o + (size_t)Cmax * 2);
+  L.code = o;  o = halign(o + (size_t)kMaxItems);
+  L.igrp = o;  o = halign(o + (size_t)kMaxItems);
+  L.fnew = o;  o = halign(o + (size_t)Cmax);
+  L.fold = o;  o = halign(o + (size_t)Cmax);
+  L.gfeas = o; o = halign(o + (size_t)Gmax);
+  L.gbase = o; o = halign(o + (size_t)Gmax * 2);
+  L.gkey = o;  o = halign(o + (size_t)Gmax * 4);
+  L.total = o;
+  return L;
+}
+
+// Global-address-space access (flat loads / stores also count in lgkmcnt, so every later LDS wait
+// would stall on them; global_* ones count in vmcnt only).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld4(const unsigned* p) {
+  const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst1(unsigned* p, unsigned v) {
+  *(__attribute__((address_space(1))) unsigned*)(p) = v;
+}
+
+// Row (16-lane) max of unsigned values below 2^31: every lane of the row ends with it.
+__device__ __forceinline__ int row_max16(int v) {
+  using ksim_replay::dpp_i;
+  v = max(v, dpp_i<0xB1>(v));
+  v = max(v, dpp_i<0x4E>(v));
+  v = max(v, dpp_i<0x141>(v));
+  v = max(v, dpp_i<0x140>(v));
+  return v;
+}
+
+// Max of a 64-key block row held as one uint4 per lane of a 16-lane row, the key of node `d`
+// excluded (lane l16 holds nodes base + 4 l16 .. base + 4 l16 + 3).
+__device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int l16, int d) {
+  const int n0 = base + 4 * l16;
+  unsigned m = 0u;
+  m = (n0 + 0 != d && v.x > m) ? v.x : m;
+  m = (n0 + 1 != d && v.y > m) ? v.y : m;
+  m = (n0 + 2 != d && v.z > m) ? v.z : m;
+  m = (n0 + 3 != d && v.w > m) ? v.w : m;
+  return (unsigned)row_max16((int)m);
+}
+
+__global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
+  using namespace ksim_replay;
+  using ksim_memo::gget;
+  using ksim_memo::gput;
+  using ksim_memo::gput_node;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  HShared& sh = *reinterpret_cast<HShared*>(smem);
+  const int gi = (int)blockIdx.x;
+  const int r = a.rep_list[gi];
+  const ReplicaDev rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int N = a.N, nb = a.nb;
+  const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
+  const HLayout L = hmemo_layout(N, a.Cmax, a.Gmax, nb);
+  PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
+  PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
+  double* s_F = reinterpret_cast<double*>(smem + L.F);
+  unsigned* s_l1 = reinterpret_cast<unsigned*>(smem + L.l1);
+  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + L.nodes);
+  int* s_last = reinterpret_cast<int*>(smem + L.last);
+  int* s_cnt = reinterpret_cast<int*>(smem + L.cnt);
+  unsigned* s_bx = reinterpret_cast<unsigned*>(smem + L.bx);
+  uint16_t* s_cgrp = reinterpret_cast<uint16_t*>(smem + L.cgrp);
+  uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
+  uint8_t* s_code = reinterpret_cast<uint8_t*>(smem + L.code);
+  uint8_t* s_igrp = reinterpret_cast<uint8_t*>(smem + L.igrp);
+  uint8_t* s_fnew = reinterpret_cast<uint8_t*>(smem + L.fnew);
+  uint8_t* s_fold = reinterpret_cast<uint8_t*>(smem + L.fold);
+  uint8_t* s_gfeas = reinterpret_cast<uint8_t*>(smem + L.gfeas);
+  int16_t* s_gbase = reinterpret_cast<int16_t*>(smem + L.gbase);
+  unsigned* s_gkey = reinterpret_cast<unsigned*>(smem + L.gkey);
+  const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
+  unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
+  const int* evc = a.evc + (size_t)gi * a.stride;
+
+  // ---- start-up: cluster (slot = rank), classes, groups, typical table, score steps, L1, counts
+  for (int i = tid; i < N; i += kHBlock) {
+    store_node(&s_nodes[i], load_node(rp.nodes + rank2idx[i]));
+    s_last[i] = -1;
+  }
+  for (int c = tid; c < C; c += kHBlock) {
+    s_cls[c] = a.cls[(size_t)gi * a.Cmax + c];
+    s_cgrp[c] = a.cgrp[(size_t)gi * a.Cmax + c];
+    s_cnt[c] = a.cnt0[(size_t)gi * a.Cmax + c];
+  }
+  for (int g = tid; g < G; g += kHBlock) {
+    s_gpod[g] = a.gpod[(size_t)gi * a.Gmax + g];
+    s_gfeas[g] = 0;
+  }
+  for (int i = tid; i < C * nb; i += kHBlock) s_l1[i] = a.l1[(size_t)gi * a.Cmax * nb + i];
+  for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
+  for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
+  if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; }
+  const bool prof = a.prof != nullptr;
+  if (prof && tid < kHProf) sh.prof[tid] = 0ull;
+  unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto mark = [&](int ph) {
+    if (prof && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - t_last;
+      t_last = t;
+    }
+  };
+  __syncthreads();
+  const bool typed = rp.typed != 0;
+
+  for (int step = 0; step < rp.n_events; ++step) {
+    const int eb = step & (kEvBuf - 1);
+    if (eb == 0) {
+      const int ne = min(kEvBuf, rp.n_events - step);
+      const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+      for (int i = tid; i < ne * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
+      for (int i = tid; i < ne; i += kHBlock) sh.evc[i] = gget(evc + step + i);
+      __syncthreads();
+    }
+    const int d = __builtin_amdgcn_readfirstlane(sh.d);
+    if (d >= 0) {
+      const NodeV dn = uniform_node(&sh.dnew);
+      const int b = d / kFan;
+      // ---- 1. class pass
+      const NodeV dold = uniform_node(&sh.dold);
+      for (int c = tid; c < C; c += kHBlock) {
+        const PodDev q = s_cls[c];
+        const bool fn = filter_node(dn, q);
+        const bool fo = filter_node(dold, q);
+        s_fnew[c] = fn ? 1 : 0;
+        s_fold[c] = fo ? 1 : 0;
+        if (fn) s_gfeas[s_cgrp[c]] = 1;
+        const unsigned old = s_l1[c * nb + b];
+        if (old != 0u && hkey_rank(old) == d) s_flist[atomicAdd(&sh.nflag, 1)] = (uint16_t)c;
+      }
+      __syncthreads();
+      mark(0);
+      // ---- 2. the flagged blocks' loads (one quarter-wave each, held in registers) | wave 0: F list
+      const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
+      const int qid = tid >> 4, l16 = tid & 15;
+      uint4 bv = make_uint4(0u, 0u, 0u, 0u);
+      if (qid < nflag) {
+        const int c = s_flist[qid];
+        bv = gld4(keys + (size_t)c * a.Npad + (size_t)b * kFan + 4 * l16);
+      }
+      if (wv == 0) {
+        const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
+        int base = 1;  // item 0: d's current state
+        for (int g0 = 0; g0 < G; g0 += 64) {
+          const int g = g0 + lane;
+          unsigned cm = 0u;
+          bool share = false;
+          if (g < G && s_gfeas[g]) {
+            const PodDev gp = s_gpod[g];
+            share = is_share_pod(gp);
+            cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
+          }
+          const int nc = __popc(cm);
+          int excl = 0, tot = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const unsigned long long m = __ballot((nc >> k) & 1);
+            excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << k;
+            tot += __popcll(m) << k;
+          }
+          int o = base + excl;
+          if (g < G) s_gbase[g] = (int16_t)o;
+          unsigned mm = cm;
+          while (mm) {
+            const int x = __builtin_ctz(mm);
+            mm &= mm - 1u;
+            s_code[o] = (uint8_t)(share ? 1 + x : 9);
+            s_igrp[o] = (uint8_t)g;
+            ++o;
+          }
+          base += tot;
+        }
+        if (lane == 0) {
+          s_code[0] = 0;
+          s_igrp[0] = 0;
+          sh.nitems = base;
+        }
+      }
+      __syncthreads();
+      mark(1);
+      // ---- 3. F of every listed state, one quad each
+      {
+        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+        const int q = tid & 3;
+        for (int j = tid >> 2; j < nit; j += kHBlock / 4) {
+          const int code = s_code[j];
+          const PodDev gp = s_gpod[s_igrp[j]];
+          int cpuL, total;
+          uint32_t gs[4];
+          fgd_candidate(dn, code, gp, &cpuL, gs, &total);
+          const uint32_t tb = 1u << dn.gpu_type();
+          const double F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
+                                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          if (q == 0) s_F[j] = F;
+        }
+        if (prof && tid == 0) { sh.prof[7] += (unsigned long long)nit; sh.prof[8] += (unsigned long long)nflag; sh.prof[9] += 1ull; }
+      }
+      __syncthreads();
+      mark(2);
+      // ---- 4. flagged blocks without d (quarter rows) | group keys on d
+      if (qid < nflag) {
+        const unsigned m = block_max_excl(bv, b * kFan, l16, d);
+        if (l16 == 0) s_bx[s_flist[qid]] = m;
+      }
+      for (int i = kQuarters + qid; i < nflag; i += kQuarters) {  // more flagged classes than quarters
+        const int c = s_flist[i];
+        const uint4 v = gld4(keys + (size_t)c * a.Npad + (size_t)b * kFan + 4 * l16);
+        const unsigned m = block_max_excl(v, b * kFan, l16, d);
+        if (l16 == 0) s_bx[c] = m;
+      }
+      for (int g = tid; g < G; g += kHBlock) {
+        if (s_gfeas[g]) {
+          s_gfeas[g] = 0;
+          const double F0 = s_F[0];
+          const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : sh.nitems;  // the group's candidates
+          unsigned k;
+          if (is_share_pod(s_gpod[g])) {
+            k = hkey(0, d, 0);  // feasible with no fitting GPU
+            for (int i = o; i < oe; ++i) {
+              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
+              k = x > k ? x : k;
+            }
+          } else {
+            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
+          }
+          s_gkey[g] = k;
+        }
+      }
+      __syncthreads();
+      mark(3);
+      // ---- 5. every class's key on d, its L1 entry, its feasible count
+      for (int c = tid; c < C; c += kHBlock) {
+        const bool fn = s_fnew[c] != 0;
+        const unsigned k = fn ? s_gkey[s_cgrp[c]] : 0u;
+        gst1(keys + (size_t)c * a.Npad + d, k);
+        s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
+        unsigned* l = &s_l1[c * nb + b];
+        const unsigned old = *l;
+        if (k > old) *l = k;
+        else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
+      }
+      if (tid == 0) sh.nflag = 0;
+      __syncthreads();
+      mark(4);
+    }
+    // ---- 6. the event: the winner of its class (create) or the unbind (delete); wave 0
+    if (wv == 0) {
+      const PodDev p = uniform_pod(&sh.ev[eb]);
+      const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
+      int rk = -1, mask = 0;
+      NodeV before{}, after{};
+      ResultDev out{-1, 0, 0, 0, ST_DELETED};
+      if (cs >= 0) {
+        const unsigned lv = lane < nb ? s_l1[cs * nb + lane] : 0u;
+        const unsigned W = (unsigned)wave_max_dpp((int)lv);
+        const int nfeas = __builtin_amdgcn_readfirstlane(s_cnt[cs]);
+        out = ResultDev{-1, 0, 0, nfeas, ST_UNSCHED};
+        if (W != 0u) {
+          const int wr = hkey_rank(W);
+          const NodeV wn = uniform_node(&s_nodes[wr]);
+          mask = select_gpus(wn, p, rp.gpusel, hkey_gpu(W), rp.seed, step);
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+          } else {
+            out.status = ST_OK;
+            out.score = result_score(rp, nfeas, hkey_score(W), 0, 0);
+            out.node = wr;  // name rank; k_memo_finish maps it to the node index
+            out.gpu_mask = mask;
+            rk = wr;
+            before = wn;
+            after = wn;
+            bind_node(after, p, mask, +1);
+          }
+        }
+      } else if (p.ref >= 0 && p.ref < step) {
+        // simulator.go:416-422 deletePod: undo the creation's Bind (its result holds the rank and mask)
+        const ResultDev cr = gget(rp.res + p.ref);
+        const int crk = __builtin_amdgcn_readfirstlane(cr.node);
+        const int cst = __builtin_amdgcn_readfirstlane(cr.status);
+        const int cmask = __builtin_amdgcn_readfirstlane(cr.gpu_mask);
+        if (crk >= 0 && cst == ST_OK) {
+          const PodDev bp = uniform_pod(reinterpret_cast<const PodDev*>(rp.ev + p.ref));
+          rk = crk;
+          before = uniform_node(&s_nodes[rk]);
+          after = before;
+          bind_node(after, bp, cmask, -1);
+          out = ResultDev{rk, cmask, 0, 0, ST_DELETED};
+        }
+      }
+      if (lane == 0) {
+        gput(rp.res + step, out);
+        if (rk >= 0) {
+          store_node(&s_nodes[rk], after);
+          store_node(&sh.dold, before);
+          store_node(&sh.dnew, after);
+          if (rp.snap) {  // cluster report: the state this event left
+            gput_node(rp.snap + step, after);
+            gput(rp.prev + step, s_last[rk]);
+          }
+          s_last[rk] = step;
+        }
+        sh.d = rk;
+      }
+      if (rk >= 0) {
+        const unsigned fm = ksim_memo::first_mask_lanes(after, lane);
+        if (lane == 0) sh.dfirst = fm;
+      }
+    }
+    __syncthreads();
+    mark(5);
+  }
+  if (prof && tid == 0) {
+    sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
+    sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;
+  }
+  __syncthreads();
+  if (prof && tid < kHProf) a.prof[(size_t)gi * kHProf + tid] = sh.prof[tid];
+  // final cluster state
+  for (int i = tid; i < N; i += kHBlock) store_node(rp.nodes + rank2idx[i], load_node(&s_nodes[i]));
+}
+
+// ---------------------------------------------------------------------------
+// Initial keys.  k_hinit_gk: per (launch replica, group, distinct initial node state) the group's
+// best (score, GPU) on that state -- memo_key_scalar's evaluation without the Filter and the rank.
+// k_hinit_keys: per (launch replica, class, rank) the key = Filter ? that with the rank : 0, the
+// feasible counts and the L1 maxima (one wave = one block of 64 ranks).
+// ---------------------------------------------------------------------------
+struct HInitArgs {
+  ReplicaDev* reps;
+  const int* rep_list;
+  int N, Npad, nb, Cmax, Gmax, Smax;
+  const int* cg;           // [Rg][2]
+  const PodDev* cls;       // [Rg][Cmax]
+  const uint16_t* cgrp;    // [Rg][Cmax]
+  const PodDev* gpod;      // [Rg][Gmax]
+  const NodeRec* st;       // [Rg][Smax] distinct initial node states
+  const int* ns;           // [Rg] distinct states
+  const int* nstate;       // [Rg][Npad] state of each rank (-1 padding)
+  unsigned* gsc;           // [Rg][Gmax][Smax] hkey(score, 0, gf) without the rank field
+  unsigned* keys;          // [Rg][Cmax][Npad]
+  unsigned* l1;            // [Rg][Cmax][nb]
+  int* cnt;                // [Rg][Cmax], zeroed before k_hinit_keys
+  const double* th;
+};
+
+__global__ __launch_bounds__(256) void k_hinit_gk(HInitArgs a, const TypDev* __restrict__ tp_all) {
+  const int gi = (int)blockIdx.z, g = (int)blockIdx.y;
+  const int s = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g >= a.cg[2 * gi + 1] || s >= a.ns[gi]) return;
+  const int r = a.rep_list[gi];
+  const ReplicaDev& rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
+  const NodeV n = load_node(a.st + (size_t)gi * a.Smax + s);
+  const PodDev p = a.gpod[(size_t)gi * a.Gmax + g];
+  const double F0 = eval_fgd_item(n, 0, PodDev{}, rp, tp);
+  unsigned k;
+  if (!is_share_pod(p)) {
+    k = hkey_norank(fgd_score_lookup(F0 - eval_fgd_item(n, 9, p, rp, tp), a.th), 0);  // fgd_score.go:137-141
+  } else {
+    k = hkey_norank(0, 0);
+    const unsigned fm = first_of_class(n, p.milli);
+    for (int x = 0; x < kMaxGpu; ++x) {
+      if ((fm >> x) & 1u) {  // fgd_score.go:111-118
+        const unsigned c = hkey_norank(fgd_score_lookup(F0 - eval_fgd_item(n, 1 + x, p, rp, tp), a.th), 15 - x);
+        k = c > k ? c : k;
+      }
+    }
+  }
+  a.gsc[((size_t)gi * a.Gmax + g) * a.Smax + s] = k;
+}
+
+__global__ __launch_bounds__(256) void k_hinit_keys(HInitArgs a) {
+  const int gi = (int)blockIdx.z, c = (int)blockIdx.y;
+  const int rank = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (c >= a.cg[2 * gi] || rank >= a.Npad) return;  // uniform per workgroup (Npad % 256 == 0 not required: waves stay whole)
+  const int s = a.nstate[(size_t)gi * a.Npad + rank];
+  unsigned k = 0u;
+  if (s >= 0) {
+    const NodeV n = load_node(a.st + (size_t)gi * a.Smax + s);
+    const PodDev q = a.cls[(size_t)gi * a.Cmax + c];
+    if (filter_node(n, q)) {
+      const int g = a.cgrp[(size_t)gi * a.Cmax + c];
+      k = a.gsc[((size_t)gi * a.Gmax + g) * a.Smax + s] | hkey_rankbits(rank);
+    }
+  }
+  a.keys[((size_t)gi * a.Cmax + c) * a.Npad + rank] = k;
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned long long fb = __ballot(k != 0u);
+  const unsigned m = (unsigned)ksim_replay::wave_max_dpp((int)k);
+  if (lane == 0) {
+    a.l1[((size_t)gi * a.Cmax + c) * a.nb + rank / kFan] = m;
+    if (fb) atomicAdd(&a.cnt[(size_t)gi * a.Cmax + c], (int)__popcll(fb));
+  }
+}
+
+}  // namespace ksim_hmemo

@@ -329,7 +329,8 @@ class Engine:
 
     def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0, wgs_per_replica=0,
                  run_mode=0):
-        """run_mode 0: persistent k_replay (default); 1: one k_step launch per pod step (hipGraph)."""
+        """run_mode (ksim_config.run_mode): 0 auto (FGD: k_memo, else k_hmemo, else k_replay), 1 k_step per
+        pod (hipGraph), 2 k_replay only, 3 k_memo required, 4 k_memo decider mode, 5 k_hmemo required."""
         self.N, self.R = n_nodes, n_replicas
         cfg = Config(device, nodes_per_block, steps_per_graph, wgs_per_replica, run_mode)
         h = _VP()
@@ -441,10 +442,11 @@ class Engine:
         return s.value
 
     def last_run_path(self):
-        """'k_replay' | 'k_memo' | 'k_memo+k_replay' | 'k_step' | 'sharded': the kernels the last run() used."""
+        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo': the kernels the last run()
+        used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
-        return ["k_replay", "k_memo", "k_memo+k_replay", "k_step", "sharded"][k.value]
+        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)

@@ -1,6 +1,6 @@
 """Parity fuzz on adversarial synthetic clusters (tests/fuzz_cases.py): every policy through every
 execution path -- auto (k_memo for FGD, k_replay for the rest), k_replay forced, k_step per pod
-(hipGraph), k_memo forced for FGD -- bit-exact against the oracle per event (node, GPU set, score,
+(hipGraph), k_hmemo forced for FGD (run_mode 5), k_memo forced for FGD -- bit-exact against the oracle per event (node, GPU set, score,
 feasible count, status) and in the final cluster state.  Every test needs a gfx950 device.
 """
 import pytest
@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 # (seed, nodes, creations, delete probability)
 CASES = [(1, 40, 500, 0.0), (2, 97, 900, 0.25), (3, 250, 1200, 0.1), (4, 7, 300, 0.4), (5, 1, 60, 0.3),
          (6, 600, 2000, 0.0)]
-PATHS = [(0, "auto"), (2, "replay"), (1, "step")]
+PATHS = [(0, "auto"), (2, "replay"), (1, "step"), (5, "hmemo")]
 
 
 def run_engine(case, policy, run_mode, seed=5, wgs=0):
@@ -64,7 +64,9 @@ def test_fuzz_memo_forced_fgd(case):
                                        gpu_sel=O.SEL_FGD, threads=16)
     try:
         got, state = run_engine(case, "FGD", 3)
-    except ksim.KsimError:
+    except ksim.KsimError as e:
+        if e.code != ksim.KSIM_ENOTSUP:
+            raise
         pytest.skip("k_memo does not fit this case")
     assert got == want
     check_state(state, want_state)

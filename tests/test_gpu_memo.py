@@ -1,4 +1,5 @@
-"""GPU parity of the memoised FGD replay (k_memo, run_mode 3) against the oracle and against the
+"""GPU parity of the memoised FGD replays -- k_memo (run_mode 3, keys in LDS over K workgroups) and
+k_hmemo (run_mode 5, keys in HBM, one workgroup per replica) -- against the oracle and against the
 scanning replay (k_replay, run_mode 2).
 
 k_memo keeps the key of every (pod class, node) pair and recomputes only the node the previous
@@ -15,8 +16,8 @@ from test_gpu_parity import assert_same, engine_run, oracle_run
 
 pytestmark = pytest.mark.gpu
 
-MEMO, SCAN, DECIDER = 3, 2, 4
-MODES = pytest.mark.parametrize("mode", [MEMO, DECIDER], ids=["memo", "decider"])
+MEMO, SCAN, DECIDER, HMEMO = 3, 2, 4, 5
+MODES = pytest.mark.parametrize("mode", [MEMO, DECIDER, HMEMO], ids=["memo", "decider", "hmemo"])
 
 
 @pytest.fixture(scope="module")
@@ -59,7 +60,7 @@ def test_memo_other_traces(trace_name, mode):
     assert_same(res, want, state, want_state, keep)
 
 
-@pytest.mark.parametrize("memo_mode", [MEMO, DECIDER], ids=["memo", "decider"])
+@pytest.mark.parametrize("memo_mode", [MEMO, DECIDER, HMEMO], ids=["memo", "decider", "hmemo"])
 def test_memo_ten_replicas_ragged(default_trace, memo_mode):
     # the C2 layout (10 seeds, one engine) with ragged stream lengths: memo == k_replay
     arr, n = default_trace.typical()
@@ -74,7 +75,9 @@ def test_memo_ten_replicas_ragged(default_trace, memo_mode):
             eng.load_events(r, rp.events, rp.n - 97 * r)
         eng.run()
         outs[mode] = [eng.results(r) for r in range(10)]
-        if mode == memo_mode:
+        if mode == memo_mode == HMEMO:
+            assert eng.last_run_wgs() == 1 and eng.last_run_path() == "k_hmemo"
+        elif mode == memo_mode:
             assert eng.last_run_wgs() >= 8 and eng.last_run_path() == "k_memo"
         eng.close()
     for r in range(10):
@@ -158,3 +161,43 @@ def test_memo_not_applicable_is_loud(default_trace):
     keep = list(range(0, default_trace.num_nodes, 3))
     with pytest.raises(ksim.KsimError):
         engine_run(default_trace, rp, keep, rp.n, "FGD", run_mode=MEMO, wgs=1)
+
+
+def test_hmemo_when_kmemo_does_not_fit(default_trace):
+    # two workgroups per replica cannot hold 151 classes x 1213 nodes of keys in LDS, so k_memo does
+    # not fit; auto mode takes k_hmemo (one workgroup per replica), bit-exact with k_replay
+    arr, n = default_trace.typical()
+    R = 30
+    outs = {}
+    for mode in (0, SCAN):
+        eng = ksim.Engine(default_trace.num_nodes, R, run_mode=mode, wgs_per_replica=2 if mode == 0 else 0)
+        for r in range(R):
+            rp = default_trace.replay(seed=100 + r)
+            eng.set_nodes(r, rp.nodes)
+            eng.set_typical(r, arr, n)
+            eng.set_policy(r, "FGD")
+            eng.load_events(r, rp.events, 600 + 7 * r)
+        eng.run()
+        if mode == 0:
+            assert eng.last_run_path() == "k_hmemo"
+        outs[mode] = [eng.results(r) for r in range(R)]
+        eng.close()
+    assert outs[0] == outs[SCAN]
+
+
+def test_hmemo_cluster_report(default_trace):
+    # the per-event report from k_hmemo's snapshots equals k_replay's (exact fixed-point sums)
+    rp = default_trace.replay(seed=47)
+    arr, n = default_trace.typical()
+    reps = {}
+    for mode in (HMEMO, SCAN):
+        eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=mode)
+        eng.set_nodes(0, rp.nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        eng.set_report(True)
+        eng.load_events(0, rp.events, 4000)
+        eng.run()
+        reps[mode] = (eng.results(0), eng.reports(0))
+        eng.close()
+    assert reps[HMEMO] == reps[SCAN]
