@@ -1107,7 +1107,16 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
   NodeRec* nr = rp.nodes + node;
   uint16_t* tg = rp.tags + (size_t)node * kTagStride;
   if (sign < 0) {
-    if (tid == 0) apply_bind(nr, tg, p, mask_in, -1);
+    // removePod (cache.go:96-111): every released device gets its milli back without exceeding the
+    // device (left + milli <= 1000, the invariant of the packed u16 lanes); else nothing changes
+    if (tid == 0) {
+      const NodeV n = load_node(nr);
+      bool ok = n.pods_left() < 32767;
+      for (int g = 0; g < kMaxGpu; ++g)
+        if ((mask_in >> g) & 1) ok = ok && g < n.gpu_cnt() && n.gl(g) + (int)p.milli <= kMilli;
+      if (ok) apply_bind(nr, tg, p, mask_in, -1);
+      *out_mask = ok ? mask_in : -1;
+    }
     return;
   }
   const NodeV n = load_node(nr);
@@ -1303,22 +1312,48 @@ static int upload_reps(ksim_engine* e) {
   return KSIM_OK;
 }
 
-template <int P, bool G>
-static void launch_replay_g(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp) {
-  if (ra.K <= 64) {
-    (void)hipFuncSetAttribute((const void*)k_replay<P, 1, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_replay<P, 1, G>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
-  } else {
-    (void)hipFuncSetAttribute((const void*)k_replay<P, 4, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((k_replay<P, 4, G>), dim3(grid), dim3(ksim_replay::kRBlock), lds, st, ra, tp);
+// Workgroups of kernel `f` (1024 threads, `lds` B of dynamic LDS) that can be resident at once on the
+// CUs the engine may use: the occupancy query times the CU count.  A persistent grid whose workgroups
+// exchange granules (K > 1) must not exceed it.
+static int resident_cap(const ksim_engine* e, const void* f, size_t lds);
+
+// A persistent launch: K > 1 workgroups per replica poll each other's granules every step, so the
+// whole grid must be resident -- a cooperative launch, which the runtime refuses up front
+// (hipErrorCooperativeLaunchTooLarge) instead of letting a non-resident workgroup stall the pollers.
+// K = 1 needs no co-residency: a plain launch (it may share the device with side-stream groups).
+template <typename A>
+static int launch_persistent(const void* f, int grid, int block, size_t lds, hipStream_t st, bool coop, A& args,
+                             const TypDev*& tp) {
+  KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* params[] = {(void*)&args, (void*)&tp};
+  const hipError_t r = coop ? hipLaunchCooperativeKernel(f, dim3(grid), dim3(block), params, (unsigned)lds, st)
+                            : hipLaunchKernel(f, dim3(grid), dim3(block), params, lds, st);
+  if (r == hipErrorCooperativeLaunchTooLarge) {
+    std::fprintf(stderr, "ksim: %d co-resident workgroups of %zu B LDS do not fit the device\n", grid, lds);
+    (void)hipGetLastError();
+    return KSIM_ERANGE;
   }
+  KSIM_HIP(r);
+  return KSIM_OK;
 }
-// general: profile timers, report stores or delete events needed; else the lean instantiation
+
+template <int P, bool G>
+static const void* replay_fn(int K) {
+  return K <= 64 ? (const void*)k_replay<P, 1, G> : (const void*)k_replay<P, 4, G>;
+}
 template <int P>
-static void launch_replay(int grid, size_t lds, hipStream_t st, const ksim_replay::ReplayArgs& ra, const TypDev* tp,
-                          bool general) {
-  if (general) launch_replay_g<P, true>(grid, lds, st, ra, tp);
-  else launch_replay_g<P, false>(grid, lds, st, ra, tp);
+static const void* replay_fn(int K, bool general) {
+  return general ? replay_fn<P, true>(K) : replay_fn<P, false>(K);
+}
+static const void* replay_kernel(int pol, int K, bool general) {
+  switch (pol) {
+    case POL_FGD: return replay_fn<POL_FGD>(K, general);
+    case POL_BESTFIT: return replay_fn<POL_BESTFIT>(K, general);
+    case POL_DOTPROD: return replay_fn<POL_DOTPROD>(K, general);
+    case POL_PACKING: return replay_fn<POL_PACKING>(K, general);
+    case POL_CLUSTERING: return replay_fn<POL_CLUSTERING>(K, general);
+    default: return replay_fn<POL_RANDOM>(K, general);
+  }
 }
 
 // ---- k_memo planning (memoised FGD replay, ksim_memo.hpp) ----
@@ -1394,6 +1429,9 @@ static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPl
     if (Cw <= kMaxCw)
       for (int f : {16, 12})  // waves 1..9 need fold buffers on the critical path
         if (memo_lds(e->N, Cw, f) <= 160 * 1024) { nfw = f; break; }
+    // every workgroup of the launch must be resident (they exchange granules every step)
+    if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, (const void*)ksim_memo::k_memo<false, false>, memo_lds(e->N, Cw, nfw)))
+      return false;
     if (nfw > 0) {
       pl.K = K;
       pl.Cw = Cw;
@@ -1696,25 +1734,14 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
     ma.prof = e->d_prof;
   }
-  if (pl.decider) {
-    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)pl.lds));
-    hipLaunchKernelGGL((ksim_memo::k_memo<true, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
-                       (const TypDev*)e->d_tp);
-  } else if (profile || tracing || e->report || !e->d_th ||
-             std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; })) {
-    // the general instantiation
-    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)pl.lds));
-    hipLaunchKernelGGL((ksim_memo::k_memo<false, true>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
-                       (const TypDev*)e->d_tp);
-  } else {
-    KSIM_HIP(hipFuncSetAttribute((const void*)ksim_memo::k_memo<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)pl.lds));
-    hipLaunchKernelGGL((ksim_memo::k_memo<false, false>), dim3(Rg * pl.K), dim3(ksim_memo::kMBlock), pl.lds, st, ma,
-                       (const TypDev*)e->d_tp);
-  }
-  KSIM_HIP(hipGetLastError());
+  // the general instantiation for the profile / trace / report / deletes / no score table, else the lean one
+  const bool general = profile || tracing || e->report || !e->d_th ||
+                       std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; });
+  const void* f = pl.decider ? (const void*)ksim_memo::k_memo<true, true>
+                             : (general ? (const void*)ksim_memo::k_memo<false, true> : (const void*)ksim_memo::k_memo<false, false>);
+  const TypDev* tpp = e->d_tp;
+  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, pl.K > 1, ma, tpp);
+  if (rc) return rc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
   KSIM_HIP(hipGetLastError());
@@ -1951,6 +1978,9 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     hipDeviceProp_t prop;
     KSIM_HIP(hipGetDeviceProperties(&prop, dev));
     e->cus = prop.multiProcessorCount;
+    // KSIM_CUS: use at most this many CUs for co-resident persistent grids (a device shared with
+    // another process; also the tests' way to exercise the residency checks)
+    if (const char* c = std::getenv("KSIM_CUS")) e->cus = std::max(1, std::min(e->cus, std::atoi(c)));
   }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
@@ -2331,22 +2361,37 @@ int ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int 
   PodDev p;
   int rc = to_pod_dev(*pod, &p);
   if (rc) return rc;
+  if (p.flags & kPodDelete) return KSIM_EINVAL;
+  // the devices a Reserve of this pod can have assigned on this node (open_gpu_share.go:242-283): none
+  // for a pod without GPU milli, else `num` devices the node has
+  if (e->h_nodes[replica].size() != (size_t)e->N) return KSIM_ESTATE;
+  const int cnt = e->h_nodes[replica][node].gpu_count;
+  if (gpu_mask < 0 || gpu_mask >= (1 << cnt)) return KSIM_EINVAL;
+  if ((p.milli == 0) != (gpu_mask == 0)) return KSIM_EINVAL;
+  if (p.milli > 0 && __builtin_popcount((unsigned)gpu_mask) != p.num) return KSIM_EINVAL;
   KSIM_HIP(hipSetDevice(e->device));
   hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, 0, e->d_scratch, -1,
                      (int)gpu_mask);
   KSIM_HIP(hipGetLastError());
+  int m = 0;
+  KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
   KSIM_HIP(hipStreamSynchronize(e->stream));
-  return KSIM_OK;
+  return m < 0 ? KSIM_ESTATE : KSIM_OK;  // the node does not hold what the pod would release
 }
 
 int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events, int n) {
   if (e) e->mplan_dirty = true;
   if (!e || replica < 0 || replica >= e->R || n < 0 || (n > 0 && !events)) return KSIM_EINVAL;
   std::vector<PodDev> h(n);
+  std::vector<char> gone(std::max(n, 1), 0);  // creations already deleted (the reference deletes a pod once)
   for (int i = 0; i < n; ++i) {
     int rc = to_pod_dev(events[i], &h[i]);
     if (rc) return rc;
-    if ((h[i].flags & kPodDelete) && (h[i].ref < 0 || h[i].ref >= i)) return KSIM_EINVAL;
+    if (h[i].flags & kPodDelete) {
+      const int ref = h[i].ref;
+      if (ref < 0 || ref >= i || (h[ref].flags & kPodDelete) || gone[ref]) return KSIM_EINVAL;
+      gone[ref] = 1;
+    }
   }
   // pod classes for k_memo: the distinct Filter + Score requests of the creation events
   {
@@ -2611,6 +2656,16 @@ static int choose_wgs(const ksim_engine* e, int R) {
   return K;
 }
 
+static int resident_cap(const ksim_engine* e, const void* f, size_t lds) {
+  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 1024, lds) != hipSuccess) {
+    (void)hipGetLastError();
+    nb = 0;
+  }
+  return nb * e->cus;
+}
+
 static size_t replay_lds(int S) {  // S real slots + the virtual node
   return sizeof(ksim_replay::ReplayShared) +
          (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double) + sizeof(int));
@@ -2704,6 +2759,20 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       S = (e->N + K - 1) / K;
     }
     if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
+    const bool general = profile || e->report || any_delete;
+    if (K > 1) {
+      // the occupancy query bounds the co-resident grid: fewer, larger slices when it is short
+      const int cap = resident_cap(e, replay_kernel(gp.first, K, general), replay_lds(S));
+      if (Rg * K > cap) {
+        if (e->wgs_req > 0 && cap < Rg) return KSIM_ERANGE;
+        K = std::max(1, std::min(K, cap / Rg));
+        S = (e->N + K - 1) / K;
+        if (replay_lds(S) > 160 * 1024) {
+          std::fprintf(stderr, "ksim: k_replay needs %d co-resident workgroups; the device holds %d\n", Rg * K, cap);
+          return KSIM_ERANGE;
+        }
+      }
+    }
     const size_t need = any_delete ? (size_t)e->R * K * std::max(max_ev, 1) : 0;
     if (need > e->hist_cap) {
       if (e->d_hist) KSIM_HIP(hipFree(e->d_hist));
@@ -2738,16 +2807,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                               e->stream));
     const int grid = Rg * K;
     const TypDev* tp = e->d_tp;
-    const bool general = profile || e->report || any_delete;
-    switch (gp.first) {
-      case POL_FGD: launch_replay<POL_FGD>(grid, lds, gs, ra, tp, general); break;
-      case POL_BESTFIT: launch_replay<POL_BESTFIT>(grid, lds, gs, ra, tp, general); break;
-      case POL_DOTPROD: launch_replay<POL_DOTPROD>(grid, lds, gs, ra, tp, general); break;
-      case POL_PACKING: launch_replay<POL_PACKING>(grid, lds, gs, ra, tp, general); break;
-      case POL_CLUSTERING: launch_replay<POL_CLUSTERING>(grid, lds, gs, ra, tp, general); break;
-      default: launch_replay<POL_RANDOM>(grid, lds, gs, ra, tp, general); break;
-    }
-    KSIM_HIP(hipGetLastError());
+    const int lrc = launch_persistent(replay_kernel(gp.first, K, general), grid, ksim_replay::kRBlock, lds, gs, K > 1, ra, tp);
+    if (lrc) return lrc;
     e->last_K = K;
     e->last_groups = (int)groups.size();
     first += Rg;

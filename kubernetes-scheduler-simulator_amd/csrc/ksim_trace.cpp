@@ -187,6 +187,7 @@ int ksim_trace_load_openb(const char* node_csv, const char* pod_csv, ksim_trace*
     while (std::getline(f, line)) {
       if (line.empty() || line == "\r") continue;
       auto v = split_csv_line(line);
+      if (c_sn >= (int)v.size() || c_cpu >= (int)v.size() || c_gpu >= (int)v.size()) { delete t; return KSIM_EIO; }
       Node n;
       n.name = v[c_sn];
       int64_t x = 0;
@@ -212,6 +213,7 @@ int ksim_trace_load_openb(const char* node_csv, const char* pod_csv, ksim_trace*
     while (std::getline(f, line)) {
       if (line.empty() || line == "\r") continue;
       auto v = split_csv_line(line);
+      if (c_name >= (int)v.size() || c_cpu >= (int)v.size() || c_num >= (int)v.size()) { delete t; return KSIM_EIO; }
       Pod p;
       p.name = v[c_name];
       int64_t x = 0;
@@ -381,11 +383,20 @@ int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod*
     rng.Shuffle(np, [&](int64_t i, int64_t j) { std::swap(order[i], order[j]); });
   }
   // TunePodsByNodeTotalResource (simulator.go:1201-1248)
-  int64_t pod_total = 0, node_total = 0;
-  for (int i = 0; i < np; ++i) pod_total += (int64_t)t->pods[i].gpu_milli * t->pods[i].gpu_count;
-  for (auto& n : t->nodes) node_total += (int64_t)n.gpu * 1000;
+  int64_t pod_total = 0, node_total = 0, pod_cpu = 0, node_cpu = 0;
+  for (int i = 0; i < np; ++i) {
+    pod_total += (int64_t)t->pods[i].gpu_milli * t->pods[i].gpu_count;
+    pod_cpu += t->pods[i].cpu;
+  }
+  for (auto& n : t->nodes) {
+    node_total += (int64_t)n.gpu * 1000;
+    node_cpu += n.cpu;
+  }
   std::vector<int> ev = order;
   const double ratio = cfg->tune_ratio;
+  // simulator.go:1203-1211: the reference panics when the workload or the cluster has no CPU or no GPU
+  // to tune against (tuneUpPods would never stop, Intn(0) would panic)
+  if (ratio > 0 && (np == 0 || pod_cpu <= 0 || pod_total <= 0 || node_cpu <= 0 || node_total <= 0)) return KSIM_EINVAL;
   if (ratio > 0) {
     const double target = ratio * (double)node_total;
     if ((double)pod_total > target) {

@@ -66,7 +66,8 @@ class Sweep:
         parts = [rest, pwr]
         if fgd_batch > 0:  # FGD experiments as separate engines of fgd_batch replicas (k_memo where they fit)
             fgd = [i for i in rest if self.exps[i][1] == "06-FGD"]
-            parts = [[i for i in rest if i not in set(fgd)], pwr] + \
+            fgd_set = set(fgd)
+            parts = [[i for i in rest if i not in fgd_set], pwr] + \
                 [fgd[k:k + fgd_batch] for k in range(0, len(fgd), fgd_batch)]
         for idx in parts:
             if not idx:

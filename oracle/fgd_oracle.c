@@ -61,8 +61,161 @@ double orc_go_exp(double x) {
     return go_ldexp_small(y, k);
 }
 
-/* plugin_utils.go:76-78 */
-double orc_sigmoid(double x) { return 1.0 / (1.0 + orc_go_exp(-x)); }
+/* plugin_utils.go:76-78.  g_exp_nudge != 0 (census runs only) moves exp's result by that many ulps:
+ * a stand-in for a different math.Exp (Go's amd64 assembly) within a few ulps of the portable one. */
+static int g_exp_nudge = 0;
+static double nudge_ulps(double e, int j) {
+    for (; j > 0; --j) e = nextafter(e, HUGE_VAL);
+    for (; j < 0; ++j) e = nextafter(e, -HUGE_VAL);
+    return e;
+}
+static int g_exp_mode = 0;  /* 0: the portable algorithm; 1: exp in x87 extended precision rounded to double */
+static double exp_cr(double x) { return (double)expl((long double)x); }
+static double census_exp(double x) {
+    const double e = g_exp_mode ? exp_cr(x) : orc_go_exp(x);
+    return g_exp_nudge ? nudge_ulps(e, g_exp_nudge) : e;
+}
+double orc_sigmoid(double x) {
+    return 1.0 / (1.0 + ((g_exp_nudge | g_exp_mode) ? census_exp(-x) : orc_go_exp(-x)));
+}
+void orc_set_exp_nudge(int ulps) { g_exp_nudge = ulps; }
+void orc_set_exp_mode(int mode) { g_exp_mode = mode; }
+
+/* ------------------------------------------------------------------ */
+/* math.Exp census (tests/golden/make_exp_census.py).     */
+/* fgd_score.go:123,144 score = int64(sigmoid((cur-new)/1000)*100) is a */
+/* step function of delta = cur - new: score >= k iff delta >= th[k].   */
+/* A different exp (Go's amd64 assembly) moves each th[k] by about      */
+/* 1000 * 2^-52 per ulp of exp; the census records how close any delta  */
+/* the path evaluates comes to any th[k].                               */
+/* ------------------------------------------------------------------ */
+static int score_of_delta(double delta) { return (int)(int64_t)(orc_sigmoid(delta / 1000) * (double)100); }
+static long long ord_key(double d) {
+    long long b;
+    memcpy(&b, &d, 8);
+    return b >= 0 ? b : (long long)(0x8000000000000000ULL - (unsigned long long)b);
+}
+static double ord_dbl(long long k) {
+    long long b = k >= 0 ? k : (long long)(0x8000000000000000ULL - (unsigned long long)k);
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+int orc_score_thresholds(double* th) {
+    th[0] = -HUGE_VAL;
+    th[101] = HUGE_VAL;
+    if (score_of_delta(-1.0e9) != 0 || score_of_delta(1.0e9) != 100) return -1;
+    for (int k = 1; k <= 100; k++) {
+        long long lo = ord_key(-1.0e9), hi = ord_key(1.0e9); /* score(lo) < k <= score(hi) */
+        while ((unsigned long long)hi - (unsigned long long)lo > 1ULL) {
+            long long mid = (long long)((unsigned long long)lo + ((unsigned long long)hi - (unsigned long long)lo) / 2);
+            if (score_of_delta(ord_dbl(mid)) >= k) hi = mid;
+            else lo = mid;
+        }
+        th[k] = ord_dbl(hi);
+        if (k > 1 && !(th[k] > th[k - 1])) return -1;
+    }
+    return 0;
+}
+static double g_th[102];
+#define ORC_CENSUS_NEAR 1.0e-10  /* > 400 x the step shift of one exp ulp (1000 * 2^-52) */
+#define ORC_CENSUS_KEEP 16
+static long long g_census_near, g_census_sens, g_census_crdiff, g_census_nkept;
+static double g_census_sens_max;  /* largest |delta| whose score a one-ulp move of exp changes */
+static orc_census_case g_census_cases[ORC_CENSUS_KEEP];       /* portable != correctly rounded */
+static orc_census_case g_census_sens_cases[ORC_CENSUS_KEEP];  /* a one-ulp move of exp changes the score */
+static int g_census_on = 0;
+static pthread_mutex_t g_census_mu = PTHREAD_MUTEX_INITIALIZER;
+static double g_census_min;
+static double g_census_delta;
+static int g_census_step, g_census_node, g_census_k;
+static long long g_census_n;
+static int g_census_cur_step = -1;
+static __thread int tl_census_node = -1;
+
+int orc_census_begin(void) {
+    if (orc_score_thresholds(g_th)) return -1;
+    g_census_min = HUGE_VAL;
+    g_census_delta = 0;
+    g_census_step = g_census_node = g_census_k = -1;
+    g_census_n = 0;
+    g_census_near = g_census_sens = g_census_crdiff = g_census_nkept = 0;
+    g_census_sens_max = 0;
+    memset(g_census_cases, 0, sizeof g_census_cases);
+    memset(g_census_sens_cases, 0, sizeof g_census_sens_cases);
+    g_census_on = 1;
+    return 0;
+}
+void orc_census_near(long long* near, long long* crdiff, long long* sensitive, double* sens_max,
+                     orc_census_case* cr_cases, orc_census_case* sens_cases) {
+    *near = g_census_near;
+    *crdiff = g_census_crdiff;
+    *sensitive = g_census_sens;
+    if (sens_max) *sens_max = g_census_sens_max;
+    memcpy(cr_cases, g_census_cases, sizeof g_census_cases);
+    memcpy(sens_cases, g_census_sens_cases, sizeof g_census_sens_cases);
+}
+void orc_census_end(double* min_dist, double* delta_at, int* step_at, int* node_at, int* k_at, long long* n,
+                    double* th) {
+    g_census_on = 0;
+    *min_dist = g_census_min;
+    *delta_at = g_census_delta;
+    *step_at = g_census_step;
+    *node_at = g_census_node;
+    *k_at = g_census_k;
+    *n = g_census_n;
+    if (th) memcpy(th, g_th, sizeof g_th);
+}
+static void census(double delta) {
+    if (!g_census_on) return;
+    const int s = score_of_delta(delta);
+    const double dlo = delta - g_th[s], dhi = g_th[s + 1] - delta;
+    const double d = dlo < dhi ? dlo : dhi;
+    __atomic_add_fetch(&g_census_n, 1, __ATOMIC_RELAXED);
+    if (d < ORC_CENSUS_NEAR) {
+        /* near a step: is the score the one a correctly rounded exp gives (ulps = 0 in the record),
+         * and does it survive exp's result moving by one ulp either way (ulps = -1 / +1)? */
+        __atomic_add_fetch(&g_census_near, 1, __ATOMIC_RELAXED);
+        const double x = -(delta / 1000);
+        const double e = orc_go_exp(x), ecr = exp_cr(x);
+        int j = 0, sj = (int)(int64_t)((1.0 / (1.0 + ecr)) * (double)100);
+        if (sj == s) {
+            for (j = -1; j <= 1; j += 2) {
+                sj = (int)(int64_t)((1.0 / (1.0 + nudge_ulps(e, j))) * (double)100);
+                if (sj != s) break;
+            }
+        }
+        if (sj != s) {
+            const long long i = __atomic_fetch_add(j == 0 ? &g_census_crdiff : &g_census_sens, 1, __ATOMIC_RELAXED);
+            if (j == 0 && i < ORC_CENSUS_KEEP) {
+                orc_census_case c = {delta, g_census_cur_step, tl_census_node, s, sj, j};
+                g_census_cases[i] = c;
+            } else if (j != 0) {
+                pthread_mutex_lock(&g_census_mu);
+                if (fabs(delta) > g_census_sens_max) g_census_sens_max = fabs(delta);
+                pthread_mutex_unlock(&g_census_mu);
+                const long long k = __atomic_fetch_add(&g_census_nkept, 1, __ATOMIC_RELAXED);
+                if (k < ORC_CENSUS_KEEP) {
+                    orc_census_case c = {delta, g_census_cur_step, tl_census_node, s, sj, j};
+                    g_census_sens_cases[k] = c;
+                }
+            }
+        }
+    }
+    double cur;
+    __atomic_load(&g_census_min, &cur, __ATOMIC_RELAXED);
+    if (d < cur) {
+        pthread_mutex_lock(&g_census_mu);
+        if (d < g_census_min) {
+            __atomic_store(&g_census_min, &d, __ATOMIC_RELAXED);
+            g_census_delta = delta;
+            g_census_step = g_census_cur_step;
+            g_census_node = tl_census_node;
+            g_census_k = dlo < dhi ? s : s + 1;
+        }
+        pthread_mutex_unlock(&g_census_mu);
+    }
+}
 
 /* ------------------------------------------------------------------ */
 /* utils.go:957-1006 IsNodeAccessibleToPodByType                        */
@@ -286,6 +439,7 @@ int64_t orc_fgd_score(const orc_node_resource* n, const orc_pod_resource* p, con
                 c.milli_cpu_left -= p->milli_cpu;
                 c.milli_gpu_left[i] -= p->milli_gpu;
                 double nw = orc_node_gpu_share_frag_amount_score(&c, tp, nt);
+                census(cur - nw);
                 int64_t fs = (int64_t)(orc_sigmoid((cur - nw) / 1000) * (double)100);
                 if (gid == -1 || fs > score) {
                     score = fs;
@@ -299,6 +453,7 @@ int64_t orc_fgd_score(const orc_node_resource* n, const orc_pod_resource* p, con
     orc_node_resource c;
     (void)orc_node_sub(n, p, &c); /* error ignored, as in the reference */
     double nw = orc_node_gpu_share_frag_amount_score(&c, tp, nt);
+    census(cur - nw);
     int64_t fs = (int64_t)(orc_sigmoid((cur - nw) / 1000) * (double)100);
     if (gpu_mask) {
         /* AllocateExclusiveGpuId; for CPU-only pods it returns "" (req = 0) */
@@ -720,6 +875,7 @@ static int64_t score_one(const work_t* w, int i, int32_t* gm, int32_t* err) {
          * fgd_score.go:74-77: inaccessible -> error */
         if (!accessible) { *err = 1; return 0; }
         int m = 0;
+        tl_census_node = i;
         int64_t s = orc_fgd_score(&nr, &pr, w->tp, w->nt, &m);
         *gm = m;
         return s;
@@ -798,6 +954,19 @@ static int cmp_name_idx(const void* a, const void* b) {
 int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_target_pod* tp, int nt,
                          orc_policy pol, const orc_event* ev, int n_ev, orc_result* res, orc_report* rep,
                          orc_node_state* final_state) {
+    /* A deletion names an earlier creation, at most once (the reference deletes a pod once). */
+    {
+        uint8_t* gone = (uint8_t*)calloc((size_t)(n_ev > 0 ? n_ev : 1), 1);
+        int bad = 0;
+        for (int s = 0; s < n_ev && !bad; s++) {
+            if (!ev[s].is_delete) continue;
+            const int ref = ev[s].ref;
+            bad = ref < 0 || ref >= s || ev[ref].is_delete || gone[ref];
+            if (!bad) gone[ref] = 1;
+        }
+        free(gone);
+        if (bad) return -1;
+    }
     node_dyn* dyn = (node_dyn*)calloc((size_t)n_nodes, sizeof(node_dyn));
     uint8_t* feas = (uint8_t*)calloc((size_t)n_nodes, 1);
     int64_t* raw = (int64_t*)calloc((size_t)n_nodes, sizeof(int64_t));
@@ -821,6 +990,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
         orc_result* R = &res[s];
         memset(R, 0, sizeof *R);
         R->node = -1;
+        g_census_cur_step = s;
         if (e->is_delete) {
             /* simulator.go:416-422 deletePod -> informer DeleteFunc -> removePod */
             int ref = e->ref;

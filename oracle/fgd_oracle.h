@@ -87,6 +87,25 @@ double  orc_node_gpu_share_frag_amount_score(const orc_node_resource* n, const o
 /* ---- Go math restated ---- */
 double  orc_go_exp(double x);          /* Go src/math/exp.go (portable algorithm) */
 double  orc_sigmoid(double x);         /* plugin_utils.go:76-78 */
+/* The FGD score as a step function of delta = cur - new: th[k] = smallest delta with score >= k
+ * (th[0] = -inf, th[101] = +inf); 0, or -1 if the steps are not monotone. */
+int     orc_score_thresholds(double* th /* [102] */);
+/* math.Exp census: while on, every FGD score delta the path evaluates is compared with th[];
+ * end returns the smallest distance |delta - th[k]|, where it happened (event, node, k) and the
+ * number of deltas seen. */
+typedef struct { double delta; int event, node, score, score_nudged, ulps; } orc_census_case;
+int     orc_census_begin(void);
+/* deltas within 1e-10 of a step; of those, the ones whose score differs from the one a correctly
+ * rounded exp gives (crdiff) and, of the rest, the ones whose score changes when exp's result moves
+ * by one ulp (sensitive); the first 16 cases of each kept */
+void    orc_census_near(long long* near, long long* crdiff, long long* sensitive, double* sens_max /* max |delta| */,
+                        orc_census_case* cr_cases /* [16] */, orc_census_case* sens_cases /* [16] */);
+/* census runs only: move every exp result by `ulps` ulps; mode 1 = exp in x87 extended precision
+ * rounded to double (a stand-in for a correctly rounded exp); 0 / 0 = the portable algorithm */
+void    orc_set_exp_nudge(int ulps);
+void    orc_set_exp_mode(int mode);
+void    orc_census_end(double* min_dist, double* delta_at, int* step_at, int* node_at, int* k_at, long long* n,
+                       double* th /* [102] or NULL */);
 
 /* ---- resource.go helpers ---- */
 int     orc_node_sub(const orc_node_resource* n, const orc_pod_resource* p, orc_node_resource* out);

@@ -125,6 +125,18 @@ def lib():
         L.orc_get_typical_pods.argtypes = [P(WorkloadPod), C.c_int, TypicalCfg, P(TargetPod), C.c_int]
         L.orc_run_events_state.argtypes = [P(NodeSpec), C.c_int, P(TargetPod), C.c_int, Policy, P(Event),
                                            C.c_int, P(Result), P(Report), P(NodeState)]
+        L.orc_score_thresholds.argtypes = [P(C.c_double)]
+        L.orc_census_begin.argtypes = []
+        L.orc_census_end.argtypes = [P(C.c_double), P(C.c_double), P(C.c_int), P(C.c_int), P(C.c_int),
+                                     P(C.c_longlong), P(C.c_double)]
+        L.orc_census_end.restype = None
+        L.orc_census_near.argtypes = [P(C.c_longlong), P(C.c_longlong), P(C.c_longlong), P(C.c_double),
+                                      P(CensusCase), P(CensusCase)]
+        L.orc_census_near.restype = None
+        L.orc_set_exp_mode.argtypes = [C.c_int]
+        L.orc_set_exp_mode.restype = None
+        L.orc_set_exp_nudge.argtypes = [C.c_int]
+        L.orc_set_exp_nudge.restype = None
         L.orc_mix64.argtypes = [C.c_uint64]
         L.orc_mix64.restype = C.c_uint64
         _LIB = L
@@ -254,3 +266,50 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
                         frag_bins_exact=list(rep[i].frag_bins_exact))
                    for i in range(ne)]
     return results, state, reports
+
+
+def score_thresholds():
+    """th[k] = smallest delta with int64(sigmoid(delta/1000)*100) >= k (th[0] = -inf, th[101] = inf)."""
+    th = (C.c_double * 102)()
+    assert lib().orc_score_thresholds(th) == 0
+    return list(th)
+
+
+def census_begin():
+    """Start the math.Exp census: every FGD score delta is compared with score_thresholds()."""
+    assert lib().orc_census_begin() == 0
+
+
+class CensusCase(C.Structure):
+    _fields_ = [("delta", C.c_double), ("event", C.c_int), ("node", C.c_int), ("score", C.c_int),
+                ("score_nudged", C.c_int), ("ulps", C.c_int)]
+
+
+def set_exp_nudge(ulps):
+    """Move every math.Exp result of the oracle by `ulps` ulps (census runs; 0 restores it)."""
+    lib().orc_set_exp_nudge(ulps)
+
+
+def census_end():
+    """Stop the census: the closest approach of any delta to a score step, and where it happened."""
+    d, x = C.c_double(0), C.c_double(0)
+    st, nd, k = C.c_int(0), C.c_int(0), C.c_int(0)
+    n = C.c_longlong(0)
+    lib().orc_census_end(C.byref(d), C.byref(x), C.byref(st), C.byref(nd), C.byref(k), C.byref(n), None)
+    near, crd, sens = C.c_longlong(0), C.c_longlong(0), C.c_longlong(0)
+    cr_cases, sens_cases = (CensusCase * 16)(), (CensusCase * 16)()
+    smax = C.c_double(0)
+    lib().orc_census_near(C.byref(near), C.byref(crd), C.byref(sens), C.byref(smax), cr_cases, sens_cases)
+
+    def cases(arr, n):
+        return [dict(delta=c.delta, event=c.event, node=c.node, score=c.score, score_other=c.score_nudged,
+                     ulps=c.ulps) for c in arr[:min(16, n)]]
+    return dict(min_dist=d.value, delta=x.value, event=st.value, node=nd.value, k=k.value, deltas=n.value,
+                near=near.value, crdiff=crd.value, sensitive=sens.value, sensitive_max_abs_delta=smax.value,
+                crdiff_cases=cases(cr_cases, crd.value), sensitive_cases=cases(sens_cases, sens.value))
+
+
+def set_exp_mode(mode):
+    """0: the portable Go algorithm (the product's); 1: exp in x87 extended precision rounded to
+    double, a stand-in for a correctly rounded exp (census runs only)."""
+    lib().orc_set_exp_mode(mode)

@@ -4,6 +4,8 @@ Bar: bit-exact (node, GPU set, score, feasible count, status) for every event,
 and identical final cluster state.  Every test here needs a gfx950 device.
 """
 import numpy as np
+import ctypes
+
 import pytest
 
 import helpers
@@ -241,6 +243,55 @@ def test_reserve_unreserve_roundtrip(default_trace):
     eng.unreserve(0, share, a, m1)
     assert bytes(eng.nodes(0)) == before
     eng.close()
+
+
+def test_unreserve_rejects_what_the_node_does_not_hold(default_trace):
+    # a mask beyond the node's GPUs, a GPU count that is not the pod's, a GPU-less pod with a
+    # mask, or a device that never held the milli is refused and changes nothing
+    rp = default_trace.replay(seed=4)
+    keep = list(range(0, default_trace.num_nodes, 12))
+    arr, n = default_trace.typical()
+    nodes = helpers.subset_nodes(rp, keep)
+    eng = ksim.Engine(len(keep), 1)
+    try:
+        eng.set_nodes(0, nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        before = bytes(eng.nodes(0))
+        share = ksim.make_pod(4000, 500, 1, mem=1024)
+        whole = ksim.make_pod(8000, 1000, 2, mem=2048)
+        cpu_only = ksim.make_pod(1000)
+        two = [i for i in range(len(keep)) if nodes[i].gpu_count == 2][0]
+        for pod, mask, code in [(share, 1 << 2, ksim.KSIM_EINVAL),   # GPU 2 on a 2-GPU node
+                                (share, 0b11, ksim.KSIM_EINVAL),     # two GPUs for a share pod
+                                (whole, 0b01, ksim.KSIM_EINVAL),     # one GPU for a 2-GPU pod
+                                (cpu_only, 0b01, ksim.KSIM_EINVAL),  # a mask for a pod without GPU milli
+                                (share, -1, ksim.KSIM_EINVAL),       # Reserve's failure code
+                                (share, 0b01, ksim.KSIM_ESTATE)]:    # GPU 0 is fully free: nothing to release
+            with pytest.raises(ksim.KsimError) as ei:
+                eng.unreserve(0, pod, two, mask)
+            assert ei.value.code == code, (mask, ei.value.code)
+        assert bytes(eng.nodes(0)) == before
+    finally:
+        eng.close()
+
+
+def test_load_events_rejects_bad_deletions(default_trace):
+    # a deletion of a deletion, or a second deletion of one creation, is invalid
+    rp = default_trace.replay(seed=4)
+    eng = ksim.Engine(default_trace.num_nodes, 1)
+    try:
+        for refs in ([0, 0], [0, 1]):
+            ev = (ksim.Pod * 3)()
+            ctypes.memmove(ctypes.byref(ev[0]), ctypes.byref(rp.events[0]), ctypes.sizeof(ksim.Pod))
+            for k, ref in enumerate(refs):
+                ctypes.memmove(ctypes.byref(ev[1 + k]), ctypes.byref(rp.events[0]), ctypes.sizeof(ksim.Pod))
+                ev[1 + k].is_delete, ev[1 + k].ref = 1, ref
+            with pytest.raises(ksim.KsimError) as ei:
+                eng.load_events(0, ev, 3)
+            assert ei.value.code == ksim.KSIM_EINVAL
+    finally:
+        eng.close()
 
 
 def test_single_feasible_and_infeasible():

@@ -119,3 +119,25 @@ def test_sweep_with_pwr_runs():
         assert len(mm) == 2 and not any(mm.values())
     print("PWR sweep: %.0f ms device time; alloc at 130%%:" % dev_ms,
           {(p, s): c["alloc"][130] for (t, p, s), c in sorted(curves.items())})
+
+
+def test_sweep_fgd_batches_rows_identical():
+    # --fgd-batch: the FGD experiments as separate engines of `fgd_batch` replicas (k_memo where they fit);
+    # rows identical to expected_results, one engine per batch
+    sw = SW.Sweep(SW.plan(traces=["openb_pod_list_default"], policies=("06-FGD", "05-BestFit")), fgd_batch=3)
+    assert len(sw.groups) == 1 + 4  # BestFit; FGD seeds in batches of 3, 3, 3, 1
+    sw.run()
+    curves = sw.curves()
+    sw.close()
+    for kind, csv in (("alloc", ALLO), ("frag", FRAG)):
+        mm = SW.row_mismatches(curves, kind, SW.expected_rows(csv))
+        assert len(mm) == 20 and not any(mm.values()), kind
+
+
+def test_default_sweep_fgd_group_is_memoised():
+    # the FGD group of a sweep (10 replicas here, next to 50 others) replays memoised, not k_replay
+    sw = SW.Sweep(SW.plan(traces=["openb_pod_list_default"]))
+    sw.run()
+    path = sw.eng.last_run_path()
+    sw.close()
+    assert path == "memo+k_replay", path

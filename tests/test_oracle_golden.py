@@ -145,3 +145,15 @@ def test_report_exact_sum_is_fsum():
         assert reps[-1]["frag_bins_exact"] == exact
         for a, b in zip(reps[-1]["frag_bins"], exact):
             assert abs(a - b) <= 1e-12 * max(b, 1.0)
+
+
+def test_oracle_rejects_bad_deletions():
+    # a deletion must name an earlier creation, at most once (mirrors ksim_engine_load_events)
+    nodes = [dict(name="n0", cpu=8000, mem=8192, pods=110, gpu=1, model="T4")]
+    tp = [(1000, 0, 0, "", 1.0)]
+    pod = dict(cpu=1000, mem=100, milli=0, num=0, type="")
+    for evs in ([pod, dict(pod, delete=1, ref=0), dict(pod, delete=1, ref=0)],
+                [pod, dict(pod, delete=1, ref=0), dict(pod, delete=1, ref=1)]):
+        with pytest.raises(AssertionError):
+            O.run_events(nodes, tp, evs)
+    O.run_events(nodes, tp, [pod, dict(pod, delete=1, ref=0)])  # a valid stream runs

@@ -136,3 +136,40 @@ def test_synthetic_cluster(default_trace):
     names = rp.node_names(s.nodes())
     order = sorted(range(20000), key=lambda i: names[i])
     assert [rp.nodes[i].name_rank for i in order] == list(range(20000))
+
+
+def _write(path, rows):
+    with open(path, "w", newline="") as f:
+        csv.writer(f).writerows(rows)
+
+
+NODE_HDR = ["sn", "cpu_milli", "memory_mib", "gpu", "model"]
+POD_HDR = ["name", "cpu_milli", "memory_mib", "num_gpu", "gpu_milli", "gpu_spec"]
+
+
+def test_loader_rejects_short_rows(tmp_path):
+    # a row without the required columns is KSIM_EIO, not an out-of-range read
+    nodes, pods = tmp_path / "n.csv", tmp_path / "p.csv"
+    _write(pods, [POD_HDR, ["p0", "1000", "1024", "1", "500", "V100M16"]])
+    _write(nodes, [NODE_HDR, ["n0", "96000", "786432", "8", "V100M16"], ["n1", "96000"]])
+    with pytest.raises(ksim.KsimError) as ei:
+        ksim.Trace.openb(str(pods), node_csv=str(nodes))
+    assert ei.value.code == ksim.KSIM_EIO
+    _write(nodes, [NODE_HDR, ["n0", "96000", "786432", "8", "V100M16"]])
+    _write(pods, [POD_HDR, ["p0", "1000", "1024", "1", "500", "V100M16"], ["p1", "1000"]])
+    with pytest.raises(ksim.KsimError) as ei:
+        ksim.Trace.openb(str(pods), node_csv=str(nodes))
+    assert ei.value.code == ksim.KSIM_EIO
+
+
+def test_tuning_needs_gpu_demand_and_capacity(tmp_path):
+    # simulator.go:1203-1211: with a tune ratio the reference panics on a workload or cluster without
+    # CPU or GPU (tuneUpPods would never end); the replay driver returns KSIM_EINVAL instead
+    nodes, pods = tmp_path / "n.csv", tmp_path / "p.csv"
+    _write(nodes, [NODE_HDR, ["n0", "96000", "786432", "8", "V100M16"]])
+    _write(pods, [POD_HDR, ["p0", "1000", "1024", "0", "0", ""], ["p1", "2000", "1024", "0", "0", ""]])
+    t = ksim.Trace.openb(str(pods), node_csv=str(nodes))
+    with pytest.raises(ksim.KsimError) as ei:
+        t.replay(seed=1, tune_ratio=1.3)
+    assert ei.value.code == ksim.KSIM_EINVAL
+    assert t.replay(seed=1, tune_ratio=0.0).n == 2  # no tuning: fine
