@@ -221,6 +221,11 @@ int  ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, 
 int  ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t step,
                          int32_t* gpu_mask_out);
 int  ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask);
+/* Reserve + Bind `pod` on `node` on the given devices: a pod whose alibabacloud.com/gpu-index annotation
+ * already names them (allocateGpuId keeps a predefined id, open_gpu_share.go:260-271).  gpu_mask must
+ * name `gpu_count` devices of the node (none for a pod without GPU milli), each with at least
+ * `gpu_milli` left: KSIM_EINVAL / KSIM_ESTATE otherwise (the reference panics), and nothing changes. */
+int  ksim_engine_bind(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask);
 
 /* One full scheduling cycle (Filter, Score, NormalizeScore, selectHost, Reserve, Bind). */
 int  ksim_engine_schedule(ksim_engine* e, int replica, const ksim_pod* pod, int32_t step, ksim_result* out);

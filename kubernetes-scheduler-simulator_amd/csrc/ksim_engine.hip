@@ -1119,6 +1119,18 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
     }
     return;
   }
+  if (mask_in >= 0) {
+    // a predefined gpu-index (open_gpu_share.go:260-271): every named device must hold the milli
+    if (tid == 0) {
+      const NodeV n = load_node(nr);
+      bool ok = true;
+      for (int g = 0; g < kMaxGpu; ++g)
+        if ((mask_in >> g) & 1) ok = ok && g < n.gpu_cnt() && n.gl(g) >= (int)p.milli;
+      if (ok) apply_bind(nr, tg, p, mask_in, +1);
+      *out_mask = ok ? mask_in : -1;
+    }
+    return;
+  }
   const NodeV n = load_node(nr);
   const bool need_fgd = rp.gpusel == SEL_FGD && is_share_pod(p) && p.milli > 0;
   if (need_fgd) {
@@ -2347,7 +2359,7 @@ int ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int no
   int rc = to_pod_dev(*pod, &p);
   if (rc) return rc;
   KSIM_HIP(hipSetDevice(e->device));
-  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, step, e->d_scratch, +1, 0);
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, step, e->d_scratch, +1, -1);
   KSIM_HIP(hipGetLastError());
   int m = 0;
   KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
@@ -2377,6 +2389,27 @@ int ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int 
   KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
   KSIM_HIP(hipStreamSynchronize(e->stream));
   return m < 0 ? KSIM_ESTATE : KSIM_OK;  // the node does not hold what the pod would release
+}
+
+int ksim_engine_bind(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask) {
+  if (!e || !pod || replica < 0 || replica >= e->R || node < 0 || node >= e->N) return KSIM_EINVAL;
+  PodDev p;
+  int rc = to_pod_dev(*pod, &p);
+  if (rc) return rc;
+  if (p.flags & kPodDelete) return KSIM_EINVAL;
+  if (e->h_nodes[replica].size() != (size_t)e->N) return KSIM_ESTATE;
+  const int cnt = e->h_nodes[replica][node].gpu_count;
+  if (gpu_mask < 0 || gpu_mask >= (1 << cnt)) return KSIM_EINVAL;
+  if ((p.milli == 0) != (gpu_mask == 0)) return KSIM_EINVAL;
+  if (p.milli > 0 && __builtin_popcount((unsigned)gpu_mask) != p.num) return KSIM_EINVAL;
+  KSIM_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(k_reserve, dim3(1), dim3(64), 0, e->stream, e->d_reps, (const TypDev*)e->d_tp, replica, p, node, 0,
+                     e->d_scratch, +1, (int)gpu_mask);
+  KSIM_HIP(hipGetLastError());
+  int m = 0;
+  KSIM_HIP(hipMemcpyAsync(&m, e->d_scratch, sizeof m, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return m < 0 ? KSIM_ESTATE : KSIM_OK;  // a named device lacks the milli (the reference panics)
 }
 
 int ksim_engine_load_events(ksim_engine* e, int replica, const ksim_pod* events, int n) {

@@ -143,6 +143,7 @@ SIGNATURES = {
                                            _P(C.c_int32)]),
     "ksim_engine_reserve": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32, _P(C.c_int32)]),
     "ksim_engine_unreserve": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32]),
+    "ksim_engine_bind": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int, C.c_int32]),
     "ksim_engine_schedule": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int32, _P(Result)]),
     "ksim_engine_load_events": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int]),
     "ksim_engine_run": (C.c_int, [_VP]),
@@ -382,6 +383,10 @@ class Engine:
 
     def unreserve(self, r, pod, node, gpu_mask):
         check(lib().ksim_engine_unreserve(self.h, r, C.byref(pod), node, gpu_mask), "unreserve")
+
+    def bind(self, r, pod, node, gpu_mask):
+        """Reserve + Bind on the devices of a predefined gpu-index annotation (open_gpu_share.go:260-271)."""
+        check(lib().ksim_engine_bind(self.h, r, C.byref(pod), node, gpu_mask), "bind")
 
     def schedule(self, r, pod, step=0):
         res = Result()

@@ -276,6 +276,33 @@ def test_unreserve_rejects_what_the_node_does_not_hold(default_trace):
         eng.close()
 
 
+def test_bind_on_predefined_devices(default_trace):
+    # a pod that already names its devices (gpu-index annotation): bound there, and unreserve undoes it;
+    # a device without the milli left is refused and changes nothing
+    rp = default_trace.replay(seed=4)
+    keep = list(range(0, default_trace.num_nodes, 12))
+    arr, n = default_trace.typical()
+    nodes = helpers.subset_nodes(rp, keep)
+    eng = ksim.Engine(len(keep), 1)
+    try:
+        eng.set_nodes(0, nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        before = bytes(eng.nodes(0))
+        eight = [i for i in range(len(keep)) if nodes[i].gpu_count == 8][0]
+        share = ksim.make_pod(2000, 700, 1, mem=512)
+        eng.bind(0, share, eight, 1 << 5)
+        st = eng.nodes(0)
+        assert st[eight].gpu_used_milli[5] == 700 and st[eight].cpu_used_milli == 2000
+        with pytest.raises(ksim.KsimError) as ei:
+            eng.bind(0, share, eight, 1 << 5)  # 300 left < 700
+        assert ei.value.code == ksim.KSIM_ESTATE
+        eng.unreserve(0, share, eight, 1 << 5)
+        assert bytes(eng.nodes(0)) == before
+    finally:
+        eng.close()
+
+
 def test_load_events_rejects_bad_deletions(default_trace):
     # a deletion of a deletion, or a second deletion of one creation, is invalid
     rp = default_trace.replay(seed=4)
