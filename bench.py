@@ -31,9 +31,51 @@ import ksim  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
 BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
-# HBM bytes per launch of the dominant kernel of this default workload from the PMC passes of
-# scripts/profile_round.sh (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section)
-PMC_FILES = [os.path.join(ROOT, "profiles", "r01", d, "pmc.json") for d in ("head_check", "lean", "final", "gorand", "memo", "round_end")]
+# Counter passes of each bench configuration (scripts/profile_config.sh NAME ...): HBM bytes per
+# dispatch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section) and its
+# VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/r02/prof/<profile_key(args)>/pmc.json.
+PROF_DIR = os.path.join(ROOT, "profiles", "r02", "prof")
+
+
+def profile_key(args):
+    """The profiles/r02/prof/ directory of a bench configuration (scripts/profile_all.sh uses these names)."""
+    k = args.config
+    if args.policy != "FGD":
+        k += "-" + args.policy.replace(" ", "_")
+    if args.run_mode:
+        k += "-rm%d" % args.run_mode
+    if args.report and args.config != "c4":
+        k += "-report"
+    if args.sharded:
+        k += "-sharded"
+    return k
+
+
+def profile_rooflines(args, kernel):
+    """(traffic, traffic_source, valu) from this configuration's counter passes, if it was profiled and
+    the profiled dominant kernel is the one this run launched."""
+    pf = os.path.join(PROF_DIR, profile_key(args), "pmc.json")
+    if not os.path.exists(pf):
+        return None, None, None
+    with open(pf) as f:
+        pmc = json.load(f)
+    dom = pmc.get("dominant") or {}
+    fam = dom.get("kernel", "")
+    # the run's path names the kernels it launched ("memo+k_replay": k_memo or k_hmemo beside k_replay)
+    if not any(t and (t in fam if t != "memo" else fam in ("k_memo", "k_hmemo")) for t in kernel.split("+")):
+        return None, None, None
+    src = os.path.relpath(pf, ROOT)
+    valu = None
+    if dom.get("valu_insts_per_dispatch"):
+        valu = {"bound": "valu", "kernel": dom["kernel"], "achieved": dom["valu_insts_per_s"],
+                "peak": dom["valu_peak_insts_per_s"], "unit": "wave-instr/s", "frac": dom["valu_frac"],
+                "insts_per_dispatch": dom["valu_insts_per_dispatch"], "f64_share": dom.get("f64_share"),
+                "f64_frac": dom.get("f64_frac"), "nonf64_frac": dom.get("nonf64_frac"),
+                "profiled_ms": dom["mean_duration_ns"] / 1e6, "source": src,
+                "note": "rate over the profiled dispatch; peak = 256 CUs x 4 SIMDs x clock / 2 cycles per wave64 "
+                        "instruction (SIMD-32), fp64 add/mul/FMA at 4 cycles (f64_frac + nonf64_frac = issue-slot share)"}
+    traffic = dom.get("hbm_bytes_per_dispatch")
+    return traffic, src, valu
 
 
 def cpu_baseline(trace, seed, threads):
@@ -61,6 +103,54 @@ def cpu_baseline(trace, seed, threads):
                 sample="openb default, seed %d, full replay (%d events x %d nodes), FGD, %d worker threads "
                        "(parallelize.Until fan-out); host nproc=%d, cpu %s" % (seed, len(ev), trace.num_nodes, threads,
                                                                                os.cpu_count(), cpu_model()))
+
+
+# paper-sweep policy directories -> the oracle's (policy, gpu selection) (tests/test_gpu_parity.py)
+ORACLE_POLICY = {"01-Random": ("POL_RANDOM", "SEL_RANDOM"), "02-DotProd": ("POL_DOTPROD", "SEL_BEST"),
+                 "03-GpuClustering": ("POL_CLUSTERING", "SEL_BEST"), "04-GpuPacking": ("POL_PACKING", "SEL_BEST"),
+                 "05-BestFit": ("POL_BESTFIT", "SEL_BEST"), "06-FGD": ("POL_FGD", "SEL_FGD")}
+
+
+def _c4_worker(job):
+    """One paper-sweep experiment on the oracle, single-threaded, over its first `prefix` events."""
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import helpers
+    import pyoracle as O
+    trace_name, policy, seed, prefix = job
+    t = ksim.Trace.openb(trace_name[len("openb_pod_list_"):])
+    rp = t.replay(seed=seed, tune_ratio=1.3, shuffle=True)
+    pol, sel = ORACLE_POLICY[policy]
+    nodes, tp = helpers.oracle_nodes(t, rp), helpers.oracle_typical(t)
+    ev = helpers.oracle_events(t, rp, prefix)
+    t0 = time.perf_counter()
+    O.run_events(nodes, tp, ev, policy=getattr(O, pol), gpu_sel=getattr(O, sel), seed=seed, threads=1)
+    return len(ev), time.perf_counter() - t0, rp.n
+
+
+def cpu_baseline_sweep(workers=16, per_worker=2, prefix=None):
+    """SURVEY §8(d)(iii) for C4: the oracle as independent single-threaded experiments on `workers` host
+    cores (the reference runs its sweep as parallel processes, one experiment each), on a bounded sample:
+    workers x per_worker whole experiments (or their first `prefix` events) spread over the paper sweep's
+    policies and traces.  Spawned before this process touches the GPU."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import ksim.sweep as SW
+    exps = SW.plan()
+    step = max(1, len(exps) // (workers * per_worker))
+    jobs = [(e[0], e[1], e[2], prefix) for e in exps[::step][:workers * per_worker]]
+    t0 = time.perf_counter()
+    with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+        out = list(ex.map(_c4_worker, jobs))
+    wall = time.perf_counter() - t0
+    events = sum(o[0] for o in out)
+    busy = sum(o[1] for o in out)
+    full = sum(o[2] for o in out) / len(out)
+    pods_s = events / busy * workers  # per-worker rate x workers (process start-up and trace loads excluded)
+    return dict(value=pods_s, unit="pods/s", cores=workers, kind="port", experiments_per_s=pods_s / full,
+                wall_s=wall,
+                sample="%d of the 1020 paper-sweep experiments (every %dth: all 6 policies, 17 traces), %s, the oracle single-threaded in %d worker processes (SURVEY §8(d)(iii)); "
+                       "experiments/s = pods/s / %.0f events per full experiment; host nproc=%d, cpu %s"
+                       % (len(jobs), step, "the first %d events of each" % prefix if prefix else "replayed to completion", workers, full, os.cpu_count(), cpu_model()))
 
 
 def cpu_model():
@@ -118,6 +208,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # C4's CPU baseline first: its worker processes are spawned before anything here touches the GPU
+    sweep_cpu = None
+    if args.config == "c4" and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sweep_cpu = cpu_baseline_sweep(workers=args.cpu_threads)
     dist = None
     if world > 1:
         import torch
@@ -136,6 +230,7 @@ def main():
         sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs)
         eng = sweep.eng
         eng.total_events = sweep.total_events
+        eng.memo_replicas = sweep.fgd_replicas()
         args.replicas = len(exps)
     elif args.config == "c5" and args.sharded:
         # one 100k-node cluster split by name rank over the ranks; every rank replays the same 1M events
@@ -184,30 +279,12 @@ def main():
     achieved = bytes_per_launch / (kern_us * 1e-6) / 1e9
 
     value = job_events / dt
-    traffic, traffic_src = None, None
-    default_cfg = (args.config == "c2" and args.policy == "FGD" and args.replicas == 10 and args.run_mode == 0
-                   and args.wgs == 0 and not args.report)
-    for pf in PMC_FILES:  # PMC bytes of THIS kernel on this workload (profiles/ summary), if profiled
-        if default_cfg and os.path.exists(pf):
-            with open(pf) as f:
-                pmc = json.load(f)
-            if pmc.get("kernel") == kernel and pmc.get("hbm_bytes_per_dispatch"):
-                traffic = pmc["hbm_bytes_per_dispatch"]
-                traffic_src = os.path.relpath(pf, ROOT)
-                break
-    # FGD is VALU-bound, so the VALU issue fraction is reported beside the HBM one. The
-    # instruction count per launch comes from a PMC pass (scripts/profile_valu.sh -> profiles/ summary);
-    # the rate uses this run's live kernel time.
-    valu = None
-    vf = os.path.join(ROOT, "profiles", "r01", "head_check", "valu.json")
-    if default_cfg and os.path.exists(vf):
-        with open(vf) as f:
-            v = json.load(f)
-        if v.get("kernel") == kernel:
-            rate = v["valu_insts_per_dispatch"] / (kern_us * 1e-6)
-            valu = {"bound": "valu", "achieved": rate, "peak": v["peak_valu_insts_per_s"], "unit": "wave-instr/s",
-                    "frac": rate / v["peak_valu_insts_per_s"], "insts_per_launch": v["valu_insts_per_dispatch"],
-                    "source": os.path.relpath(vf, ROOT)}
+    # HBM traffic and the VALU issue fraction (FGD is fp64 VALU work) of the dominant kernel
+    # from this configuration's counter passes (scripts/profile_config.sh -> profiles/r02/prof/)
+    traffic, traffic_src, valu = profile_rooflines(args, kernel)
+    # executed work (the memoised paths skip most node evaluations): feasible (pod, node) score evaluations
+    # of the reference's Score phase, and the (class, node) keys the memoised FGD replicas recomputed
+    score_evals, key_refreshes = eng.work(getattr(eng, "memo_replicas", None))
     line = {
         "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
         "value": value,
@@ -226,6 +303,8 @@ def main():
                    "replicas_per_gpu": args.replicas, "events_per_gpu": total_events,
                    "parallelism": "replicas%d" % world},
         "node_evals_per_s": value * trace.num_nodes,
+        "score_evals_per_s": score_evals * args.steps * world / dt,
+        "key_refreshes_per_s": key_refreshes * args.steps * world / dt if "memo" in kernel else None,
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -259,6 +338,8 @@ def main():
         line["report_ms_per_step"] = eng.last_report_ms()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         line["cpu_baseline"] = cpu_baseline(trace, seeds[0], args.cpu_threads)
+    if sweep_cpu is not None:
+        line["cpu_baseline"] = sweep_cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()

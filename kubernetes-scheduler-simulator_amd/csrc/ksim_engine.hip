@@ -1200,6 +1200,7 @@ struct ksim_engine {
                            // 2: k_replay only, 3: k_memo required for FGD
   int wgs_req = 0;         // requested workgroups per replica (0 = auto)
   int cus = 256;
+  bool coop = true;  // K > 1 persistent grids through hipLaunchCooperativeKernel (KSIM_COOP=0: plain launch)
   unsigned long long* d_gran = nullptr;
   int2* d_hist = nullptr;
   size_t hist_cap = 0;
@@ -1752,7 +1753,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   const void* f = pl.decider ? (const void*)ksim_memo::k_memo<true, true>
                              : (general ? (const void*)ksim_memo::k_memo<false, true> : (const void*)ksim_memo::k_memo<false, false>);
   const TypDev* tpp = e->d_tp;
-  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, pl.K > 1, ma, tpp);
+  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
   if (rc) return rc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
@@ -1993,6 +1994,10 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     // KSIM_CUS: use at most this many CUs for co-resident persistent grids (a device shared with
     // another process; also the tests' way to exercise the residency checks)
     if (const char* c = std::getenv("KSIM_CUS")) e->cus = std::max(1, std::min(e->cus, std::atoi(c)));
+    // KSIM_COOP=0: launch K > 1 grids with hipLaunchKernel (the grid is still capped by resident_cap);
+    // the profiler passes of scripts/profile_config.sh use it -- rocprofv3 7.2 faults at process exit
+    // after a cooperative launch
+    if (const char* c = std::getenv("KSIM_COOP")) e->coop = std::atoi(c) != 0;
   }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
@@ -2840,7 +2845,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                               e->stream));
     const int grid = Rg * K;
     const TypDev* tp = e->d_tp;
-    const int lrc = launch_persistent(replay_kernel(gp.first, K, general), grid, ksim_replay::kRBlock, lds, gs, K > 1, ra, tp);
+    const int lrc = launch_persistent(replay_kernel(gp.first, K, general), grid, ksim_replay::kRBlock, lds, gs, e->coop && K > 1, ra, tp);
     if (lrc) return lrc;
     e->last_K = K;
     e->last_groups = (int)groups.size();

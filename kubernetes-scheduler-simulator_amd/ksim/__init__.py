@@ -397,6 +397,33 @@ class Engine:
     def load_events(self, r, events, n):
         check(lib().ksim_engine_load_events(self.h, r, events, n), "load_events")
         self.n_events[r] = n
+        if not hasattr(self, "events"):
+            self.events = [None] * self.R
+        self.events[r] = np.ctypeslib.as_array(events)[:n].copy() if n else None
+
+    def work(self, memo_replicas=None):
+        """Work the last run() did, from its results: feasible (pod, node) score evaluations (Score runs on
+        every feasible node, framework.go:635-710; the single-feasible shortcut skips it,
+        generic_scheduler.go:158-164), and for the memoised FGD replicas (memo_replicas; default all) the
+        (class, node) keys the refreshes recomputed (every class, on the node the previous event changed)."""
+        score_evals, refreshes = 0, 0
+        memo = set(range(self.R) if memo_replicas is None else memo_replicas)
+        for r in range(self.R):
+            n = self.n_events[r]
+            if not n:
+                continue
+            res = self.results_array(r)
+            ev = self.events[r]
+            create = ev["is_delete"] == 0
+            nf = res["n_feasible"].astype(np.int64)
+            score_evals += int(nf[create & (nf > 1)].sum())
+            changed = ((res["status"] == SCHEDULED) & create) | ((res["status"] == DELETED) & ~create & (res["node"] >= 0))
+            keys = np.stack([ev["cpu_milli"], ev["cpu_nz_milli"], ev["mem_mib"], ev["gpu_milli"], ev["gpu_count"],
+                             ev["type_mask"].astype(np.int64)], axis=1)[create]
+            classes = len(np.unique(keys, axis=0)) if len(keys) else 0
+            if r in memo:
+                refreshes += int(changed[:-1].sum()) * classes
+        return score_evals, refreshes
 
     def run(self):
         check(lib().ksim_engine_run(self.h), "run")
@@ -468,6 +495,13 @@ class Engine:
         out = (Result * max(1, n))()
         check(lib().ksim_engine_get_results(self.h, r, out, n), "get_results")
         return [(out[i].node, out[i].gpu_mask, out[i].score, out[i].n_feasible, out[i].status) for i in range(n)]
+
+    def results_array(self, r):
+        """The results of replica r as a numpy structured array (node, gpu_mask, score, n_feasible, status)."""
+        n = self.n_events[r]
+        out = (Result * max(1, n))()
+        check(lib().ksim_engine_get_results(self.h, r, out, n), "get_results")
+        return np.ctypeslib.as_array(out)[:n].copy()
 
     def nodes(self, r):
         out = (Node * self.N)()

@@ -90,6 +90,10 @@ class Sweep:
         self.eng = self.groups[0][0]  # the persistent-kernel engine (bench.py --config c4)
         self.report = report
 
+    def fgd_replicas(self, group=0):
+        """Replica indices of one group's engine that run FGD (the memoised paths)."""
+        return [r for r, i in enumerate(self.groups[group][1]) if self.exps[i][1] == "06-FGD"]
+
     def run(self):
         t0 = time.perf_counter()
         dev_ms = sum(eng.run() for eng, _ in self.groups)

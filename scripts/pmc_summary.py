@@ -1,13 +1,23 @@
-"""Summarise a profile_round.sh run: the dominant kernel's duration (kernel trace: the kernel with
-the largest total time, k_memo or k_replay) and its HBM bytes per dispatch from the FETCH_SIZE /
-WRITE_SIZE passes.  FETCH_SIZE is doubled
-(MI355X_MICROARCH.md, HBM section: on gfx950 it reports half the bytes of wide
-coalesced reads); WRITE_SIZE is taken as is.  FETCH/WRITE_SIZE are in KiB."""
+"""Summarise a profile_config.sh (or profile_round.sh) run into pmc.json: per kernel the dispatches,
+mean duration, HBM bytes (FETCH_SIZE x2 -- MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced reads -- + WRITE_SIZE, KiB), VALU instructions and the fp64 ones
+(SQ_INSTS_VALU_{ADD,MUL,FMA}_F64), and the dominant kernel (largest total time) with its rooflines:
+  hbm:  bytes per dispatch / duration vs 8 TB/s;
+  valu: wave-level VALU instructions per dispatch / duration vs 256 CUs x 4 SIMDs x clock / 2 cycles
+        (CDNA4 SIMDs are 32 lanes wide: a wave64 VALU instruction issues over 2 cycles, MI355X_MICROARCH.md;
+        157.3 TF/s fp32 = 256 x 4 x 32 x 2 x 2.4 GHz; clock = GRBM_GUI_ACTIVE / 8 XCDs / duration, 2.4 GHz
+        if that is implausible); the fp64 adds / muls / FMAs priced at their own rate, 4 cycles per wave64
+        instruction (78.6 TF/s fp64 vector = 256 x 4 x 16 lanes x 2 flop x 2.4 GHz).
+Usage: python3 scripts/pmc_summary.py DIR [bench args]"""
 import csv
 import glob
 import json
 import os
+import re
 import sys
+
+HBM_PEAK = 8.0e12
+CUS, SIMDS, XCDS = 256, 4, 8
 
 
 def rows(pattern):
@@ -18,40 +28,70 @@ def rows(pattern):
     return out
 
 
-def main(d):
-    def kernel_of(name):  # demangled or mangled names
-        if "k_memo(" in name or "k_memoENS" in name or "k_memo<" in name or "k_memoILb" in name:
-            return "k_memo"
-        return "k_replay" if "k_replay" in name else name
+def kernel_of(name):
+    """Kernel family from a (mangled or demangled) name: k_memo, k_hmemo, k_replay<policy>, ..."""
+    for k in ("k_hinit_gk", "k_hinit_keys", "k_hmemo", "k_memo_finish", "k_memo", "k_report_delta", "k_report_scan",
+              "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance"):
+        if k in name:
+            return k
+    if "k_replay" in name:
+        m = re.search(r"k_replay<(\d+)", name) or re.search(r"k_replayILi(\d+)E", name)
+        return "k_replay<%s>" % (m.group(1) if m else "?")
+    return name[:60]
 
-    allk = rows(os.path.join(d, "kt", "**", "*kernel_trace.csv"))
-    tot = {}
-    for r in allk:
+
+def main(d, args=""):
+    kt = rows(os.path.join(d, "kt", "**", "*kernel_trace.csv"))
+    per = {}
+    for r in kt:
         k = kernel_of(r.get("Kernel_Name", ""))
-        tot[k] = tot.get(k, 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    kname = max(tot, key=tot.get)
-    kt = [r for r in allk if kernel_of(r.get("Kernel_Name", "")) == kname]
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt]
+        e = per.setdefault(k, {"dispatches": 0, "total_ns": 0})
+        e["dispatches"] += 1
+        e["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 
     def counter(sub, name):
-        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv"))
-                if kernel_of(r.get("Kernel_Name", "")) == kname and r.get("Counter_Name") == name]
-        return vals
+        acc = {}
+        for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
+            if r.get("Counter_Name") != name:
+                continue
+            k = kernel_of(r.get("Kernel_Name", ""))
+            a = acc.setdefault(k, {})
+            a[r.get("Dispatch_Id", len(a))] = a.get(r.get("Dispatch_Id", len(a)), 0.0) + float(r["Counter_Value"])
+        return {k: sum(v.values()) / len(v) for k, v in acc.items()}  # mean per dispatch (summed over SEs)
 
-    fetch = counter("fetch", "FETCH_SIZE")
-    write = counter("write", "WRITE_SIZE")
-    res = {
-        "kernel": kname,
-        "dispatches": len(durs),
-        "mean_duration_ns": sum(durs) / len(durs) if durs else None,
-        "fetch_kib_per_dispatch_raw": (sum(fetch) / len(fetch)) if fetch else None,
-        "write_kib_per_dispatch": (sum(write) / len(write)) if write else None,
-    }
-    if fetch and write:
-        res["hbm_bytes_per_dispatch"] = (2 * res["fetch_kib_per_dispatch_raw"] + res["write_kib_per_dispatch"]) * 1024
-        res["note"] = "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> bytes, mean over dispatches"
-    print(json.dumps(res, indent=1))
+    fetch, write = counter("fetch", "FETCH_SIZE"), counter("write", "WRITE_SIZE")
+    valu, waves, gui = counter("valu", "SQ_INSTS_VALU"), counter("valu", "SQ_WAVES"), counter("valu", "GRBM_GUI_ACTIVE")
+    f64 = {n: counter("valu", "SQ_INSTS_VALU_%s_F64" % n) for n in ("ADD", "MUL", "FMA")}
+    for k, e in per.items():
+        e["mean_duration_ns"] = e["total_ns"] / e["dispatches"]
+        t = e["mean_duration_ns"] * 1e-9
+        if k in fetch and k in write:
+            e["hbm_bytes_per_dispatch"] = (2 * fetch[k] + write[k]) * 1024
+            e["hbm_frac"] = e["hbm_bytes_per_dispatch"] / t / HBM_PEAK
+        if k in valu:
+            e["valu_insts_per_dispatch"] = valu[k]
+            e["waves_per_dispatch"] = waves.get(k)
+            clock = gui[k] / XCDS / t if k in gui and t > 0 else 0.0
+            if not 0.5e9 < clock < 3.0e9:
+                clock = 2.4e9
+            e["clock_hz"] = clock
+            peak = CUS * SIMDS * clock / 2.0
+            e["valu_peak_insts_per_s"] = peak
+            e["valu_insts_per_s"] = valu[k] / t
+            e["valu_frac"] = valu[k] / t / peak
+            nf = sum(f64[n].get(k, 0.0) for n in f64)
+            e["f64_insts_per_dispatch"] = nf
+            e["f64_share"] = nf / valu[k] if valu[k] else 0.0
+            e["f64_frac"] = nf / t / (CUS * SIMDS * clock / 4.0)
+            e["nonf64_frac"] = (valu[k] - nf) / t / peak
+    dom = max(per, key=lambda k: per[k]["total_ns"])
+    out = {"args": args, "dominant": dict(kernel=dom, **per[dom]), "kernels": per,
+           "note": "FETCH_SIZE x2 + WRITE_SIZE (KiB -> B), mean per dispatch; VALU fraction vs 2 cycles per wave64 "
+                   "instruction (SIMD-32), fp64 at 4 cycles; clock from GRBM_GUI_ACTIVE / 8 XCDs"}
+    # the fields bench.py reads (the dominant kernel)
+    out.update(kernel=dom, hbm_bytes_per_dispatch=per[dom].get("hbm_bytes_per_dispatch"))
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")

@@ -1,7 +1,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r2a; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_memo.py -k "hmemo" -p no:cacheprovider > $O/memo.log 2>&1 || { echo "memo tests rc=$?"; tail -30 $O/memo.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_memo.py tests/test_gpu_fuzz.py -k "hmemo or (all_paths and FGD) or (cluster_report and FGD)" -p no:cacheprovider > $O/memo.log 2>&1 || { echo "memo tests rc=$?"; tail -30 $O/memo.log; exit 1; }
 tail -3 $O/memo.log
 KSIM_PROFILE=1 timeout -k 10 300 python bench.py --run-mode 5 --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_h_prof.json 2> $O/bench_h_prof.err || { echo "prof rc=$?"; tail $O/bench_h_prof.err; exit 1; }
 grep hmemo $O/bench_h_prof.err | head -3
