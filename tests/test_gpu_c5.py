@@ -89,3 +89,25 @@ def test_c5_full_replay_properties(c5):
     assert res2 == res
     print("C5 FGD: %d events on %d nodes, %d workgroups: %.1f ms (%.0f pods/s, %.3g node-evals/s)"
           % (N_PODS, N_NODES, k, ms2, N_PODS / ms2 * 1e3, N_PODS * N_NODES / ms2 * 1e3))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_c5_sharded_group_equals_unsharded(c5, world):
+    # the node-sharded mode at C5 scale, as an in-process group on one device (the
+    # same per-shard kernels as one process per GPU; the exchange is a gather kernel, not RCCL)
+    import time
+    import ksim.shard as SH
+    t, rp = c5
+    n_ev = 5000
+    want, _, ms1, _ = run(t, rp, n_ev, run_mode=2)
+    g = SH.ShardGroup(rp.nodes, t.typical(), world)
+    try:
+        g.load_events(rp.events, n_ev)
+        t0 = time.perf_counter()
+        ms = g.run()
+        wall = time.perf_counter() - t0
+        assert g.results() == want
+    finally:
+        g.close()
+    print("C5 %d events: unsharded k_replay %.1f us/pod, %d-shard group %.1f us/pod (wall %.1f)"
+          % (n_ev, ms1 * 1e3 / n_ev, world, ms * 1e3 / n_ev, wall * 1e6 / n_ev))
