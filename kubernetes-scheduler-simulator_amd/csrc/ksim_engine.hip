@@ -347,6 +347,9 @@ __device__ __forceinline__ long long result_score(const ReplicaDev& rp, int nfea
   if (rp.policy == POL_BESTFIT) return (hi > lo ? 100 : 0) * 1000LL;  // NormalizeScore (plugin_utils.go:48-74)
   if (rp.policy == POL_RANDOM) return 100 * 1000LL;
   if (rp.policy == POL_PWR_FGD) return (long long)wscore;  // already w_pwr * PWR + w_fgd * FGD
+  // PWRScorePlugin.NormalizeScore maps the max raw score to 100 (and all-equal scores to 100), and
+  // the winner holds the max raw score
+  if (rp.policy == POL_PWR) return 100 * 1000LL;
   return (long long)wscore * 1000LL;
 }
 
@@ -634,7 +637,17 @@ __global__ void k_shard_gather(unsigned long long* const* sends, unsigned long l
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
-// Dynamic LDS: ReplayShared | NodeRec nodes[S+1] | u16 tags[S+1][16] | f64 F0[S+1] | i32 last[S+1].
+// Dynamic LDS: ReplayShared | NodeRec nodes[S+1] | u16 tags[S+1][16] | f64 F0[S+1] | f64 E0[S+1] |
+// i32x2 pe[S+1] | i32 last[S+1] | i32 praw[S+1] | i32 pinf[S+1].
+//
+// PWR: NormalizeScore (pwr_score.go:104-141) sends exactly the nodes with the max raw score to 100,
+// so the argmax of the normalized score is the argmax of the raw one: one key exchange per step, the
+// raw score biased into the 24-bit key field.  PWR + FGD (the weighted sum, framework.go:686-704)
+// needs the cluster's min / max raw PWR score before any node's total is known: an A round (min,
+// max, feasible count, Score error) per step, then the normalized totals of the slice and the key
+// round, which overlaps the next step's evaluation as for every other policy.
+constexpr int kPfFeas = 1 << 30, kPfErr = 1 << 29;  // pinf flags (low 16 bits: FGD score, GPU choices)
+constexpr int kPwrKeyBias = 1 << 23;                // raw PWR score -> 24-bit key field
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -654,9 +667,11 @@ template <int kPol, int kSub, bool kGeneral>
 __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
                                                                  const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
-  constexpr bool kFgd = kPol == POL_FGD;
+  constexpr bool kPwr = kPol == POL_PWR;
+  constexpr bool kPF = kPol == POL_PWR_FGD;
+  constexpr bool kFgd = kPol == POL_FGD || kPF;  // the FGD candidate evaluation
   constexpr bool kMinMax = kPol == POL_BESTFIT;  // NormalizeScore needs the raw min / max
-  constexpr bool kErr = kPol == POL_BESTFIT || kPol == POL_PACKING || kPol == POL_CLUSTERING;
+  constexpr bool kErr = kPol == POL_BESTFIT || kPol == POL_PACKING || kPol == POL_CLUSTERING || kPwr || kPF;
   // all LDS is dynamic (no static __shared__ in front of it), carved 16-byte aligned
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ReplayShared& sh = *reinterpret_cast<ReplayShared*>(smem);
@@ -672,17 +687,29 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)S1 * sizeof(NodeRec));
   double* s_F0 = reinterpret_cast<double*>(smem + sizeof(ReplayShared) +
                                            (size_t)S1 * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t)));
+  // PWR policies: the cached energy of each slot's current state (kEnergyStale: recompute) and the
+  // node's static energy terms {rc, ncpus << 3 | CPU model} (energy_static)
+  double* s_E0 = s_F0 + S1;
+  int2* s_pe = reinterpret_cast<int2*>(s_E0 + S1);
   // cluster report: the last event that changed each slot (-1: none yet)
-  int* s_last = reinterpret_cast<int*>(s_F0 + S1);
+  int* s_last = reinterpret_cast<int*>(s_pe + S1);
+  int* s_praw = s_last + S1;  // PWR+FGD per-slot scratch of the current step
+  int* s_pinf = s_praw + S1;
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   // (null when no replica of the launch has a delete event: nothing ever reads it)
   int2* hist = (kGeneral && a.hist) ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
   NodeRec* const snap = kGeneral ? rp.snap : nullptr;
-  unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * 4;
+  unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * kGranW;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
   for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
   for (int i = tid; i <= ns; i += kRBlock) s_last[i] = -1;
+  if (kPwr || kPF) {
+    for (int i = tid; i < (int)(sizeof(PowerDev) / 8); i += kRBlock)
+      reinterpret_cast<unsigned long long*>(&sh.pw)[i] = reinterpret_cast<const unsigned long long*>(rp.pw)[i];
+    for (int i = tid; i < ns; i += kRBlock) s_pe[i] = energy_static(rp.cap[n_lo + i], rp.cpum[n_lo + i], *rp.pw);
+    for (int i = tid; i <= ns; i += kRBlock) s_E0[i] = kEnergyStale;
+  }
   if (kFgd) {
     for (int i = tid; i <= ns; i += kRBlock) s_F0[i] = -1.0;  // every cached F stale
     for (int i = tid; i < rp.nt * 2; i += kRBlock)
@@ -693,7 +720,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     sh.agg_cnt = 0;
     sh.agg_err = 0;
     sh.agg_lo = 0x7fffffff;
-    sh.agg_hi = -1;
+    sh.agg_hi = kPF ? INT_MIN : -1;
   };
   if (tid == 0) { sh.stop = 0; sh.nitems = 0; sh.pend_valid = 0; sh.pend_b = -1; reset_agg(); }
 
@@ -718,16 +745,73 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   // Wave 0, lane k: the granules of workgroups k, k+64, .. (< K) of the pending exchange
   // (relaxed agent-scope loads).
   auto poll_once = [&](GranV<kSub>& g) {
-    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * 4;
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
 #pragma unroll
     for (int j = 0; j < kSub; ++j) {
       const int k = lane + 64 * j;
       if (k < a.K) {
-        g.g0[j] = gload(slot + (size_t)k * 4 + 0);
-        g.g1[j] = gload(slot + (size_t)k * 4 + 1);
-        g.g2[j] = gload(slot + (size_t)k * 4 + 2);
+        g.g0[j] = gload(slot + (size_t)k * kGranW + 0);
+        g.g1[j] = gload(slot + (size_t)k * kGranW + 1);
+        g.g2[j] = gload(slot + (size_t)k * kGranW + 2);
       }
     }
+  };
+  // Wave 0, PWR+FGD: the A round of the current step (seq) -- publish this slice's min / max raw
+  // PWR score, feasible count and Score error, then every workgroup reduces all K of them.  The
+  // slots are safe to reuse two steps later for the same reason as the key round's.
+  auto exchange_a = [&](int c, int e, int l, int h, int* gc, int* ge, int* gl, int* gh) -> bool {
+    unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+    const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
+    if (lane == 0) {
+      gstore(slot + (size_t)w * kGranW + 4, tag | (unsigned)l);
+      gstore(slot + (size_t)w * kGranW + 5, tag | (unsigned)h);
+      gstore(slot + (size_t)w * kGranW + 6, tag | ((unsigned)e << 31) | ((unsigned)c & 0x7fffffffu));
+    }
+    unsigned long long x0[kSub], x1[kSub], x2[kSub];
+    auto load = [&]() {
+#pragma unroll
+      for (int j = 0; j < kSub; ++j) {
+        const int k = lane + 64 * j;
+        if (k < a.K) {
+          x0[j] = gload(slot + (size_t)k * kGranW + 4);
+          x1[j] = gload(slot + (size_t)k * kGranW + 5);
+          x2[j] = gload(slot + (size_t)k * kGranW + 6);
+        }
+      }
+    };
+    auto ready = [&]() {
+      bool r = true;
+#pragma unroll
+      for (int j = 0; j < kSub; ++j)
+        r = r && (lane + 64 * j >= a.K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag &&
+                                          (x2[j] & ~0xffffffffull) == tag));
+      return r;
+    };
+    load();
+    unsigned spins = 0;
+    bool ok = true;
+    while (!__all(ready())) {
+      if (++spins > kSpinLimit) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+      load();
+    }
+    int cs = 0, lo = INT_MAX, hi = INT_MIN;
+    bool e1 = false;
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) {
+      if (lane + 64 * j < a.K) {
+        const unsigned st = (unsigned)(x2[j] & 0xffffffffull);
+        cs += (int)(st & 0x7fffffffu);
+        e1 = e1 || (st >> 31) != 0u;
+        lo = min(lo, (int)(unsigned)(x0[j] & 0xffffffffull));
+        hi = max(hi, (int)(unsigned)(x1[j] & 0xffffffffull));
+      }
+    }
+    *gc = wave_sum_dpp(cs);
+    *ge = __any(e1) ? 1 : 0;
+    *gl = wave_min_dpp(lo);
+    *gh = wave_max_dpp(hi);
+    return ok;
   };
   // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
   // this workgroup's own totals (K == 1); g holds an earlier poll.  Returns the winning key.
@@ -805,6 +889,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
               reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
                   reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
+            else if (lane == 8 && kPF) { s_praw[p_b] = s_praw[ns]; s_pinf[p_b] = s_pinf[ns]; }
+            else if (lane == 9 && (kPwr || kPF)) s_E0[p_b] = s_E0[ns];
             else if (lane == 7 && snap) {  // cluster report: the post-Bind record (the virtual slot)
               store_node(snap + p_step, load_node(&s_nodes[ns]));
               rp.prev[p_step] = s_last[p_b];
@@ -831,6 +917,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
       int gc, ge, gl, gh;
       bool ok;
       const unsigned long long W = exchange(g, &gc, &ge, &gl, &gh, &ok);
+      if (kPF) { gc = p_st0; ge = p_st1; gl = p_st2; gh = p_st3; }  // the step's A round
       if (ok) commit(W, gc, ge, gl, gh);
       if (lane == 0) {
         if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
@@ -865,6 +952,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
           const int loc = h.x - n_lo;
           apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
+          if (kPwr || kPF) s_E0[loc] = kEnergyStale;
           if (snap) {
             store_node(snap + step, load_node(&s_nodes[loc]));
             rp.prev[step] = s_last[loc];
@@ -906,6 +994,17 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         if (kErr) {
           if (__any(agg && e1) && lane == 0) atomicOr(&sh.agg_err, 1);
         }
+      }
+    };
+    // PWR+FGD: a feasible node's raw PWR score into the slice's A-round aggregate (the pending best
+    // node and the virtual slot join after the commit, from their per-slot scratch)
+    auto route_a = [&](bool leader, int i, bool feas, bool e1, int praw) {
+      const bool agg = leader && feas && i != vb && i != ns;
+      const unsigned long long am = __ballot(agg);
+      if (am) {
+        if (agg) { atomicMin(&sh.agg_lo, praw); atomicMax(&sh.agg_hi, praw); }
+        if (lane == 0) atomicAdd(&sh.agg_cnt, (int)__popcll(am));
+        if (__any(agg && e1) && lane == 0) atomicOr(&sh.agg_err, 1);
       }
     };
     if constexpr (kFgd) {
@@ -976,13 +1075,75 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         int v = -1;
         if (cand) v = fgd_frag_score(s_F0[i], sh.F[my_item]) * 16 + (15 - g);
         v = group8_max(v);
+        // PWR + FGD: the node's raw PWR score and GPU choice by the same 8 lanes
+        int pv = -1;
+        bool perr = false;
+        if constexpr (kPF) {
+          bool ovf = false;
+          if (feas) {
+            const int2 pe = s_pe[i == ns ? vb : i];
+            double e0 = s_E0[i];
+            if (e0 == kEnergyStale) {
+              e0 = node_energy_now(n, pe, sh.pw);
+              if (g == 0) s_E0[i] = e0;
+            }
+            pv = pwr_cand8(n, p, pe, e0, sh.pw, g, &perr, &ovf);
+          }
+          if (ovf) atomicOr(a.fail, 2);
+          pv = group8_max(pv);
+        }
         // a feasible node with no candidate (share pod with milli 0 on a GPU-less node) scores 0
         const int raw = v < 0 ? 0 : v >> 4;
         const int gpu = (share && v >= 0) ? 15 - (v & 15) : -1;
-        const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, gpu, i == ns ? vb : i) : 0ull;
-        route(valid && g == 0, i, feas, false, raw, k);
+        if constexpr (kPF) {
+          // the node's raw PWR score and GPU choice (pwr_score.go:48-91) beside its FGD score
+          int pgpu = -1;
+          const int praw = pwr8_finish(pv, &pgpu);
+          if (valid && g == 0) {
+            s_praw[i] = praw;
+            s_pinf[i] = feas ? (kPfFeas | (perr ? kPfErr : 0) | (raw & 0xff) | ((pgpu + 1) & 0xf) << 8 |
+                                ((gpu + 1) & 0xf) << 12)
+                             : 0;
+          }
+          route_a(valid && g == 0, i, feas, perr, praw);
+        } else {
+          const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, gpu, i == ns ? vb : i) : 0ull;
+          route(valid && g == 0, i, feas, false, raw, k);
+        }
         if (c0 + kFChunk < nsv) __syncthreads();  // F / items are reused by the next chunk
         mark(3);
+      }
+    } else if constexpr (kPwr) {
+      // PWR: eight lanes per node (lane g <-> GPU g), the raw score biased into the key field
+      if (pend && a.K > 1 && wv == 0) poll_once(pg);
+      for (int c0 = 0; c0 < nsv; c0 += kFChunk) {
+        const int cn = min(kFChunk, nsv - c0);
+        const int i = c0 + (tid >> 3), g = tid & 7;
+        const bool valid = (tid >> 3) < cn;
+        NodeV n{};
+        bool feas = false, perr = false, ovf = false;
+        int pv = -1;
+        if (valid) {
+          n = load_node(&s_nodes[i]);
+          feas = filter_node(n, p);
+          if (feas) {
+            const int2 pe = s_pe[i == ns ? vb : i];
+            double e0 = s_E0[i];
+            if (e0 == kEnergyStale) {
+              e0 = node_energy_now(n, pe, sh.pw);
+              if (g == 0) s_E0[i] = e0;
+            }
+            pv = pwr_cand8(n, p, pe, e0, sh.pw, g, &perr, &ovf);
+          }
+        }
+        if (ovf) atomicOr(a.fail, 2);
+        pv = group8_max(pv);
+        int pgpu = -1;
+        const int pr = pwr8_finish(pv, &pgpu);
+        const unsigned raw = (unsigned)(pr + kPwrKeyBias);  // |pr| < 2^23 (else the run fails)
+        const unsigned long long k =
+            feas ? pack_key(raw, n.name_rank, rp.gpusel == SEL_PWR ? pgpu : -1, i == ns ? vb : i) : 0ull;
+        route(valid && g == 0, i, feas, perr, (int)raw, k);
       }
     } else {
       if (pend && a.K > 1 && wv == 0) poll_once(pg);
@@ -1003,7 +1164,101 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     }
     __syncthreads();
     mark(4);
-    if (wv == 0) {
+    if constexpr (kPF) {
+      // 1. finish the pending key round (its latency overlapped the evaluation above) and commit it
+      //    with its own A round's totals
+      if (wv == 0 && pend) {
+        int gc, ge, gl, gh;
+        bool ok = true;
+        const unsigned long long W = exchange(pg, &gc, &ge, &gl, &gh, &ok);
+        if (ok) commit(W, p_st0, p_st1, p_st2, p_st3);
+        else if (lane == 0) { sh.stop = 1; atomicOr(a.fail, 1); }
+      }
+      __syncthreads();
+      if (sh.stop) break;
+      mark(5);
+      // 2. this step's A round: the slice's aggregate plus the pending best node as committed
+      if (wv == 0) {
+        int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
+        if (vb >= 0) {
+          const int inf = s_pinf[vb];
+          if (inf & kPfFeas) {
+            ++c;
+            e |= (inf & kPfErr) ? 1 : 0;
+            l = min(l, s_praw[vb]);
+            h = max(h, s_praw[vb]);
+          }
+        }
+        int gc = c, ge = e, gl = l, gh = h;
+        bool ok = true;
+        if (a.K > 1) ok = exchange_a(c, e, l, h, &gc, &ge, &gl, &gh);
+        p_st0 = gc; p_st1 = ge; p_st2 = gl; p_st3 = gh;
+        if (lane == 0) {
+          sh.a_lo = gl;
+          sh.a_hi = gh;
+          reset_agg();
+          if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
+        }
+      }
+      __syncthreads();
+      if (sh.stop) break;
+      // 3. the slice's weighted totals w_pwr * NormalizeScore(PWR) + w_fgd * FGD (framework.go:686-704)
+      {
+        const int glo = sh.a_lo, ghi = sh.a_hi;
+        for (int i = tid; i < ns; i += kRBlock) {
+          const int inf = s_pinf[i];
+          if (inf & kPfFeas) {
+            const int norm = pwr_normalize(s_praw[i], glo, ghi);
+            const int total = rp.w_pwr * norm + rp.w_fgd * (inf & 0xff);
+            const int kg = rp.gpusel == SEL_PWR ? ((inf >> 8) & 0xf) - 1 : ((inf >> 12) & 0xf) - 1;
+            atomicMax(&sh.agg_key, pack_key((unsigned)total, load_node(&s_nodes[i]).name_rank, kg, i));
+          }
+        }
+      }
+      __syncthreads();
+      // 4. publish the key round, then prepare the virtual node as below
+      if (wv == 0) {
+        const unsigned long long mk = sh.agg_key;
+        if (lane == 0) {
+          if (a.K > 1) {
+            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+            const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
+            gstore(slot + (size_t)w * kGranW + 0, tag | (mk & 0xffffffffull));
+            gstore(slot + (size_t)w * kGranW + 1, tag | (mk >> 32));
+            gstore(slot + (size_t)w * kGranW + 2, tag);
+          }
+          sh.agg_key = 0ull;
+        }
+        const int mloc = key_loc(mk);
+        int mask = -1;
+        if (mk != 0ull) {
+          NodeV bn = load_node(&s_nodes[mloc]);
+          mask = select_gpus(bn, p, rp.gpusel, key_gpu(mk), rp.seed, step);
+          if (mask >= 0) bind_node(bn, p, mask, +1);
+          if (lane == 0) store_node(&s_nodes[ns], bn);
+          else if (lane >= 2 && lane < 6) {
+            uint2 t = reinterpret_cast<const uint2*>(&s_tags[(size_t)mloc * kTagStride])[lane - 2];
+            if (mask >= 0 && p.tag >= 0 && (p.tag >> 2) == lane - 2) {
+              const uint32_t inc = 1u << (16 * (p.tag & 1));
+              t.x += (p.tag & 2) ? 0u : inc;
+              t.y += (p.tag & 2) ? inc : 0u;
+            }
+            reinterpret_cast<uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2] = t;
+          } else if (lane == 6) {
+            s_F0[ns] = mask >= 0 ? -1.0 : s_F0[mloc];
+          } else if (lane == 7) {
+            s_E0[ns] = mask >= 0 ? kEnergyStale : s_E0[mloc];
+          }
+        }
+        p_step = step;
+        p_seq = seq;
+        p_b = mk != 0ull ? mloc : -1;
+        p_key = mk;
+        p_mask = mask;
+        ++seq;
+        if (lane == 0) { sh.pend_valid = 1; sh.pend_b = p_b; }
+      }
+    } else if (wv == 0) {
       // the slice's aggregate without b (LDS atomics above), then b's two versions
       unsigned long long mk = sh.agg_key;
       int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
@@ -1032,13 +1287,13 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         if (lane == 0) {
           // publish this step first: granules {tag, key lo32}, {tag, key hi32}, {tag, err|hi|lo|cnt}
           if (a.K > 1) {
-            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * 4;
+            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
             const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
             const unsigned stat = ((unsigned)e << 31) | ((unsigned)(h < 0 ? 0 : h) & 0x7f) << 24 |
                                   ((unsigned)(l > 127 ? 127 : l) & 0x7f) << 17 | ((unsigned)c & 0x1ffff);
-            gstore(slot + (size_t)w * 4 + 0, tag | (mk & 0xffffffffull));
-            gstore(slot + (size_t)w * 4 + 1, tag | (mk >> 32));
-            gstore(slot + (size_t)w * 4 + 2, tag | stat);
+            gstore(slot + (size_t)w * kGranW + 0, tag | (mk & 0xffffffffull));
+            gstore(slot + (size_t)w * kGranW + 1, tag | (mk >> 32));
+            gstore(slot + (size_t)w * kGranW + 2, tag | stat);
           }
           reset_agg();
         }
@@ -1062,6 +1317,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
             reinterpret_cast<uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2] = t;
           } else if (lane == 6 && kFgd) {
             s_F0[ns] = mask >= 0 ? -1.0 : s_F0[mloc];
+          } else if (lane == 7 && kPwr) {
+            s_E0[ns] = mask >= 0 ? kEnergyStale : s_E0[mloc];
           }
         }
         p_step = step;
@@ -1365,6 +1622,8 @@ static const void* replay_kernel(int pol, int K, bool general) {
     case POL_DOTPROD: return replay_fn<POL_DOTPROD>(K, general);
     case POL_PACKING: return replay_fn<POL_PACKING>(K, general);
     case POL_CLUSTERING: return replay_fn<POL_CLUSTERING>(K, general);
+    case POL_PWR: return replay_fn<POL_PWR>(K, general);
+    case POL_PWR_FGD: return replay_fn<POL_PWR_FGD>(K, general);
     default: return replay_fn<POL_RANDOM>(K, general);
   }
 }
@@ -2019,7 +2278,8 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_feas, (size_t)n_nodes));
   KSIM_HIP(hipMalloc(&e->d_score, sizeof(int32_t) * n_nodes));
   KSIM_HIP(hipMalloc(&e->d_gpu, sizeof(int32_t) * n_nodes));
-  KSIM_HIP(hipMalloc(&e->d_gran, sizeof(unsigned long long) * (size_t)n_replicas * 2 * ksim_replay::kMaxK * 4));
+  KSIM_HIP(hipMalloc(&e->d_gran, sizeof(unsigned long long) * (size_t)n_replicas * 2 * ksim_replay::kMaxK *
+                                     ksim_replay::kGranW));
   KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
   KSIM_HIP(hipMalloc(&e->d_replist, sizeof(int) * (size_t)n_replicas));
   KSIM_HIP(hipMalloc(&e->d_cap, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
@@ -2706,7 +2966,8 @@ static int resident_cap(const ksim_engine* e, const void* f, size_t lds) {
 
 static size_t replay_lds(int S) {  // S real slots + the virtual node
   return sizeof(ksim_replay::ReplayShared) +
-         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + sizeof(double) + sizeof(int));
+         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + 2 * sizeof(double) + sizeof(int2) +
+                            3 * sizeof(int));
 }
 
 
@@ -2715,7 +2976,7 @@ static size_t replay_lds(int S) {  // S real slots + the virtual node
 static int run_persistent(ksim_engine* e, int max_ev) {
   std::vector<int> order;
   std::vector<std::pair<int, int>> groups;  // (policy, count) in `order`
-  for (int pol = POL_FGD; pol <= POL_RANDOM; ++pol) {
+  for (int pol = POL_FGD; pol <= POL_PWR_FGD; ++pol) {
     int c = 0;
     for (int r = 0; r < e->R; ++r)
       if (e->reps[r].policy == pol) { order.push_back(r); ++c; }
@@ -2841,7 +3102,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     // re-initialise every polled word before the launch (granule tags restart at step 1; K = 1 polls none)
     if (K > 1)
-      KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * 4,
+      KSIM_HIP(hipMemsetAsync(e->d_gran, 0,
+                              sizeof(unsigned long long) * (size_t)e->R * 2 * ksim_replay::kMaxK * ksim_replay::kGranW,
                               e->stream));
     const int grid = Rg * K;
     const TypDev* tp = e->d_tp;
@@ -2887,9 +3149,8 @@ int ksim_engine_run(ksim_engine* e) {
   rc = reset_state(e);
   if (rc) return rc;
   if (e->report) KSIM_HIP(hipMemsetAsync(e->d_last, 0xff, sizeof(int32_t) * (size_t)e->N * e->R, e->stream));
-  // PWR policies run on the per-pod path: NormalizeScore over the cluster sits between Score and
-  // selectHost (k_step + k_step_pwr per pod, hipGraph)
-  const bool step_path = e->run_mode == 1 || any_pwr(e);
+  // run_mode 1: the per-pod path (k_step, + k_step_pwr for the PWR policies, hipGraph)
+  const bool step_path = e->run_mode == 1;
   for (int r = 0; r < e->R; ++r)
     if (is_pwr_policy(e->reps[r].policy) && !e->pw_set[r]) return KSIM_ESTATE;
   if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
@@ -2912,6 +3173,7 @@ int ksim_engine_run(ksim_engine* e) {
   if (!step_path && e->shard_world == 0) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
+    if (fail & 2) return KSIM_ERANGE;  // a raw PWR score outside the 24-bit key field
     if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
   }
   return KSIM_OK;

@@ -45,7 +45,8 @@ constexpr int kChunk = kRBlock;      // nodes per chunk, one lane per node (non-
 constexpr int kFChunk = kRBlock / 8; // nodes per chunk, 8 lanes per node -- lane g <-> GPU g (FGD)
 constexpr int kRMaxCand = 9;         // FGD items per node: stale current state + up to 8 candidates
 constexpr int kMaxK = 256;         // workgroups per replica (<= 64: one granule column per polling lane)
-constexpr int kGran = 3;           // granules per workgroup per step
+constexpr int kGran = 3;           // granules per workgroup per step (the key exchange)
+constexpr int kGranW = 8;          // granule words per workgroup per parity: key round 0-2, PWR+FGD's A round 4-6
 constexpr unsigned kSpinLimit = 1u << 22;  // ~seconds: only a non-resident workgroup can stall a poll
 constexpr int kEvBuf = 128;        // events staged in LDS per refill (4 KB)
 
@@ -55,7 +56,7 @@ struct ReplayArgs {
   int N;
   int K;            // workgroups per replica
   int S;            // slice size (nodes per workgroup)
-  unsigned long long* gran;  // [launch replica][2][K][4]
+  unsigned long long* gran;  // [launch replica][2][K][kGranW]
   int2* hist;       // [R][K][hist_stride]: (node, mask+1) of pods this workgroup bound
   int hist_stride;
   int* fail;
@@ -65,7 +66,8 @@ constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11
 
 // Per-workgroup state at the start of the dynamic LDS region (16-B aligned).  After it:
 // NodeRec nodes[S+1], u16 tags[S+1][16], double F0[S+1] (cached F of the current state,
-// < 0 = stale).  Slot ns (one past the slice) is the VIRTUAL node: the pending step's
+// < 0 = stale), i32 last[S+1] (cluster report), i32 praw[S+1] + i32 pinf[S+1] (PWR+FGD: the
+// step's raw PWR score and packed FGD score / GPU choices of every slot).  Slot ns (one past the slice) is the VIRTUAL node: the pending step's
 // local best node with that step's Bind already applied (see the pipelining note).
 struct __align__(16) ReplayShared {
   PodDev ev[kEvBuf];
@@ -80,9 +82,11 @@ struct __align__(16) ReplayShared {
   int pend_valid, pend_b;
   int stop;
   int nitems;                   // FGD work-list length of the current chunk
-  int pad0[3];
+  int a_lo, a_hi;               // PWR+FGD: the step's cluster-wide min / max raw PWR score (A round)
+  int pad0;
   unsigned long long prof[kProfPhases];  // KSIM_PROFILE phase sums (thread 0)
   unsigned long long prof_pad[4];
+  PowerDev pw;                  // PWR policies: the replica's energy model
   double F[kFChunk * kRMaxCand];
   uint16_t item_node[kFChunk * kRMaxCand];
   uint8_t item_code[kFChunk * kRMaxCand];
@@ -308,6 +312,99 @@ __device__ __forceinline__ double frag_F_quad(int cpuL, const uint32_t (&g)[4], 
   out += b5;
   out += b6;
   return out;
+}
+
+// getEnergyConsumptionNode (pwr_score.go:147) with the node's static terms precomputed:
+// rc = ceil(MilliCpuCapacity / 1000 / 2) and ncpus = ceil(rc / cores per CPU) are integer-valued
+// doubles computed by the same expressions as node_energy's, so the energy is bit-identical.
+__device__ __forceinline__ bool energy_rc(int cpuL, double rc, double ncpus, int cm, int free_gpus, int cnt, int gt,
+                                          const PowerDev& pw, double* energy) {
+  double gpu = 0;
+  if (!((pw.gnone >> gt) & 1u)) {
+    if (!((pw.gvalid >> gt) & 1u)) return false;
+    const double num_idle = (double)free_gpus;
+    const double num_working = (double)cnt - num_idle;
+    gpu = (pw.gidle[gt] * num_idle) + (pw.gfull[gt] * num_working);
+  }
+  if (!((pw.cvalid >> cm) & 1u)) return false;
+  const double idle_cores = floor((double)cpuL / (double)kMilli / 2);
+  const double working_cores = rc - idle_cores;
+  const double num_active = ceil(working_cores / pw.cnc[cm]);
+  const double num_idle_cpus = ncpus - num_active;
+  const double cpu = (pw.cidle[cm] * num_idle_cpus) + (pw.cfull[cm] * num_active);
+  *energy = cpu + gpu;
+  return true;
+}
+
+// The static terms of a node (host of energy_rc): {rc, ncpus << 3 | cpu model}.
+__device__ __forceinline__ int2 energy_static(int cap, int cm, const PowerDev& pw) {
+  const double rc = ceil((double)cap / (double)kMilli / 2);
+  const double nc = ((pw.cvalid >> cm) & 1u) ? ceil(rc / pw.cnc[cm]) : 0.0;
+  return make_int2((int)rc, (int)nc << 3 | cm);
+}
+
+// Fully free GPUs (GetFullyFreeGpuNum, resource.go:170-177) of packed milli-left words, GPU `g`
+// reduced by `d` first (g < 0: none), or the GPUs of `sub` reduced by `d`.
+__device__ __forceinline__ int free_gpus_after(const NodeV& n, int cnt, unsigned sub, int d) {
+  int f = 0;
+#pragma unroll
+  for (int h = 0; h < kMaxGpu; ++h) {
+    const int v = (int)((n.g[h >> 1] >> (16 * (h & 1))) & 0xffffu) - (((sub >> h) & 1u) ? d : 0);
+    f += (h < cnt && v == kMilli) ? 1 : 0;
+  }
+  return f;
+}
+
+// PWR score of a node by the 8 lanes of its group (lane g <-> GPU g), first half: lane g's packed
+// candidate (calculatePWRShareExtendScore, pwr_score.go:143-212).  Share pods: lane g evaluates the
+// pod on GPU g when it fits, v = (score + kBias) << 4 | (14 - g), so the group max (pwr8_finish,
+// after a uniform group8_max) is the first GPU reaching the max score, as the sequential loop keeps
+// it.  Other pods: the NodeResource.Sub state on every lane (v carries the score, GPU none).
+// old_e: the node's current energy (cached per slot; kEnergyErr when the model fails -> *err).
+// *ovf: a score outside the packed range.
+constexpr int kPwrVBias = 1 << 23;
+constexpr double kEnergyStale = -1.0, kEnergyErr = -2.0;
+__device__ __forceinline__ double node_energy_now(const NodeV& n, int2 pe, const PowerDev& pw) {
+  double e = 0;
+  const int cnt = n.gpu_cnt();
+  if (!energy_rc(n.cpu_left, (double)pe.x, (double)(pe.y >> 3), pe.y & 7, free_gpus_after(n, cnt, 0u, 0), cnt,
+                 n.gpu_type(), pw, &e))
+    return kEnergyErr;
+  return e;
+}
+__device__ __forceinline__ int pwr_cand8(const NodeV& n, const PodDev& p, int2 pe, double old_e, const PowerDev& pw,
+                                         int g, bool* err, bool* ovf) {
+  const int cnt = n.gpu_cnt(), gt = n.gpu_type(), cm = pe.y & 7;
+  const double rc = (double)pe.x, ncpus = (double)(pe.y >> 3);
+  double new_e = 0;
+  *ovf = false;
+  *err = old_e == kEnergyErr;
+  if (*err) return -1;
+  int s = 0, gsel = 15;
+  if (is_share_pod(p)) {
+    if (!(g < cnt && gl_dyn(n, g) >= p.milli)) return -1;
+    (void)energy_rc(n.cpu_left - p.cpu_nz, rc, ncpus, cm, free_gpus_after(n, cnt, 1u << g, p.milli), cnt, gt, pw,
+                    &new_e);
+    s = (int)(long long)(old_e - new_e);
+    gsel = 14 - g;
+  } else {
+    int gl[kMaxGpu];
+    unpack_gl(n, gl);
+    bool ok = false;
+    int cpuL = n.cpu_left;
+    const unsigned sm = sub_gpu_mask(gl, cnt, cpuL, p, &ok);
+    if (ok) cpuL -= p.cpu_nz;
+    (void)energy_rc(cpuL, rc, ncpus, cm, free_gpus_after(n, cnt, ok ? sm : 0u, p.milli), cnt, gt, pw, &new_e);
+    s = (int)(long long)(old_e - new_e);
+  }
+  if (s <= -kPwrVBias || s >= kPwrVBias) { *ovf = true; return -1; }
+  return ((s + kPwrVBias) << 4) | gsel;
+}
+// Second half, on the group max: the score and the GPU (-1: none / not a share pod).
+__device__ __forceinline__ int pwr8_finish(int v, int* gpu) {
+  if (v < 0) { *gpu = -1; return 0; }
+  *gpu = (v & 15) == 15 ? -1 : 14 - (v & 15);
+  return (v >> 4) - kPwrVBias;
 }
 
 // Workgroup-wide exclusive scan of one int per thread (kRBlock threads), total in *tot.

@@ -1,10 +1,12 @@
 """GPU parity of PWRScore and the weighted PWRScore + FGDScore combinations
 (pkg/simulator/plugin/pwr_score.go; generate_run_scripts.py:31-42 "PWR", "PWR 500 FGD 500", ...).
 
-The engine runs PWR replicas on the per-pod path: k_step (Filter, raw PWR score, FGD candidates)
-then k_step_pwr (NormalizeScore with the cluster's min / max, weighted sum, selectHost, Reserve,
-Bind), one pair per pod in a hipGraph.  Bar: bit-exact against the oracle, event by event, and the
-same final cluster state.  Every test needs a gfx950 device.
+The engine replays PWR replicas with the persistent k_replay (PWR: one key round per pod, the raw
+score decides; PWR + FGD: an A round for the cluster's min / max raw PWR score, then the normalized
+weighted key round) and, with run_mode 1, on the per-pod path: k_step (Filter, raw PWR score, FGD
+candidates) then k_step_pwr (NormalizeScore, weighted sum, selectHost, Reserve, Bind) in a hipGraph.
+Bar: bit-exact against the oracle, event by event, and the same final cluster state, on every path.
+Every test needs a gfx950 device.
 """
 import pytest
 
@@ -20,11 +22,15 @@ def default_trace():
     return ksim.Trace.openb("default")
 
 
-def engine_run(trace, replay, keep, n_ev, policy, nodes=None):
+PATHS = {"k_replay": dict(), "k_replay-K1": dict(wgs_per_replica=1), "k_replay-K4": dict(wgs_per_replica=4),
+         "k_step": dict(run_mode=1)}
+
+
+def engine_run(trace, replay, keep, n_ev, policy, nodes=None, **kw):
     nodes = helpers.subset_nodes(replay, keep) if keep is not None else replay.nodes
     nn = len(keep) if keep is not None else trace.num_nodes
     arr, n = trace.typical()
-    eng = ksim.Engine(nn, 1)
+    eng = ksim.Engine(nn, 1, **kw)
     eng.set_nodes(0, nodes)
     eng.set_typical(0, arr, n)
     eng.set_policy(0, policy)
@@ -59,14 +65,15 @@ def assert_same(res, want, state, want_state):
         assert [1000 - s.gpu_used_milli[g] if g < s.gpu_count else 0 for g in range(8)] == gl
 
 
+@pytest.mark.parametrize("run", sorted(PATHS))
 @pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500", "PWR 100 FGD 900", "PWR 50 FGD 950"])
-def test_subset_replay(default_trace, policy):
+def test_subset_replay(default_trace, policy, run):
     rp = default_trace.replay(seed=42)
     keep = list(range(3, default_trace.num_nodes, 7))  # 173 nodes, every GPU model
     n_ev = 1500
-    res, state, path = engine_run(default_trace, rp, keep, n_ev, policy)
+    res, state, path = engine_run(default_trace, rp, keep, n_ev, policy, **PATHS[run])
     want, want_state, _ = oracle_run(default_trace, rp, keep, n_ev, policy)
-    assert path == "k_step"
+    assert path == run.split("-")[0]
     assert_same(res, want, state, want_state)
     assert sum(1 for r in res if r[0] >= 0) > 300 and any(r[4] == 1 for r in res)  # fills up, then fails
 
@@ -74,9 +81,42 @@ def test_subset_replay(default_trace, policy):
 @pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500"])
 def test_full_trace(default_trace, policy):
     rp = default_trace.replay(seed=43)
-    res, state, _ = engine_run(default_trace, rp, None, rp.n, policy)
+    res, state, path = engine_run(default_trace, rp, None, rp.n, policy)
+    assert path == "k_replay"
     want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, policy)
     assert_same(res, want, state, want_state)
+
+
+@pytest.mark.parametrize("run", ["k_replay", "k_replay-K1", "k_step"])
+@pytest.mark.parametrize("policy", ["PWR", "PWR 500 FGD 500"])
+def test_deletes_and_report(default_trace, policy, run):
+    # a create / delete stream with the per-event cluster report on (k_replay's general instantiation)
+    rp = default_trace.replay(seed=44)
+    keep = list(range(1, default_trace.num_nodes, 5))
+    evs, oev = helpers.delete_stream(default_trace, rp, 1000, p_delete=0.3, seed=3)
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(len(keep), 1, **PATHS[run])
+    try:
+        eng.set_nodes(0, helpers.subset_nodes(rp, keep))
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, policy)
+        eng.set_power_model(0, default_trace.power_model())
+        eng.set_report(True)
+        eng.load_events(0, evs, len(evs))
+        eng.run()
+        assert eng.last_run_path() == run.split("-")[0]
+        got, state = eng.results(0), eng.nodes(0)
+    finally:
+        eng.close()
+    name, w = ksim.parse_policy(policy)
+    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    w_pwr, w_fgd = w if w else (0, 0)
+    want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev,
+                                       policy=O.POL_PWR if name == "PWR" else O.POL_PWR_FGD,
+                                       gpu_sel=O.SEL_PWR if name == "PWR" else O.SEL_FGD, threads=16,
+                                       w_pwr=w_pwr, w_fgd=w_fgd)
+    assert any(r[4] == 3 for r in got)
+    assert_same(got, want, state, want_state)
 
 
 def test_plugin_level_score_and_reserve(default_trace):
