@@ -1528,7 +1528,8 @@ struct ksim_engine {
   unsigned* d_h_l1 = nullptr;
   int* d_h_cnt = nullptr;
   unsigned long long* d_h_prof = nullptr;
-  size_t h_cap[13] = {};
+  uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
+  size_t h_cap[14] = {};
   int last_hmemo = 0;
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
   bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
@@ -1766,6 +1767,7 @@ static const double* score_table() {
 // ---- k_hmemo planning (memoised FGD replay with the keys in HBM, ksim_hmemo.hpp) ----
 struct HPlan {
   int Cmax = 1, Gmax = 1, Smax = 1, Npad = 0, nb = 0;
+  int K = 1, S = 0, nbw = 0;      // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
   size_t lds = 0;
   std::vector<int> cg;            // [Rg][2] classes, groups
   std::vector<PodDev> cls, gpod;  // [Rg][Cmax] (sorted by group), [Rg][Gmax]
@@ -1782,9 +1784,23 @@ struct HPlan {
 static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int stride, HPlan& pl) {
   using namespace ksim_hmemo;
   const int Rg = (int)reps.size();
-  if (Rg == 0 || e->N > kMaxNb * kFan || e->N > kHRankMax || !score_table()) return false;
+  if (Rg == 0 || e->N > kHRankMax || !score_table()) return false;
   pl.Npad = (e->N + kFan - 1) / kFan * kFan;
   pl.nb = pl.Npad / kFan;
+  // one workgroup per replica while one L1 level covers the cluster; wider clusters are sliced over
+  // K co-resident workgroups (at most 64: one granule column per polling lane), S a multiple of 64
+  if (e->N <= kMaxNb * kFan && e->wgs_req <= 1) {
+    pl.K = 1;
+    pl.S = e->N;
+    pl.nbw = pl.nb;
+  } else {
+    const int want = e->wgs_req > 1 ? e->wgs_req : 64;
+    pl.S = std::max(kFan, (e->N + want - 1) / want + kFan - 1) / kFan * kFan;
+    if (pl.S > kMaxNb * kFan) return false;
+    pl.K = (e->N + pl.S - 1) / pl.S;
+    pl.nbw = pl.S / kFan;
+    if ((size_t)Rg * pl.K > (size_t)e->cus) return false;
+  }
   std::vector<std::vector<int>> ord(Rg), gof(Rg), slot(Rg), gfirst(Rg), sof(Rg);
   std::vector<std::vector<NodeRec>> sts(Rg);
   pl.Cmax = pl.Gmax = pl.Smax = 1;
@@ -1824,7 +1840,7 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     }
     pl.Smax = std::max(pl.Smax, (int)sts[i].size());
   }
-  pl.lds = hmemo_layout(e->N, pl.Cmax, pl.Gmax, pl.nb).total;
+  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw).total;
   if (pl.lds > 160 * 1024) return false;
   pl.cg.assign((size_t)Rg * 2, 0);
   pl.cls.assign((size_t)Rg * pl.Cmax, PodDev{});
@@ -2155,38 +2171,65 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   ma.cnt0 = e->d_h_cnt;
   ma.th = e->d_th;
   ma.prof = nullptr;
+  ma.K = pl.K;
+  ma.S = pl.S;
+  ma.nbw = pl.nbw;
+  ma.gran = e->d_gran;
+  ma.fail = e->d_fail;
+  ma.hist = nullptr;
+  bool any_delete = false;
+  for (const int r : e->mplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
+  if (pl.K > 1) {
+    if (any_delete) {
+      int rc = ensure_buf(e->d_h_hist, e->h_cap[13], (size_t)Rg * pl.K * stride);
+      if (rc) return rc;
+      ma.hist = e->d_h_hist;
+    }
+    KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)Rg * 2 * pl.K * 2, st));
+  }
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   if (profile) {
-    int rc = ensure_buf(e->d_h_prof, e->h_cap[12], (size_t)Rg * kHProf);
+    int rc = ensure_buf(e->d_h_prof, e->h_cap[12], (size_t)Rg * pl.K * kHProf);
     if (rc) return rc;
-    KSIM_HIP(hipMemsetAsync(e->d_h_prof, 0, sizeof(unsigned long long) * (size_t)Rg * kHProf, st));
+    KSIM_HIP(hipMemsetAsync(e->d_h_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * kHProf, st));
     ma.prof = e->d_h_prof;
   }
-  KSIM_HIP(hipFuncSetAttribute((const void*)k_hmemo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
-  hipLaunchKernelGGL(k_hmemo, dim3((unsigned)Rg), dim3(kHBlock), pl.lds, st, ma, (const TypDev*)e->d_tp);
-  KSIM_HIP(hipGetLastError());
+  const void* f = pl.K <= 64 ? (const void*)k_hmemo<1> : (const void*)k_hmemo<4>;
+  if (pl.K > 1 && Rg * pl.K > resident_cap(e, f, pl.lds)) {
+    std::fprintf(stderr, "ksim: k_hmemo needs %d co-resident workgroups\n", Rg * pl.K);
+    return KSIM_ERANGE;
+  }
+  const TypDev* tpp = e->d_tp;
+  const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
+  if (lrc) return lrc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
   KSIM_HIP(hipGetLastError());
   if (profile) {
+    // per workgroup phase sums; refresh phases 0-4 run on one workgroup per step (the owner of the
+    // changed node), so they are summed over a replica's workgroups, phase 5 is averaged over them
     KSIM_HIP(hipStreamSynchronize(st));
-    std::vector<unsigned long long> h((size_t)Rg * kHProf);
+    const int nwg = Rg * pl.K;
+    std::vector<unsigned long long> h((size_t)nwg * kHProf);
     KSIM_HIP(hipMemcpy(h.data(), e->d_h_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     static const char* names[] = {"class pass", "list+loads", "F eval", "blocks+group keys", "class update", "decide+bind"};
-    std::fprintf(stderr, "ksim hmemo profile: %d replicas, LDS %zu B, Cmax %d Gmax %d Smax %d; us/step mean [max]:", Rg,
-                 pl.lds, pl.Cmax, pl.Gmax, pl.Smax);
+    std::fprintf(stderr, "ksim hmemo profile: %d replicas x K=%d (S %d), LDS %zu B, Cmax %d Gmax %d Smax %d; us/step mean [max]:",
+                 Rg, pl.K, pl.S, pl.lds, pl.Cmax, pl.Gmax, pl.Smax);
+    const double steps = std::max(max_ev, 1);
     for (int ph = 0; ph < 6; ++ph) {
       double sum = 0, mx = 0;
-      for (int b = 0; b < Rg; ++b) {
-        const double us = (double)h[(size_t)b * kHProf + ph] / 100.0 / std::max(max_ev, 1);
+      for (int g = 0; g < Rg; ++g) {
+        double us = 0;
+        for (int k = 0; k < pl.K; ++k) us += (double)h[((size_t)g * pl.K + k) * kHProf + ph] / 100.0 / steps;
+        if (ph == 5) us /= pl.K;
         sum += us;
         mx = std::max(mx, us);
       }
       std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / Rg, mx);
     }
     double it = 0, fl = 0, rs = 0, cyc = 0, tick = 0;
-    for (int b = 0; b < Rg; ++b) {
+    for (int b = 0; b < nwg; ++b) {
       it += (double)h[(size_t)b * kHProf + 7];
       fl += (double)h[(size_t)b * kHProf + 8];
       rs += (double)h[(size_t)b * kHProf + 9];
@@ -2194,7 +2237,7 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
       tick += (double)h[(size_t)b * kHProf + 11];
     }
     if (rs > 0) std::fprintf(stderr, " F items/refresh %.1f, flagged classes/refresh %.1f;", it / rs, fl / rs);
-    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / Rg / 1e5);
+    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nwg / 1e5);
     std::fprintf(stderr, "\n");
   }
   return KSIM_OK;
@@ -2354,7 +2397,8 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
-                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof};
+                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
+                  e->d_h_hist};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -2999,7 +3043,10 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   for (const auto& gp : groups) {
     if (!concurrent) break;
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
-    if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) continue;  // one workgroup per replica
+    if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) {
+      if (e->hplan->K > 1) { concurrent = false; break; }  // a co-resident wide launch
+      continue;  // one workgroup per replica
+    }
     int K = choose_wgs(e, gp.second);
     int S = (e->N + K - 1) / K;
     while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && gp.second * (K + 1) <= e->cus) {
@@ -3043,7 +3090,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
         const int rc = launch_hmemo(e, Rg, first, max_ev, gs);
         if (rc) return rc;
-        e->last_K = 1;
+        e->last_K = e->hplan->K;
         e->last_groups = (int)groups.size();
         e->last_hmemo += Rg;
         first += Rg;

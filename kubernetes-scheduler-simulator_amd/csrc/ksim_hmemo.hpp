@@ -28,6 +28,14 @@
 //
 // Keys are produced before the run by k_hinit_gk / k_hinit_keys: one evaluation per (group,
 // distinct initial node state), then key = Filter ? that score with the node's rank : 0.
+//
+// Wide clusters (C5: 100k nodes; one level of L1 covers 4096): K > 1 co-resident workgroups per
+// replica, workgroup w owning the ranks [w S, w S + S) (S a multiple of 64, so no L1 block straddles
+// two workgroups) -- their records and the L1 of their blocks in LDS; the keys stay in HBM.  Per
+// pod step only the owner of d refreshes (steps 1-5); at step 6 every workgroup takes its slice's
+// max key and feasible count of the event's class, publishes them as two {tag, value} granules,
+// polls all K (k_replay's exchange), and the owner of the global winner runs Reserve + Bind.  A
+// delete is undone by the workgroup that bound the creation (a per-workgroup bind history).
 #pragma once
 
 namespace ksim_hmemo {
@@ -77,7 +85,11 @@ struct HMemoArgs {
   const unsigned* l1;       // [Rg][Cmax][nb] initial L1 (k_hinit_keys)
   const int* cnt0;          // [Rg][Cmax] initial feasible counts
   const double* th;         // [102] FGD score steps
-  unsigned long long* prof; // optional [Rg][kHProf] (KSIM_PROFILE=1)
+  unsigned long long* prof; // optional [Rg * K][kHProf] (KSIM_PROFILE=1)
+  int K, S, nbw;            // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
+  unsigned long long* gran; // K > 1: [Rg][2][K][2] exchange granules {tag, value}
+  uint8_t* hist;            // K > 1 with deletes: [Rg][K][stride] 1 bound here, 2 Reserve failed here, 3 no winner
+  int* fail;                // K > 1: a granule poll timed out
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -90,6 +102,8 @@ struct __align__(16) HShared {
   int d;               // its rank, -1 none
   unsigned dfirst;     // first_of_class(dnew, 0)
   int nitems, nflag;
+  int stop;            // K > 1: a poll timed out, every workgroup leaves its loop
+  int pad_[3];
   unsigned long long prof[kHProf];
 };
 static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned");
@@ -156,6 +170,8 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
   return (unsigned)row_max16((int)m);
 }
 
+// kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1).
+template <int kSub>
 __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
   using ksim_memo::gget;
@@ -163,14 +179,16 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   using ksim_memo::gput_node;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HShared& sh = *reinterpret_cast<HShared*>(smem);
-  const int gi = (int)blockIdx.x;
+  const int K = a.K;
+  const int gi = (int)blockIdx.x / K, w = (int)blockIdx.x % K;
   const int r = a.rep_list[gi];
   const ReplicaDev rp = a.reps[r];
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int N = a.N, nb = a.nb;
+  const int N = a.N, nb = a.nbw;  // nb: L1 blocks of this workgroup's slice
+  const int lo = w * a.S, ns = min(a.S, N - lo), b0 = lo / kFan;
   const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
-  const HLayout L = hmemo_layout(N, a.Cmax, a.Gmax, nb);
+  const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb);
   PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
   double* s_F = reinterpret_cast<double*>(smem + L.F);
@@ -191,25 +209,36 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
   const int* evc = a.evc + (size_t)gi * a.stride;
+  unsigned long long* gr = K > 1 ? a.gran + (size_t)gi * 2 * K * 2 : nullptr;
+  uint8_t* hist = (K > 1 && a.hist) ? a.hist + ((size_t)gi * K + w) * a.stride : nullptr;
 
-  // ---- start-up: cluster (slot = rank), classes, groups, typical table, score steps, L1, counts
-  for (int i = tid; i < N; i += kHBlock) {
-    store_node(&s_nodes[i], load_node(rp.nodes + rank2idx[i]));
+  // ---- start-up: the slice (slot = rank - lo), classes, groups, typical table, score steps, L1, counts
+  for (int i = tid; i < ns; i += kHBlock) {
+    store_node(&s_nodes[i], load_node(rp.nodes + rank2idx[lo + i]));
     s_last[i] = -1;
   }
   for (int c = tid; c < C; c += kHBlock) {
     s_cls[c] = a.cls[(size_t)gi * a.Cmax + c];
     s_cgrp[c] = a.cgrp[(size_t)gi * a.Cmax + c];
-    s_cnt[c] = a.cnt0[(size_t)gi * a.Cmax + c];
+    if (K == 1) s_cnt[c] = a.cnt0[(size_t)gi * a.Cmax + c];
+  }
+  if (K > 1) {  // the slice's feasible count of every class (the initial keys hold the Filter)
+    for (int c = wv; c < C; c += kHWaves) {
+      int n = 0;
+      for (int i = lane; i < ns; i += 64) n += gget(keys + (size_t)c * a.Npad + lo + i) != 0u ? 1 : 0;
+      n = wave_sum_dpp(n);
+      if (lane == 0) s_cnt[c] = n;
+    }
   }
   for (int g = tid; g < G; g += kHBlock) {
     s_gpod[g] = a.gpod[(size_t)gi * a.Gmax + g];
     s_gfeas[g] = 0;
   }
-  for (int i = tid; i < C * nb; i += kHBlock) s_l1[i] = a.l1[(size_t)gi * a.Cmax * nb + i];
+  for (int i = tid; i < C * nb; i += kHBlock)
+    s_l1[i] = b0 + i % nb < a.nb ? a.l1[((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb] : 0u;
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
-  if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; }
+  if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; sh.stop = 0; }
   const bool prof = a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
   unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -223,6 +252,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   };
   __syncthreads();
   const bool typed = rp.typed != 0;
+  int seq = 0;  // K > 1: exchanges so far (wave 0; every workgroup sees the same events)
 
   for (int step = 0; step < rp.n_events; ++step) {
     const int eb = step & (kEvBuf - 1);
@@ -233,10 +263,10 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       for (int i = tid; i < ne; i += kHBlock) sh.evc[i] = gget(evc + step + i);
       __syncthreads();
     }
-    const int d = __builtin_amdgcn_readfirstlane(sh.d);
+    const int d = __builtin_amdgcn_readfirstlane(sh.d);  // changed rank in this slice, -1 none
     if (d >= 0) {
       const NodeV dn = uniform_node(&sh.dnew);
-      const int b = d / kFan;
+      const int b = d / kFan - b0;  // the slice's L1 block of d
       // ---- 1. class pass
       const NodeV dold = uniform_node(&sh.dold);
       for (int c = tid; c < C; c += kHBlock) {
@@ -257,7 +287,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       uint4 bv = make_uint4(0u, 0u, 0u, 0u);
       if (qid < nflag) {
         const int c = s_flist[qid];
-        bv = gld4(keys + (size_t)c * a.Npad + (size_t)b * kFan + 4 * l16);
+        bv = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
       }
       if (wv == 0) {
         const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
@@ -320,13 +350,13 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       mark(2);
       // ---- 4. flagged blocks without d (quarter rows) | group keys on d
       if (qid < nflag) {
-        const unsigned m = block_max_excl(bv, b * kFan, l16, d);
+        const unsigned m = block_max_excl(bv, (b0 + b) * kFan, l16, d);
         if (l16 == 0) s_bx[s_flist[qid]] = m;
       }
       for (int i = kQuarters + qid; i < nflag; i += kQuarters) {  // more flagged classes than quarters
         const int c = s_flist[i];
-        const uint4 v = gld4(keys + (size_t)c * a.Npad + (size_t)b * kFan + 4 * l16);
-        const unsigned m = block_max_excl(v, b * kFan, l16, d);
+        const uint4 v = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
+        const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
         if (l16 == 0) s_bx[c] = m;
       }
       for (int g = tid; g < G; g += kHBlock) {
@@ -369,56 +399,126 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       const PodDev p = uniform_pod(&sh.ev[eb]);
       const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
       int rk = -1, mask = 0;
+      bool write = false;
       NodeV before{}, after{};
       ResultDev out{-1, 0, 0, 0, ST_DELETED};
       if (cs >= 0) {
         const unsigned lv = lane < nb ? s_l1[cs * nb + lane] : 0u;
-        const unsigned W = (unsigned)wave_max_dpp((int)lv);
-        const int nfeas = __builtin_amdgcn_readfirstlane(s_cnt[cs]);
+        unsigned W = (unsigned)wave_max_dpp((int)lv);
+        int nfeas = __builtin_amdgcn_readfirstlane(s_cnt[cs]);
+        if (K > 1) {
+          // the slices' maxima and feasible counts: granules {tag, key}, {tag, count} (k_replay's exchange)
+          unsigned long long* slot = gr + (size_t)(seq & 1) * K * 2;
+          const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
+          if (lane == 0) {
+            ksim_replay::gstore(slot + (size_t)w * 2 + 0, tag | W);
+            ksim_replay::gstore(slot + (size_t)w * 2 + 1, tag | (unsigned)nfeas);
+          }
+          unsigned long long x0[kSub], x1[kSub];
+          auto load = [&]() {
+#pragma unroll
+            for (int j = 0; j < kSub; ++j) {
+              const int k = lane + 64 * j;
+              if (k < K) {
+                x0[j] = ksim_replay::gload(slot + (size_t)k * 2 + 0);
+                x1[j] = ksim_replay::gload(slot + (size_t)k * 2 + 1);
+              }
+            }
+          };
+          auto ready = [&]() {
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < kSub; ++j)
+              ok = ok && (lane + 64 * j >= K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
+            return ok;
+          };
+          load();
+          unsigned spins = 0;
+          while (!__all(ready())) {
+            if (++spins > ksim_replay::kSpinLimit) {
+              if (lane == 0) { atomicOr(a.fail, 1); sh.stop = 1; }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            load();
+          }
+          unsigned m = 0u;
+          int c = 0;
+#pragma unroll
+          for (int j = 0; j < kSub; ++j) {
+            if (lane + 64 * j < K) {
+              const unsigned kj = (unsigned)(x0[j] & 0xffffffffull);
+              m = kj > m ? kj : m;
+              c += (int)(unsigned)(x1[j] & 0xffffffffull);
+            }
+          }
+          W = (unsigned)wave_max_dpp((int)m);
+          nfeas = wave_sum_dpp(c);
+          ++seq;
+        }
         out = ResultDev{-1, 0, 0, nfeas, ST_UNSCHED};
+        write = W == 0u && w == 0;  // nobody feasible: workgroup 0 reports
+        uint8_t h = 3;
         if (W != 0u) {
           const int wr = hkey_rank(W);
-          const NodeV wn = uniform_node(&s_nodes[wr]);
-          mask = select_gpus(wn, p, rp.gpusel, hkey_gpu(W), rp.seed, step);
-          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
-            out.status = ST_ERROR;
-          } else {
-            out.status = ST_OK;
-            out.score = result_score(rp, nfeas, hkey_score(W), 0, 0);
-            out.node = wr;  // name rank; k_memo_finish maps it to the node index
-            out.gpu_mask = mask;
-            rk = wr;
-            before = wn;
-            after = wn;
-            bind_node(after, p, mask, +1);
+          h = 0;
+          if (wr >= lo && wr < lo + ns) {  // the winner is in this slice
+            const NodeV wn = uniform_node(&s_nodes[wr - lo]);
+            mask = select_gpus(wn, p, rp.gpusel, hkey_gpu(W), rp.seed, step);
+            write = true;
+            if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+              out.status = ST_ERROR;
+              h = 2;
+            } else {
+              out.status = ST_OK;
+              out.score = result_score(rp, nfeas, hkey_score(W), 0, 0);
+              out.node = wr;  // name rank; k_memo_finish maps it to the node index
+              out.gpu_mask = mask;
+              rk = wr;
+              before = wn;
+              after = wn;
+              bind_node(after, p, mask, +1);
+              h = 1;
+            }
           }
         }
+        if (hist && lane == 0) hist[step] = h;
       } else if (p.ref >= 0 && p.ref < step) {
-        // simulator.go:416-422 deletePod: undo the creation's Bind (its result holds the rank and mask)
-        const ResultDev cr = gget(rp.res + p.ref);
-        const int crk = __builtin_amdgcn_readfirstlane(cr.node);
-        const int cst = __builtin_amdgcn_readfirstlane(cr.status);
-        const int cmask = __builtin_amdgcn_readfirstlane(cr.gpu_mask);
-        if (crk >= 0 && cst == ST_OK) {
-          const PodDev bp = uniform_pod(reinterpret_cast<const PodDev*>(rp.ev + p.ref));
-          rk = crk;
-          before = uniform_node(&s_nodes[rk]);
-          after = before;
-          bind_node(after, bp, cmask, -1);
-          out = ResultDev{rk, cmask, 0, 0, ST_DELETED};
+        // simulator.go:416-422 deletePod: undo the creation's Bind (its result holds the rank and mask);
+        // with K > 1 only the workgroup that bound it (its own history) reads that result
+        const int hh = hist ? (int)hist[p.ref] : 1;
+        if (hh == 1) {
+          const ResultDev cr = gget(rp.res + p.ref);
+          const int crk = __builtin_amdgcn_readfirstlane(cr.node);
+          const int cst = __builtin_amdgcn_readfirstlane(cr.status);
+          const int cmask = __builtin_amdgcn_readfirstlane(cr.gpu_mask);
+          if (crk >= 0 && cst == ST_OK) {
+            const PodDev bp = uniform_pod(reinterpret_cast<const PodDev*>(rp.ev + p.ref));
+            rk = crk;
+            before = uniform_node(&s_nodes[rk - lo]);
+            after = before;
+            bind_node(after, bp, cmask, -1);
+            out = ResultDev{rk, cmask, 0, 0, ST_DELETED};
+          }
+          write = true;
+        } else {
+          write = hh == 2 || (hh == 3 && w == 0);
         }
+        if (hist && lane == 0) hist[step] = 0;
+      } else {
+        write = w == 0;
       }
       if (lane == 0) {
-        gput(rp.res + step, out);
+        if (write) gput(rp.res + step, out);
         if (rk >= 0) {
-          store_node(&s_nodes[rk], after);
+          store_node(&s_nodes[rk - lo], after);
           store_node(&sh.dold, before);
           store_node(&sh.dnew, after);
           if (rp.snap) {  // cluster report: the state this event left
             gput_node(rp.snap + step, after);
-            gput(rp.prev + step, s_last[rk]);
+            gput(rp.prev + step, s_last[rk - lo]);
           }
-          s_last[rk] = step;
+          s_last[rk - lo] = step;
         }
         sh.d = rk;
       }
@@ -429,15 +529,16 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
     }
     __syncthreads();
     mark(5);
+    if (K > 1 && sh.stop) break;
   }
   if (prof && tid == 0) {
     sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
     sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;
   }
   __syncthreads();
-  if (prof && tid < kHProf) a.prof[(size_t)gi * kHProf + tid] = sh.prof[tid];
+  if (prof && tid < kHProf) a.prof[(size_t)blockIdx.x * kHProf + tid] = sh.prof[tid];
   // final cluster state
-  for (int i = tid; i < N; i += kHBlock) store_node(rp.nodes + rank2idx[i], load_node(&s_nodes[i]));
+  for (int i = tid; i < ns; i += kHBlock) store_node(rp.nodes + rank2idx[lo + i], load_node(&s_nodes[i]));
 }
 
 // ---------------------------------------------------------------------------

@@ -1,6 +1,7 @@
 """GPU parity of the memoised FGD replays -- k_memo (run_mode 3, keys in LDS over K workgroups) and
-k_hmemo (run_mode 5, keys in HBM, one workgroup per replica) -- against the oracle and against the
-scanning replay (k_replay, run_mode 2).
+k_hmemo (run_mode 5, keys in HBM; one workgroup per replica, or with wgs_per_replica > 1 / clusters
+over 4096 nodes the wide form: K workgroups each owning a slice of ranks, one exchange per pod) --
+against the oracle and against the scanning replay (k_replay, run_mode 2).
 
 k_memo keeps the key of every (pod class, node) pair and recomputes only the node the previous
 event changed; in decider mode (run_mode 4) workgroup 0 decides every event from the class owners'
@@ -185,13 +186,44 @@ def test_hmemo_when_kmemo_does_not_fit(default_trace):
     assert outs[0] == outs[SCAN]
 
 
-def test_hmemo_cluster_report(default_trace):
+@pytest.mark.parametrize("wgs", [2, 7, 19, 64])
+def test_hmemo_wide_vs_oracle(default_trace, wgs):
+    # the wide k_hmemo: ceil(1213 / S) workgroups of S ranks (S a multiple of 64), one exchange per pod
+    rp = default_trace.replay(seed=48)
+    n_ev = 3000
+    res, state = engine_run(default_trace, rp, None, n_ev, "FGD", run_mode=HMEMO, wgs=wgs)
+    want, want_state, _ = oracle_run(default_trace, rp, None, n_ev, O.POL_FGD, O.SEL_FGD)
+    assert_same(res, want, state, want_state, None)
+
+
+def test_hmemo_wide_replicas_and_path(default_trace):
+    # three replicas x K workgroups in one cooperative launch; the engine reports the path and K
+    arr, n = default_trace.typical()
+    outs = {}
+    for mode, wgs in ((HMEMO, 5), (SCAN, 0)):
+        eng = ksim.Engine(default_trace.num_nodes, 3, run_mode=mode, wgs_per_replica=wgs)
+        for r in range(3):
+            rp = default_trace.replay(seed=60 + r)
+            eng.set_nodes(r, rp.nodes)
+            eng.set_typical(r, arr, n)
+            eng.set_policy(r, "FGD")
+            eng.load_events(r, rp.events, 2000 + 300 * r)
+        eng.run()
+        if mode == HMEMO:
+            assert eng.last_run_path() == "k_hmemo" and eng.last_run_wgs() == 5
+        outs[mode] = [eng.results(r) for r in range(3)]
+        eng.close()
+    assert outs[HMEMO] == outs[SCAN]
+
+
+@pytest.mark.parametrize("wgs", [0, 5])
+def test_hmemo_cluster_report(default_trace, wgs):
     # the per-event report from k_hmemo's snapshots equals k_replay's (exact fixed-point sums)
     rp = default_trace.replay(seed=47)
     arr, n = default_trace.typical()
     reps = {}
     for mode in (HMEMO, SCAN):
-        eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=mode)
+        eng = ksim.Engine(default_trace.num_nodes, 1, run_mode=mode, wgs_per_replica=wgs if mode == HMEMO else 0)
         eng.set_nodes(0, rp.nodes)
         eng.set_typical(0, arr, n)
         eng.set_policy(0, "FGD")
