@@ -11,19 +11,20 @@
 //   LDS   L1[c][b] = max key[c][64b .. 64b+63]    (a max tree of fan-out 64, one level: N <= 4096)
 //         the cluster (node slot = name rank), the class table, the typical table.
 // Per pod step, with d = the node changed by the previous event (its Bind or a delete):
-//   1. class pass (one thread per class): Filter on d's new and old records (feasible counts),
-//      which score groups (same cpu_nz, milli, num: same candidate states, fgd_score.go:99-149)
-//      some class finds feasible, and which classes had d as the max of d's block (flagged);
-//   2. wave 0 lists the F evaluations: d's current state + each feasible group's candidates (one
-//      per distinct milli-left value among the fitting GPUs, or the NodeResource.Sub state); every
-//      quarter-wave issues the HBM load of one flagged class's 64-key block (held in registers);
-//   3. every quad of lanes evaluates one state's F (frag_F_quad, bit-exact with frag.go);
-//   4. the flagged blocks' maxima without d (quarter-wave DPP), the groups' keys on d;
-//   5. class pass: key[c][d] (HBM store) and L1[c][d/64] (max with the new key, or the block max
-//      without d when d was the block max);
-//   6. wave 0: the winner of the event's class = max over L1[class][*] (selectHost: max score, ties
+//   1. wave 0 lists the F evaluations: d's current state + every score group's candidates (groups:
+//      same cpu_nz, milli, num, hence the same candidate states, fgd_score.go:99-149; one candidate
+//      per distinct milli-left value among the fitting GPUs, or the NodeResource.Sub state), while
+//      waves 1-15 run the class pass: Filter on d's new and old records (feasible counts) and which
+//      classes had d as the max of d's block (flagged);
+//   2. every quarter-wave issues the HBM load of one flagged class's 64-key block (held in
+//      registers), every quad of lanes evaluates one state's F (frag_F_quad, bit-exact with
+//      frag.go), then the quarter-waves take their blocks' maxima without d (DPP);
+//   3. class pass: the class's group key on d (score steps of its candidates), key[c][d] (HBM
+//      store), L1[c][d/64] (max with the new key, or the block max without d when d was the block
+//      max), the feasible count;
+//   4. wave 0: the winner of the event's class = max over L1[class][*] (selectHost: max score, ties
 //      to the smallest name), Reserve's GPU selector on it, the Bind in LDS, the result.
-// Every key of every class is fresh at step 6, so the decision is the one k_replay / k_step / the
+// Every key of every class is fresh at step 4, so the decision is the one k_replay / k_step / the
 // oracle make (same device functions: filter_node, fgd_candidate + frag_F_quad, the score table).
 //
 // Keys are produced before the run by k_hinit_gk / k_hinit_keys: one evaluation per (group,
@@ -32,7 +33,7 @@
 // Wide clusters (C5: 100k nodes; one level of L1 covers 4096): K > 1 co-resident workgroups per
 // replica, workgroup w owning the ranks [w S, w S + S) (S a multiple of 64, so no L1 block straddles
 // two workgroups) -- their records and the L1 of their blocks in LDS; the keys stay in HBM.  Per
-// pod step only the owner of d refreshes (steps 1-5); at step 6 every workgroup takes its slice's
+// pod step only the owner of d refreshes (steps 1-3); at step 4 every workgroup takes its slice's
 // max key and feasible count of the event's class, publishes them as two {tag, value} granules,
 // polls all K (k_replay's exchange), and the owner of the global winner runs Reserve + Bind.  A
 // delete is undone by the workgroup that bound the creation (a per-workgroup bind history).
@@ -110,7 +111,7 @@ static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned"
 
 // Dynamic LDS after HShared (16-B aligned regions).
 struct HLayout {
-  size_t cls, gpod, F, l1, nodes, last, cnt, bx, cgrp, flist, code, igrp, fnew, fold, gfeas, gbase, gkey, total;
+  size_t cls, gpod, F, l1, nodes, last, cnt, bx, cgrp, flist, code, igrp, fnew, fold, gbase, total;
 };
 KSIM_HD size_t halign(size_t x) { return (x + 15) & ~(size_t)15; }
 KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
@@ -130,9 +131,7 @@ KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
   L.igrp = o;  o = halign(o + (size_t)kMaxItems);
   L.fnew = o;  o = halign(o + (size_t)Cmax);
   L.fold = o;  o = halign(o + (size_t)Cmax);
-  L.gfeas = o; o = halign(o + (size_t)Gmax);
   L.gbase = o; o = halign(o + (size_t)Gmax * 2);
-  L.gkey = o;  o = halign(o + (size_t)Gmax * 4);
   L.total = o;
   return L;
 }
@@ -203,9 +202,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   uint8_t* s_igrp = reinterpret_cast<uint8_t*>(smem + L.igrp);
   uint8_t* s_fnew = reinterpret_cast<uint8_t*>(smem + L.fnew);
   uint8_t* s_fold = reinterpret_cast<uint8_t*>(smem + L.fold);
-  uint8_t* s_gfeas = reinterpret_cast<uint8_t*>(smem + L.gfeas);
   int16_t* s_gbase = reinterpret_cast<int16_t*>(smem + L.gbase);
-  unsigned* s_gkey = reinterpret_cast<unsigned*>(smem + L.gkey);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
   const int* evc = a.evc + (size_t)gi * a.stride;
@@ -232,7 +229,6 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   }
   for (int g = tid; g < G; g += kHBlock) {
     s_gpod[g] = a.gpod[(size_t)gi * a.Gmax + g];
-    s_gfeas[g] = 0;
   }
   for (int i = tid; i < C * nb; i += kHBlock)
     s_l1[i] = b0 + i % nb < a.nb ? a.l1[((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb] : 0u;
@@ -267,28 +263,8 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
     if (d >= 0) {
       const NodeV dn = uniform_node(&sh.dnew);
       const int b = d / kFan - b0;  // the slice's L1 block of d
-      // ---- 1. class pass
-      const NodeV dold = uniform_node(&sh.dold);
-      for (int c = tid; c < C; c += kHBlock) {
-        const PodDev q = s_cls[c];
-        const bool fn = filter_node(dn, q);
-        const bool fo = filter_node(dold, q);
-        s_fnew[c] = fn ? 1 : 0;
-        s_fold[c] = fo ? 1 : 0;
-        if (fn) s_gfeas[s_cgrp[c]] = 1;
-        const unsigned old = s_l1[c * nb + b];
-        if (old != 0u && hkey_rank(old) == d) s_flist[atomicAdd(&sh.nflag, 1)] = (uint16_t)c;
-      }
-      __syncthreads();
-      mark(0);
-      // ---- 2. the flagged blocks' loads (one quarter-wave each, held in registers) | wave 0: F list
-      const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
-      const int qid = tid >> 4, l16 = tid & 15;
-      uint4 bv = make_uint4(0u, 0u, 0u, 0u);
-      if (qid < nflag) {
-        const int c = s_flist[qid];
-        bv = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
-      }
+      // ---- 1. wave 0: the F list over every score group (d's current state + each group's candidates;
+      //         a group no class admits just goes unused) | waves 1-15: the class pass
       if (wv == 0) {
         const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
         int base = 1;  // item 0: d's current state
@@ -296,7 +272,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           const int g = g0 + lane;
           unsigned cm = 0u;
           bool share = false;
-          if (g < G && s_gfeas[g]) {
+          if (g < G) {
             const PodDev gp = s_gpod[g];
             share = is_share_pod(gp);
             cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
@@ -326,10 +302,38 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           s_igrp[0] = 0;
           sh.nitems = base;
         }
+      } else {
+        // Filter on d's new and old records (feasible counts), and which classes had d as the max of
+        // d's block (flagged: their block max must be recomputed without d)
+        const NodeV dold = uniform_node(&sh.dold);
+        for (int c = tid - 64; c < C; c += kHBlock - 64) {
+          const PodDev q = s_cls[c];
+          s_fnew[c] = filter_node(dn, q) ? 1 : 0;
+          s_fold[c] = filter_node(dold, q) ? 1 : 0;
+          const unsigned old = s_l1[c * nb + b];
+          const bool fl = old != 0u && hkey_rank(old) == d;
+          const unsigned long long fm = __ballot(fl);
+          if (fm) {
+            int o = 0;
+            if (lane == __builtin_ctzll(fm)) o = atomicAdd(&sh.nflag, (int)__popcll(fm));
+            o = __builtin_amdgcn_readlane(o, __builtin_ctzll(fm));
+            if (fl)
+              s_flist[o + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u))] =
+                  (uint16_t)c;
+          }
+        }
       }
       __syncthreads();
-      mark(1);
-      // ---- 3. F of every listed state, one quad each
+      mark(0);
+      // ---- 2. the flagged blocks' loads (one quarter-wave each, held in registers), F of every listed
+      //         state (one quad each), then the flagged blocks' maxima without d
+      const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
+      const int qid = tid >> 4, l16 = tid & 15;
+      uint4 bv = make_uint4(0u, 0u, 0u, 0u);
+      if (qid < nflag) {
+        const int c = s_flist[qid];
+        bv = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
+      }
       {
         const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
         const int q = tid & 3;
@@ -346,9 +350,6 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         }
         if (prof && tid == 0) { sh.prof[7] += (unsigned long long)nit; sh.prof[8] += (unsigned long long)nflag; sh.prof[9] += 1ull; }
       }
-      __syncthreads();
-      mark(2);
-      // ---- 4. flagged blocks without d (quarter rows) | group keys on d
       if (qid < nflag) {
         const unsigned m = block_max_excl(bv, (b0 + b) * kFan, l16, d);
         if (l16 == 0) s_bx[s_flist[qid]] = m;
@@ -359,42 +360,42 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
         if (l16 == 0) s_bx[c] = m;
       }
-      for (int g = tid; g < G; g += kHBlock) {
-        if (s_gfeas[g]) {
-          s_gfeas[g] = 0;
-          const double F0 = s_F[0];
-          const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : sh.nitems;  // the group's candidates
-          unsigned k;
-          if (is_share_pod(s_gpod[g])) {
-            k = hkey(0, d, 0);  // feasible with no fitting GPU
-            for (int i = o; i < oe; ++i) {
-              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
-              k = x > k ? x : k;
-            }
-          } else {
-            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
-          }
-          s_gkey[g] = k;
-        }
-      }
       __syncthreads();
-      mark(3);
-      // ---- 5. every class's key on d, its L1 entry, its feasible count
-      for (int c = tid; c < C; c += kHBlock) {
-        const bool fn = s_fnew[c] != 0;
-        const unsigned k = fn ? s_gkey[s_cgrp[c]] : 0u;
-        gst1(keys + (size_t)c * a.Npad + d, k);
-        s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
-        unsigned* l = &s_l1[c * nb + b];
-        const unsigned old = *l;
-        if (k > old) *l = k;
-        else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
+      mark(2);
+      // ---- 3. every class: its group's key on d (if d passes the class's Filter), the key, its L1
+      //         entry, its feasible count
+      {
+        const double F0 = s_F[0];
+        const int nit = sh.nitems;
+        for (int c = tid; c < C; c += kHBlock) {
+          const bool fn = s_fnew[c] != 0;
+          unsigned k = 0u;
+          if (fn) {
+            const int g = s_cgrp[c];
+            const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
+            if (is_share_pod(s_gpod[g])) {
+              k = hkey(0, d, 0);  // feasible with no fitting GPU
+              for (int i = o; i < oe; ++i) {
+                const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
+                k = x > k ? x : k;
+              }
+            } else {
+              k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
+            }
+          }
+          gst1(keys + (size_t)c * a.Npad + d, k);
+          s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
+          unsigned* l = &s_l1[c * nb + b];
+          const unsigned old = *l;
+          if (k > old) *l = k;
+          else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
+        }
       }
       if (tid == 0) sh.nflag = 0;
       __syncthreads();
       mark(4);
     }
-    // ---- 6. the event: the winner of its class (create) or the unbind (delete); wave 0
+    // ---- 4. the event: the winner of its class (create) or the unbind (delete); wave 0
     if (wv == 0) {
       const PodDev p = uniform_pod(&sh.ev[eb]);
       const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
