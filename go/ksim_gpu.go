@@ -67,8 +67,12 @@ const (
 type KsimGpuPluginCfg struct {
 	// Policy: the score plugin the engine computes, by its reference name (pkg/type/const.go:7-13).
 	Policy string `json:"policy,omitempty"`
-	// GpuSelMethod: Open-Gpu-Share's gpuSelMethod ("best", "worst", "random", "FGDScore", "PWRScore").
+	// GpuSelMethod: Open-Gpu-Share's gpuSelMethod ("best", "worst", "random", "FGDScore", "PWRScore",
+	// "DotProductScore").
 	GpuSelMethod string `json:"gpuSelMethod,omitempty"`
+	// DimExtMethod / NormMethod: DotProductScore's GpuPluginCfg (pkg/type/config.go:3-55); the
+	// reference's harness gives the score plugin and Open-Gpu-Share the same values.
+	simontype.GpuPluginCfg
 	// Seed of the Random contract (RandomScore and the random GPU selector; DESIGN.md §4).
 	Seed int64 `json:"seed,omitempty"`
 	// WriteGpuIndex: patch the alibabacloud.com/gpu-index annotation in Reserve (set when
@@ -94,6 +98,20 @@ var ksimGpuSels = map[string]C.int{
 	string(simontype.SelRandomGpu):   C.KSIM_GPUSEL_RANDOM,
 	simontype.FGDScorePluginName:     C.KSIM_GPUSEL_FGD,
 	simontype.PWRScorePluginName:     C.KSIM_GPUSEL_PWR,
+	simontype.DotProductScorePluginName: C.KSIM_GPUSEL_DOTPROD,
+}
+
+var ksimDimExt = map[simontype.GpuDimExtMethod]C.int{
+	simontype.MergeGpuDim:                     C.KSIM_DIMEXT_MERGE,
+	simontype.SeparateGpuDimAndShareOtherDim:  C.KSIM_DIMEXT_SHARE,
+	simontype.SeparateGpuDimAndDivideOtherDim: C.KSIM_DIMEXT_DIVIDE,
+	simontype.ExtGpuDim:                       C.KSIM_DIMEXT_EXTEND,
+}
+
+var ksimNorm = map[simontype.NormMethod]C.int{
+	simontype.NormByMax:  C.KSIM_NORM_MAX,
+	simontype.NormByNode: C.KSIM_NORM_NODE,
+	simontype.NormByPod:  C.KSIM_NORM_POD,
 }
 
 // The engine's CPU model ids: the order of the CPU table ksim_trace_power_model fills
@@ -379,6 +397,27 @@ func (p *KsimGpuPlugin) ensureEngine() error {
 	}
 	if rc := C.ksim_engine_set_policy(eng, 0, p.policy, p.gpuSel, C.uint64_t(p.cfg.Seed)); rc != 0 {
 		return fail("set_policy", rc)
+	}
+	if p.policy == C.KSIM_POLICY_DOTPROD {
+		// GenerateSchedulingMatchGroups' cfg (utils.go:1274-1342); empty = the paper's merge / max
+		dim, norm := C.int(C.KSIM_DIMEXT_MERGE), C.int(C.KSIM_NORM_MAX)
+		if p.cfg.DimExtMethod != "" {
+			d, ok := ksimDimExt[p.cfg.DimExtMethod]
+			if !ok {
+				return fmt.Errorf("ksim: undefined gpu dimension extension method: %v", p.cfg.DimExtMethod)
+			}
+			dim = d
+		}
+		if p.cfg.NormMethod != "" {
+			n, ok := ksimNorm[p.cfg.NormMethod]
+			if !ok {
+				return fmt.Errorf("ksim: undefined normalization for dot product: %v", p.cfg.NormMethod)
+			}
+			norm = n
+		}
+		if rc := C.ksim_engine_set_plugin_cfg(eng, 0, dim, norm); rc != 0 {
+			return fail("set_plugin_cfg", rc)
+		}
 	}
 	if p.policy == C.KSIM_POLICY_PWR {
 		pm := p.powerModel()

@@ -63,7 +63,8 @@ enum ksim_status {
 enum ksim_policy {
     KSIM_POLICY_FGD = 0,
     KSIM_POLICY_BESTFIT = 1,
-    KSIM_POLICY_DOTPROD = 2,        /* dimExtMethod=merge, normMethod=max (paper configuration) */
+    KSIM_POLICY_DOTPROD = 2,        /* DotProductScore; dimExtMethod / normMethod via ksim_engine_set_plugin_cfg
+                                       (default merge / max: the paper configuration) */
     KSIM_POLICY_GPUPACKING = 3,
     KSIM_POLICY_GPUCLUSTERING = 4,
     KSIM_POLICY_RANDOM = 5,
@@ -78,8 +79,19 @@ enum ksim_gpusel {
     KSIM_GPUSEL_WORST = 1,
     KSIM_GPUSEL_RANDOM = 2,
     KSIM_GPUSEL_FGD = 3,
-    KSIM_GPUSEL_PWR = 4             /* "PWRScore": allocateGpuIdBasedOnPWRScore (pwr_score.go:214-219) */
+    KSIM_GPUSEL_PWR = 4,            /* "PWRScore": allocateGpuIdBasedOnPWRScore (pwr_score.go:214-219) */
+    KSIM_GPUSEL_DOTPROD = 5         /* "DotProductScore": the best match group's GPU id
+                                       (allocateGpuIdBasedOnDotProduct, dot_product_score.go:102-107) */
 };
+
+/* GpuPluginCfg of the DotProduct score (pkg/type/config.go:3-55) */
+enum ksim_dim_ext {
+    KSIM_DIMEXT_MERGE = 0,          /* "merge": <cpu left, total GPU milli left> */
+    KSIM_DIMEXT_SHARE = 1,          /* "share": one virtual node per partly used GPU + one of the idle GPUs */
+    KSIM_DIMEXT_DIVIDE = 2,         /* "divide": as share, CPU left scaled by the GPU's share of the GPU left */
+    KSIM_DIMEXT_EXTEND = 3          /* "extend": one dimension per formalized GPU entry */
+};
+enum ksim_norm { KSIM_NORM_MAX = 0, KSIM_NORM_NODE = 1, KSIM_NORM_POD = 2 };
 
 /* Result status (framework.Status codes) */
 enum ksim_result_status { KSIM_SCHEDULED = 0, KSIM_UNSCHEDULABLE = 1, KSIM_ERROR = 2, KSIM_DELETED = 3 };
@@ -207,6 +219,10 @@ int  ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel,
  * KSIM_POLICY_PWR_FGD, the two plugin weights of the scheduler configuration. */
 int  ksim_engine_set_power_model(ksim_engine* e, int replica, const ksim_power_model* pm);
 int  ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t w_fgd);
+/* DotProduct's dimExtMethod / normMethod (the score plugin's and Open-Gpu-Share's args, which the
+ * reference harness sets alike: generate_config_and_run.py:269-277).  Replaces
+ * GenerateSchedulingMatchGroups' cfg arguments (pkg/utils/utils.go:1274-1342). */
+int  ksim_engine_set_plugin_cfg(ksim_engine* e, int replica, int dim_ext, int norm);
 
 /* Plugin-level entry points (no state change).  For one pod, Filter + Score
  * every node of the replica: feasible[n] (0/1), score[n] (the plugin's Score

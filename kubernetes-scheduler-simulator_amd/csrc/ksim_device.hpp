@@ -137,7 +137,7 @@ struct ReplicaDev {
   const NodeRec* init;   // [N]
   int32_t* last;         // [N] k_step: last event that changed each node
   int32_t node_off;      // node-sharded cluster: global index (= name rank) of local node 0, else 0
-  int32_t pad_;
+  int32_t dpcfg;         // DotProduct GpuPluginCfg: dimExtMethod | normMethod << 4 (dp_dim / dp_norm)
   // PWR (pwr_score.go): energy model, CPU model id per node, per-node PWR scratch of the
   // two-phase k_step cycle (raw PWR score | packed FGD score and GPU choices), plugin weights
   const struct PowerDev* pw;
@@ -167,7 +167,7 @@ struct __align__(64) Accum {
 
 enum : int { POL_FGD = 0, POL_BESTFIT = 1, POL_DOTPROD = 2, POL_PACKING = 3, POL_CLUSTERING = 4, POL_RANDOM = 5,
              POL_PWR = 6, POL_PWR_FGD = 7 };
-enum : int { SEL_BEST = 0, SEL_WORST = 1, SEL_RANDOM = 2, SEL_FGD = 3, SEL_PWR = 4 };
+enum : int { SEL_BEST = 0, SEL_WORST = 1, SEL_RANDOM = 2, SEL_FGD = 3, SEL_PWR = 4, SEL_DOTPROD = 5 };
 KSIM_HD bool is_pwr_policy(int pol) { return pol == POL_PWR || pol == POL_PWR_FGD; }
 
 // PWR energy model (== ksim_power_model): resource.go:536-563 GetEnergyConsumptionNode with the
@@ -220,6 +220,25 @@ KSIM_HD double go_exp(double x) {
 
 // plugin_utils.go:76-78
 KSIM_HD double go_sigmoid(double x) { return 1.0 / (1.0 + go_exp(-x)); }
+
+// Go math.Tanh, portable algorithm (Go src/math/tanh.go: the Cephes rational form below 0.625,
+// 1 - 2 / (exp(2|x|) + 1) above), operation for operation; the oracle's orc_go_tanh is the same
+// sequence.  Used by DotProduct's normMethod "pod" (dot_product_score.go:79).
+KSIM_HD double go_tanh(double x) {
+  const double P0 = -9.64399179425052238628e-1, P1 = -9.92877231001918586564e1, P2 = -1.61468768441708447952e3;
+  const double Q0 = 1.12811678491632931402e2, Q1 = 2.23548839060100448583e3, Q2 = 4.84406305325125486048e3;
+  const double kMaxLog = 8.8029691931113054295988e+01;  // log(2**127)
+  double z = x < 0 ? -x : x;
+  if (z > 0.5 * kMaxLog) return x < 0 ? -1.0 : 1.0;
+  if (z >= 0.625) {
+    const double s = go_exp(2 * z);
+    z = 1 - 2 / (s + 1);
+    return x < 0 ? -z : z;
+  }
+  if (x == 0) return x;
+  const double s = x * x;
+  return x + x * s * ((P0 * s + P1) * s + P2) / (((s + Q0) * s + Q1) * s + Q2);
+}
 
 // fgd_score.go:123 fragScore = int64(sigmoid((cur-new)/1000) * MaxNodeScore)
 KSIM_HD int fgd_frag_score(double cur, double nw) {
@@ -566,12 +585,100 @@ KSIM_HD int bestfit_score(const NodeV& n, const PodDev& p, int total) {
   return (int)s;
 }
 
-// calculateDotProductScore with merge/max (dot_product_score.go:64-100,
-// utils.go:1274-1342, resource.go:296-328, utils.go:1220-1248)
-KSIM_HD int dotprod_score(const NodeV& n, const PodDev& p, int total) {
+// DotProduct's GpuPluginCfg (config.go:3-55): dimExtMethod, normMethod; packed in ReplicaDev.dpcfg
+enum : int { DIM_MERGE = 0, DIM_SHARE = 1, DIM_DIVIDE = 2, DIM_EXTEND = 3 };
+enum : int { NORM_MAX = 0, NORM_NODE = 1, NORM_POD = 2 };
+KSIM_HD int dp_dim(int cfg) { return cfg & 15; }
+KSIM_HD int dp_norm(int cfg) { return (cfg >> 4) & 15; }
+
+// One match group of calculateDotProductScore (dot_product_score.go:70-92): node (n0, n1) and pod
+// (p0, p1) normalized by (c0, c1) (NormalizeVector, utils.go:1220-1236: / c, or 0 when c <= 0),
+// CalculateVectorDotProduct in order (utils.go:1238-1248), / len(podVec), tanh(x / 10) for "pod",
+// 1 - x; the group replaces the best when strictly larger (the first max keeps its GPU id).  The
+// extend method's pod vectors are zero except at one GPU dimension, so their dot product is
+// exactly n0 p0 + nj pj (adding +0.0 to a non-negative sum changes nothing): the same two terms.
+KSIM_HD void dp_group(double n0, double n1, double p0, double p1, double c0, double c1, int len, int norm, int gid,
+                      double* best, int* best_gid) {
+  const double a0 = c0 > 0 ? n0 / c0 : 0, a1 = c1 > 0 ? n1 / c1 : 0;
+  const double b0 = c0 > 0 ? p0 / c0 : 0, b1 = c1 > 0 ? p1 / c1 : 0;
+  double cur = 0;
+  cur += a0 * b0;
+  cur += a1 * b1;
+  if (cur == -1) return;
+  cur /= (double)len;
+  if (norm == NORM_POD) cur = go_tanh(cur / 10);
+  cur = 1 - cur;
+  if (*best < cur) {
+    *best = cur;
+    *best_gid = gid;
+  }
+}
+
+// calculateDotProductScore for every dimExtMethod / normMethod (dot_product_score.go:64-100 over
+// GenerateSchedulingMatchGroups, utils.go:1274-1342; ToVirtualNodeResourceList /
+// ToVirtualPodResourceList / ToFormalizedGpuResourceList, resource.go:217-381).  cap: the node's
+// MilliCpuCapacity (normMethod "node").  *gid: the best group's GpuId as a GPU mask (0 = "", the
+// merge method's and no group's) -- allocateGpuIdBasedOnDotProduct (:102-107).
+KSIM_HD int dotprod_cfg_score(const NodeV& n, const PodDev& p, int cap, int cfg, int* gid) {
+  const int dim = dp_dim(cfg), norm = dp_norm(cfg);
+  double best = -1;
+  *gid = 0;
+  const int cpuL = n.cpu_left, cpu = p.cpu_nz;  // MilliCpuLeft; PodResource.MilliCpu (non-zero default)
+  const int req = (int)p.milli * (int)p.num;    // podMilliGpuReq / TotalMilliGpu
+  const int cnt = n.gpu_cnt();
+  if (cpuL >= cpu) {  // ToVirtualNodeResourceList: nil when the CPU left is short
+    const int tot = n.total();
+    int idle = 0, part = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) {
+      idle += (g < cnt && n.gl(g) == kMilli) ? 1 : 0;
+      part += (g < cnt && n.gl(g) > 0 && n.gl(g) < kMilli) ? 1 : 0;
+    }
+    const int excl = req <= idle * kMilli ? exclusive_gpu_mask(n, p) : -1;  // AllocateExclusiveGpuId
+    const double c0 = norm == NORM_NODE ? (double)cap : norm == NORM_POD ? (double)cpu : (double)kMaxSpecCpu;
+    const double c1 = norm == NORM_NODE ? (double)(cnt * kMilli) : norm == NORM_POD ? (double)req : (double)kMaxSpecGpu;
+    // extend: ToFormalizedGpuResourceList = the partly used GPUs (0 < left < 1000) in index order, then
+    // one entry of all idle GPUs, and one pod vector per entry that holds the request (its length
+    // 1 + entries); share / divide: a share pod on each partly used GPU that holds it (divide: the CPU
+    // left scaled by that GPU's share of the GPU left), then the idle GPUs; merge: one group.
+    // Candidates j = 0..7 are GPU j, j = 8 the idle group (merge: j = 8 is the merged node).
+    const int len = dim == DIM_EXTEND ? 1 + part + (idle > 0 ? 1 : 0) : 2;
+#pragma unroll 1
+    for (int j = (dim == DIM_MERGE ? kMaxGpu : 0); j <= kMaxGpu; ++j) {
+      bool use;
+      int v1, g_id;
+      if (j < kMaxGpu) {
+        const int l = n.gl(j);
+        use = j < cnt && l < kMilli && l >= req && (dim == DIM_EXTEND ? l > 0 : req < kMilli);
+        v1 = l;
+        g_id = 1 << j;
+      } else if (dim == DIM_MERGE) {
+        use = true;
+        v1 = tot;
+        g_id = 0;
+      } else {
+        use = dim == DIM_EXTEND ? (idle > 0 && idle * kMilli >= req) : req <= idle * kMilli;
+        v1 = idle * kMilli;
+        g_id = excl;
+      }
+      if (!use) continue;
+      const double v0 = dim == DIM_DIVIDE ? (double)((long long)cpuL * v1) / (double)tot : (double)cpuL;
+      dp_group(v0, (double)v1, (double)cpu, (double)req, c0, c1, len, norm, g_id, &best, gid);
+    }
+  }
+  if (best == -1) {
+    *gid = 0;
+    return 0;
+  }
+  return (int)((double)100 * best);
+}
+
+// The paper's configuration (merge / max) in closed form: one match group, the same operations as
+// dotprod_cfg_score's (the fast path of the scanning kernels; tests check the two agree).
+KSIM_HD int dotprod_merge_max(const NodeV& n, const PodDev& p) {
   if (n.cpu_left < p.cpu_nz) return 0;
   const double a0 = (double)n.cpu_left / (double)kMaxSpecCpu;
-  const double a1 = (double)total / (double)kMaxSpecGpu;
+  const double a1 = (double)n.total() / (double)kMaxSpecGpu;
   const double c0 = (double)p.cpu_nz / (double)kMaxSpecCpu;
   const double c1 = (double)((int)p.milli * (int)p.num) / (double)kMaxSpecGpu;
   double cur = 0;
@@ -579,9 +686,7 @@ KSIM_HD int dotprod_score(const NodeV& n, const PodDev& p, int total) {
   cur += a1 * c1;
   cur /= (double)2;
   cur = 1 - cur;
-  double score = -1;
-  if (score < cur) score = cur;
-  return (int)((double)100 * score);
+  return (int)((double)100 * cur);
 }
 
 // getPackingScore (gpu_packing_score.go:71-117); *err on allocation failure

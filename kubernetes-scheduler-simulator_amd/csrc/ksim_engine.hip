@@ -98,9 +98,12 @@ __device__ __forceinline__ int wave_max_i(int v) {
 // allocateGpuId (open_gpu_share.go:252-283) on one node: the replica's gpuSelMethod.
 // fgd_gpu: the FGD selector's device for share pods (first max-score index), -1 if none.
 // Returns the GPU mask, 0 for pods without GPU milli, -1 where the reference panics / returns "".
+// fgd_gpu: the FGD / PWR selectors' GPU index; for SEL_DOTPROD the best match group's GPU mask
+// (dotprod_cfg_score, 0 = "": Reserve fails).
 __device__ int select_gpus(const NodeV& n, const PodDev& p, int gpusel, int fgd_gpu, uint64_t seed, int step) {
   if (p.milli <= 0) return 0;                                         // open_gpu_share.go:185-187
   if (p.milli < kMilli && p.num > 1) return -1;                       // :266-268 panic
+  if (gpusel == SEL_DOTPROD) return fgd_gpu <= 0 ? -1 : fgd_gpu;      // dot_product_score.go:102-107
   if (!is_share_pod(p)) return exclusive_gpu_mask(n, p);              // exclusive branch of every selector
   switch (gpusel) {
     case SEL_FGD:                                                     // fgd_score.go:153-156
@@ -198,18 +201,32 @@ __device__ __forceinline__ unsigned first_of_class(const NodeV& n, int milli) {
 // Per-node pieces shared by k_step (one launch per pod) and k_replay (persistent).
 // ---------------------------------------------------------------------------
 
+// The selector argument of select_gpus for a winner `n` (global node index `node`): the FGD / PWR
+// GPU index from the key, or DotProduct's best-group mask recomputed on the node.
+// kDp = false: a kernel specialised on a policy other than DotProduct (no DotProduct selector there).
+template <bool kDp = true>
+__device__ __forceinline__ int sel_arg(const ReplicaDev& rp, const NodeV& n, const PodDev& p, int node, int key_gpu) {
+  if (!kDp || rp.gpusel != SEL_DOTPROD) return key_gpu;
+  int gid = 0;
+  (void)dotprod_cfg_score(n, p, dp_norm(rp.dpcfg) == NORM_NODE ? rp.cap[node] : 0, rp.dpcfg, &gid);
+  return gid;
+}
+
 // Raw score of a feasible node under a non-FGD policy (compile-time policy, used by
 // k_replay); *err on a Score error.  Same functions and semantics as node_phase1.
+// `cap`: the node's MilliCpuCapacity (DotProduct's normMethod "node").
 template <int kPol>
 __device__ __forceinline__ int cheap_score(const NodeV& n, const PodDev& p, uint64_t seed, const uint16_t* tags,
-                                           int step, bool* err) {
+                                           int step, bool* err, int dpcfg = 0, int cap = 0) {
   *err = false;
   if constexpr (kPol == POL_BESTFIT) {
     const int r = bestfit_score(n, p, n.total());
     if (r < 0) { *err = true; return 0; }
     return r;
   } else if constexpr (kPol == POL_DOTPROD) {
-    return dotprod_score(n, p, n.total());
+    if (dpcfg == (DIM_MERGE | NORM_MAX << 4)) return dotprod_merge_max(n, p);  // uniform per replica
+    int gid = 0;
+    return dotprod_cfg_score(n, p, cap, dpcfg, &gid);
   } else if constexpr (kPol == POL_PACKING) {
     bool perr = false;
     const int r = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
@@ -244,9 +261,12 @@ __device__ __forceinline__ bool node_phase1(const NodeV& n, const PodDev& p, con
       *raw = bestfit_score(n, p, total);
       if (*raw < 0) { *err = true; *raw = 0; }
       break;
-    case POL_DOTPROD:
-      *raw = dotprod_score(n, p, total);
+    case POL_DOTPROD: {  // any dimExtMethod / normMethod; *pgpu: the best group's GPU mask
+      int gid = 0;
+      *raw = dotprod_cfg_score(n, p, rp.cap[node], rp.dpcfg, &gid);
+      if (pgpu) *pgpu = gid;
       break;
+    }
     case POL_PACKING: {
       bool perr = false;
       *raw = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
@@ -370,7 +390,7 @@ __device__ void finish_cycle(const StepArgs& a, const ReplicaDev& rp, const PodD
       } else {
         NodeRec* nr = rp.nodes + node;
         const NodeV wn = load_node(nr);
-        const int mask = select_gpus(wn, p, rp.gpusel, key_gpu(best), rp.seed, step);
+        const int mask = select_gpus(wn, p, rp.gpusel, sel_arg(rp, wn, p, node, key_gpu(best)), rp.seed, step);
         if (mask < 0) {
           out.status = ST_ERROR;  // Reserve failed: allocateGpuId returned "" / panicked
           out.score = 0;
@@ -476,7 +496,9 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs a, const TypDev* __res
     if (tid < nb) {
       a.out_feas[n0 + tid] = feas ? 1 : 0;
       a.out_score[n0 + tid] = feas ? (pwr ? praw : raw) : 0;
-      a.out_gpu[n0 + tid] = feas ? select_gpus(n, p, rp.gpusel, rp.gpusel == SEL_PWR ? pgpu : gpu, rp.seed, step) : 0;
+      a.out_gpu[n0 + tid] =
+          feas ? select_gpus(n, p, rp.gpusel, (rp.gpusel == SEL_PWR || rp.gpusel == SEL_DOTPROD) ? pgpu : gpu, rp.seed, step)
+               : 0;
     }
     return;
   }
@@ -1156,7 +1178,10 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         if (tid < cn) {
           n = load_node(&s_nodes[i]);
           feas = filter_node(n, p);
-          if (feas) raw = cheap_score<kPol>(n, p, rp.seed, &s_tags[(size_t)i * kTagStride], step, &e1);
+          if (feas) {
+            const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[n_lo + (i == ns ? vb : i)] : 0;
+            raw = cheap_score<kPol>(n, p, rp.seed, &s_tags[(size_t)i * kTagStride], step, &e1, rp.dpcfg, cap);
+          }
         }
         const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, -1, i == ns ? vb : i) : 0ull;
         route(tid < cn, i, feas, e1, raw, k);
@@ -1233,7 +1258,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         int mask = -1;
         if (mk != 0ull) {
           NodeV bn = load_node(&s_nodes[mloc]);
-          mask = select_gpus(bn, p, rp.gpusel, key_gpu(mk), rp.seed, step);
+          mask = select_gpus(bn, p, rp.gpusel, sel_arg<kPol == POL_DOTPROD>(rp, bn, p, n_lo + mloc, key_gpu(mk)), rp.seed,
+                             step);
           if (mask >= 0) bind_node(bn, p, mask, +1);
           if (lane == 0) store_node(&s_nodes[ns], bn);
           else if (lane >= 2 && lane < 6) {
@@ -1303,7 +1329,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         int mask = -1;
         if (mk != 0ull) {
           NodeV bn = load_node(&s_nodes[mloc]);
-          mask = select_gpus(bn, p, rp.gpusel, key_gpu(mk), rp.seed, step);
+          mask = select_gpus(bn, p, rp.gpusel, sel_arg<kPol == POL_DOTPROD>(rp, bn, p, n_lo + mloc, key_gpu(mk)), rp.seed,
+                             step);
           if (mask >= 0) bind_node(bn, p, mask, +1);
           if (lane == 0) store_node(&s_nodes[ns], bn);
           else if (lane >= 2 && lane < 6) {
@@ -1431,7 +1458,7 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
     (void)pwr_score(n, p, rp.cap[node], rp.cpum[node], *rp.pw, &fgd_gpu, &perr);
     if (perr) fgd_gpu = -1;
   }
-  const int mask = select_gpus(n, p, rp.gpusel, fgd_gpu, rp.seed, step);
+  const int mask = select_gpus(n, p, rp.gpusel, sel_arg(rp, n, p, node, fgd_gpu), rp.seed, step);
   *out_mask = mask;
   if (mask >= 0) apply_bind(nr, tg, p, mask, +1);
 }
@@ -2543,9 +2570,11 @@ int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp,
 int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, uint64_t seed) {
   if (e) e->mplan_dirty = true;
   if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
-  if (policy < POL_FGD || policy > POL_PWR_FGD || gpusel < SEL_BEST || gpusel > SEL_PWR) return KSIM_ENOTSUP;
-  // allocateGpuIdFunc only holds the selectors of the enabled plugins (fgd_score.go:37, pwr_score.go:40)
+  if (policy < POL_FGD || policy > POL_PWR_FGD || gpusel < SEL_BEST || gpusel > SEL_DOTPROD) return KSIM_ENOTSUP;
+  // allocateGpuIdFunc only holds the selectors of the enabled plugins (fgd_score.go:37, pwr_score.go:40,
+  // dot_product_score.go:37)
   if (gpusel == SEL_PWR && !is_pwr_policy(policy)) return KSIM_ENOTSUP;
+  if (gpusel == SEL_DOTPROD && policy != POL_DOTPROD) return KSIM_ENOTSUP;
   if (policy == POL_PWR_FGD && e->reps[replica].policy != POL_PWR_FGD) {
     e->reps[replica].w_pwr = 500;  // "PWR 500 FGD 500" (generate_run_scripts.py:40) until set_weights
     e->reps[replica].w_fgd = 500;
@@ -2556,6 +2585,17 @@ int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, 
   e->reps[replica].policy = policy;
   e->reps[replica].gpusel = gpusel;
   e->reps[replica].seed = seed;
+  KSIM_HIP(hipSetDevice(e->device));
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_set_plugin_cfg(ksim_engine* e, int replica, int dim_ext, int norm) {
+  if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  if (dim_ext < DIM_MERGE || dim_ext > DIM_EXTEND || norm < NORM_MAX || norm > NORM_POD) return KSIM_ENOTSUP;
+  e->reps[replica].dpcfg = dim_ext | norm << 4;
   KSIM_HIP(hipSetDevice(e->device));
   int rc = upload_reps(e);
   if (rc) return rc;

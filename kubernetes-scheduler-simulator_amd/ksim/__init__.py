@@ -30,7 +30,10 @@ NUM_TAGS = 9
 
 POLICY = {"FGD": 0, "BestFit": 1, "DotProd": 2, "GpuPacking": 3, "GpuClustering": 4, "Random": 5,
           "PWR": 6, "PWR+FGD": 7}
-GPUSEL = {"best": 0, "worst": 1, "random": 2, "FGD": 3, "PWR": 4}
+GPUSEL = {"best": 0, "worst": 1, "random": 2, "FGD": 3, "PWR": 4, "DotProd": 5}
+# DotProduct's GpuPluginCfg (pkg/type/config.go:3-55)
+DIM_EXT = {"merge": 0, "share": 1, "divide": 2, "extend": 3}
+NORM = {"max": 0, "node": 1, "pod": 2}
 # experiments/run_scripts/expected_run_scripts_0511.sh and generate_run_scripts.py:31-42:
 # policy -> gpuSelMethod
 DEFAULT_GPUSEL = {"FGD": "FGD", "BestFit": "best", "DotProd": "best", "GpuPacking": "best",
@@ -160,6 +163,7 @@ SIGNATURES = {
     "ksim_shard_comm_id": (C.c_int, [_P(C.c_uint8)]),
     "ksim_engine_set_shard": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _P(C.c_uint8)]),
     "ksim_shard_group_run": (C.c_int, [_P(_VP), C.c_int]),
+    "ksim_engine_set_plugin_cfg": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
     "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
     "ksim_trace_free": (None, [_VP]),
@@ -352,13 +356,23 @@ class Engine:
     def set_typical(self, r, tp, n):
         check(lib().ksim_engine_set_typical(self.h, r, tp, n), "set_typical")
 
-    def set_policy(self, r, policy="FGD", gpusel=None, seed=0):
-        """policy: a POLICY key or a generate_run_scripts.py string such as "PWR 500 FGD 500"."""
+    def set_policy(self, r, policy="FGD", gpusel=None, seed=0, dim_ext=None, norm=None):
+        """policy: a POLICY key or a generate_run_scripts.py string such as "PWR 500 FGD 500".
+        DotProd: dim_ext / norm as generate_config_and_run.py's -dimext / -norm (default merge / max,
+        the paper's); like that script, a dim_ext other than merge selects GPUs with the DotProduct
+        selector ("DotProd") unless gpusel says otherwise."""
         policy, weights = parse_policy(policy)
+        if policy == "DotProd" and dim_ext not in (None, "merge") and gpusel is None:
+            gpusel = "DotProd"  # generate_config_and_run.py:271-275
         gs = gpusel or DEFAULT_GPUSEL[policy]
         check(lib().ksim_engine_set_policy(self.h, r, POLICY[policy], GPUSEL[gs], seed), "set_policy")
         if weights:
             self.set_weights(r, *weights)
+        if policy == "DotProd" or dim_ext is not None or norm is not None:
+            self.set_plugin_cfg(r, dim_ext or "merge", norm or "max")
+
+    def set_plugin_cfg(self, r, dim_ext="merge", norm="max"):
+        check(lib().ksim_engine_set_plugin_cfg(self.h, r, DIM_EXT[dim_ext], NORM[norm]), "set_plugin_cfg")
 
     def set_weights(self, r, w_pwr, w_fgd):
         check(lib().ksim_engine_set_weights(self.h, r, w_pwr, w_fgd), "set_weights")

@@ -478,27 +478,176 @@ int64_t orc_best_fit_score(const orc_node_resource* n, const orc_pod_resource* p
     return (int64_t)score;
 }
 
-/* dot_product_score.go:64-100 with GenerateSchedulingMatchGroups(merge, max)
- * (utils.go:1274-1342, resource.go:246-381, utils.go:1220-1248) */
-int64_t orc_dot_product_score(const orc_node_resource* n, const orc_pod_resource* p) {
-    double score = -1;
-    /* ToVirtualNodeResourceList(merge): nil when cpu left < request */
-    if (n->milli_cpu_left < p->milli_cpu) return 0;
-    double nodeVec[2] = {(double)n->milli_cpu_left, (double)orc_get_gpu_milli_left_total(n)};
-    double podVec[2] = {(double)p->milli_cpu, (double)(p->milli_gpu * (int64_t)p->gpu_number)};
-    double maxCap[2] = {(double)ORC_MAX_SPEC_CPU, (double)ORC_MAX_SPEC_GPU};
-    for (int i = 0; i < 2; i++) {
-        nodeVec[i] = maxCap[i] > 0 ? nodeVec[i] / maxCap[i] : 0;
-        podVec[i] = maxCap[i] > 0 ? podVec[i] / maxCap[i] : 0;
+/* Go math.Tanh, portable algorithm (src/math/tanh.go) */
+double orc_go_tanh(double x) {
+    static const double P[3] = {-9.64399179425052238628e-1, -9.92877231001918586564e1, -1.61468768441708447952e3};
+    static const double Q[3] = {1.12811678491632931402e2, 2.23548839060100448583e3, 4.84406305325125486048e3};
+    const double MAXLOG = 8.8029691931113054295988e+01; /* log(2**127) */
+    double z = fabs(x);
+    if (z > 0.5 * MAXLOG) return x < 0 ? -1 : 1;
+    if (z >= 0.625) {
+        double e = orc_go_exp(2 * z);
+        z = 1 - 2 / (e + 1);
+        if (x < 0) z = -z;
+        return z;
     }
-    double cur = 0;
-    for (int i = 0; i < 2; i++) cur += nodeVec[i] * podVec[i];
-    if (cur == -1) return 0;
-    cur /= (double)2;
-    cur = 1 - cur;
-    if (score < cur) score = cur;
-    if (score == -1) return 0;
+    if (x == 0) return x;
+    double s = x * x;
+    return x + x * s * ((P[0] * s + P[1]) * s + P[2]) / (((s + Q[0]) * s + Q[1]) * s + Q[2]);
+}
+
+/* A virtual node / pod resource of GenerateSchedulingMatchGroups: a vector and a GPU id (bitmask;
+ * 0 = "", -1 = "" from a panicking AllocateExclusiveGpuId, which the callers never reach). */
+typedef struct { double v[ORC_MAX_GPU_LIST + 1]; int len; int gid; } orc_vres;
+
+/* resource.go:217-244 ToFormalizedGpuResourceList: partly used GPUs in index order, then all idle ones */
+static int formalized_gpus(const orc_node_resource* n, int64_t* left, int* ids) {
+    int k = 0, idle = 0, idle_ids = 0;
+    for (int id = 0; id < n->n_gpu_left; id++) {
+        int64_t l = n->milli_gpu_left[id];
+        if (l == ORC_MILLI) { idle++; idle_ids |= 1 << id; }
+        else if (l > 0) { left[k] = l; ids[k] = 1 << id; k++; }
+    }
+    if (idle > 0) { left[k] = (int64_t)idle * ORC_MILLI; ids[k] = idle_ids; k++; }
+    return k;
+}
+
+static int fully_free(const orc_node_resource* n) {
+    int c = 0;
+    for (int id = 0; id < n->n_gpu_left; id++) c += n->milli_gpu_left[id] == ORC_MILLI;
+    return c;
+}
+
+/* resource.go:296-381 ToVirtualNodeResourceList */
+static int virtual_nodes(const orc_node_resource* n, const orc_pod_resource* p, int dim, orc_vres* out) {
+    if (n->milli_cpu_left < p->milli_cpu) return 0;
+    int64_t req = p->milli_gpu * (int64_t)p->gpu_number;
+    int64_t tot = orc_get_gpu_milli_left_total(n);
+    int c = 0;
+    if (dim == ORC_DIM_MERGE) {
+        out[0].v[0] = (double)n->milli_cpu_left;
+        out[0].v[1] = (double)tot;
+        out[0].len = 2;
+        out[0].gid = 0;
+        return 1;
+    }
+    if (dim == ORC_DIM_SHARE || dim == ORC_DIM_DIVIDE) {
+        if (req < ORC_MILLI) {
+            for (int id = 0; id < n->n_gpu_left; id++) {
+                int64_t l = n->milli_gpu_left[id];
+                if (l >= ORC_MILLI) continue;
+                if (l < req) continue;
+                out[c].v[0] = dim == ORC_DIM_SHARE ? (double)n->milli_cpu_left
+                                                   : (double)(n->milli_cpu_left * l) / (double)tot;
+                out[c].v[1] = (double)l;
+                out[c].len = 2;
+                out[c].gid = 1 << id;
+                c++;
+            }
+        }
+        int idle = fully_free(n);
+        if (req <= (int64_t)idle * ORC_MILLI) {
+            out[c].gid = orc_allocate_exclusive_gpu_id(n, p);
+            out[c].v[0] = dim == ORC_DIM_SHARE ? (double)n->milli_cpu_left
+                                               : (double)(n->milli_cpu_left * (int64_t)(idle * ORC_MILLI)) / (double)tot;
+            out[c].v[1] = (double)(idle * ORC_MILLI);
+            out[c].len = 2;
+            c++;
+        }
+        return c;
+    }
+    /* extend */
+    int64_t left[ORC_MAX_GPU_LIST + 1];
+    int ids[ORC_MAX_GPU_LIST + 1];
+    int k = formalized_gpus(n, left, ids);
+    out[0].v[0] = (double)n->milli_cpu_left;
+    for (int i = 0; i < k; i++) out[0].v[1 + i] = (double)left[i];
+    out[0].len = 1 + k;
+    out[0].gid = 0;
+    return 1;
+}
+
+/* resource.go:246-294 ToVirtualPodResourceList */
+static int virtual_pods(const orc_pod_resource* p, int dim, const orc_node_resource* n, orc_vres* out) {
+    int64_t req = p->milli_gpu * (int64_t)p->gpu_number;
+    if (dim != ORC_DIM_EXTEND) {
+        out[0].v[0] = (double)p->milli_cpu;
+        out[0].v[1] = (double)req;
+        out[0].len = 2;
+        out[0].gid = 0;
+        return 1;
+    }
+    int64_t left[ORC_MAX_GPU_LIST + 1];
+    int ids[ORC_MAX_GPU_LIST + 1];
+    int k = formalized_gpus(n, left, ids), c = 0;
+    for (int i = 0; i < k; i++) {
+        if (left[i] < req) continue;
+        out[c].v[0] = (double)p->milli_cpu;
+        for (int j = 0; j < k; j++) out[c].v[1 + j] = j == i ? (double)req : 0;
+        out[c].len = 1 + k;
+        out[c].gid = left[i] < ORC_MILLI ? ids[i] : orc_allocate_exclusive_gpu_id(n, p);
+        c++;
+    }
+    return c;
+}
+
+/* utils.go:1220-1236 NormalizeVector (in place) */
+void orc_normalize_vector(double* v, int len, const double* nv, int nlen) {
+    if (nlen == 0 || len == 0 || nlen != len) return;
+    for (int i = 0; i < len; i++) v[i] = nv[i] > 0 ? v[i] / nv[i] : 0;
+}
+
+/* utils.go:1238-1248 CalculateVectorDotProduct */
+double orc_vector_dot_product(const double* a, int la, const double* b, int lb) {
+    if (la == 0 || lb == 0 || la != lb) return -1;
+    double ip = 0;
+    for (int i = 0; i < la; i++) ip += a[i] * b[i];
+    return ip;
+}
+
+/* dot_product_score.go:64-100 calculateDotProductScore over GenerateSchedulingMatchGroups
+ * (utils.go:1274-1342); *gid: the best group's GpuId (bitmask, 0 = "") */
+int64_t orc_dot_product_score_cfg(const orc_node_resource* n, const orc_pod_resource* p, int dim, int norm,
+                                  int* gid) {
+    orc_vres vn[ORC_MAX_GPU_LIST + 2], vp[ORC_MAX_GPU_LIST + 2];
+    int nn = virtual_nodes(n, p, dim, vn);
+    int np = virtual_pods(p, dim, n, vp);
+    double score = -1;
+    *gid = 0;
+    for (int a = 0; a < nn; a++) {
+        for (int b = 0; b < np; b++) {
+            double nv[ORC_MAX_GPU_LIST + 1], pv[ORC_MAX_GPU_LIST + 1];
+            memcpy(nv, vn[a].v, sizeof nv);
+            memcpy(pv, vp[b].v, sizeof pv);
+            int ln = vn[a].len, lp = vp[b].len;
+            int g = 0;
+            if (dim == ORC_DIM_SHARE || dim == ORC_DIM_DIVIDE) g = vn[a].gid;
+            else if (dim == ORC_DIM_EXTEND) g = vp[b].gid;
+            double cv[ORC_MAX_GPU_LIST + 1];
+            int lc = dim == ORC_DIM_EXTEND ? ln : 2;
+            double c0, cg;
+            if (norm == ORC_NORM_NODE) { c0 = (double)n->milli_cpu_capacity; cg = (double)(n->gpu_number * ORC_MILLI); }
+            else if (norm == ORC_NORM_POD) { c0 = (double)p->milli_cpu; cg = (double)(p->milli_gpu * (int64_t)p->gpu_number); }
+            else { c0 = (double)ORC_MAX_SPEC_CPU; cg = (double)ORC_MAX_SPEC_GPU; }
+            cv[0] = c0;
+            for (int i = 1; i < lc; i++) cv[i] = cg;
+            orc_normalize_vector(nv, ln, cv, lc);
+            orc_normalize_vector(pv, lp, cv, lc);
+            double cur = orc_vector_dot_product(nv, ln, pv, lp);
+            if (cur == -1) continue;
+            cur /= (double)lp;
+            if (norm == ORC_NORM_POD) cur = orc_go_tanh(cur / 10);
+            cur = 1 - cur;
+            if (score < cur) { score = cur; *gid = g; }
+        }
+    }
+    if (score == -1) { *gid = 0; return 0; }
     return (int64_t)((double)100 * score);
+}
+
+int64_t orc_dot_product_score(const orc_node_resource* n, const orc_pod_resource* p) {
+    int g = 0;
+    return orc_dot_product_score_cfg(n, p, ORC_DIM_MERGE, ORC_NORM_MAX, &g);
 }
 
 /* gpu_packing_score.go:71-117 getPackingScore */
@@ -886,8 +1035,12 @@ static int64_t score_one(const work_t* w, int i, int32_t* gm, int32_t* err) {
         if (s == -1) { *err = 1; return 0; }
         return s;
     }
-    case ORC_POL_DOTPROD:
-        return orc_dot_product_score(&nr, &pr);
+    case ORC_POL_DOTPROD: {
+        int g = 0;
+        int64_t sc = orc_dot_product_score_cfg(&nr, &pr, w->pol.dim_ext, w->pol.norm, &g);
+        *gm = g;
+        return sc;
+    }
     case ORC_POL_PACKING: {
         if (w->e->gpu_milli <= 0) return 0;
         if (!accessible) { *err = 1; return 0; }
@@ -1106,6 +1259,13 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                         break;
                     }
                     case ORC_SEL_WORST: mask = alloc_gpu_worst_fit(&nr, &pr); break;
+                    case ORC_SEL_DOTPROD: { /* dot_product_score.go:102-107 allocateGpuIdBasedOnDotProduct */
+                        if (pr.milli_gpu < ORC_MILLI && pr.gpu_number > 1) { mask = -1; break; } /* :266-268 panic */
+                        int g = 0;
+                        (void)orc_dot_product_score_cfg(&nr, &pr, pol.dim_ext, pol.norm, &g);
+                        mask = g <= 0 ? -1 : g;
+                        break;
+                    }
                     case ORC_SEL_RANDOM:
                         if (pr.milli_gpu < ORC_MILLI) {
                             uint64_t nk = rand_node_key(pol.seed, s, rank[winner]);

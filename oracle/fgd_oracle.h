@@ -122,6 +122,13 @@ int64_t orc_fgd_score(const orc_node_resource* n, const orc_pod_resource* p, con
                       int* gpu_mask);
 int64_t orc_best_fit_score(const orc_node_resource* n, const orc_pod_resource* p);      /* -1 = error */
 int64_t orc_dot_product_score(const orc_node_resource* n, const orc_pod_resource* p);   /* merge/max */
+/* dimExtMethod / normMethod (config.go:3-55); *gid = the best match group's GpuId as a bitmask */
+enum { ORC_DIM_MERGE = 0, ORC_DIM_SHARE = 1, ORC_DIM_DIVIDE = 2, ORC_DIM_EXTEND = 3 };
+enum { ORC_NORM_MAX = 0, ORC_NORM_NODE = 1, ORC_NORM_POD = 2 };
+int64_t orc_dot_product_score_cfg(const orc_node_resource* n, const orc_pod_resource* p, int dim, int norm, int* gid);
+double  orc_vector_dot_product(const double* a, int la, const double* b, int lb);
+void    orc_normalize_vector(double* v, int len, const double* nv, int nlen);
+double  orc_go_tanh(double x);
 int64_t orc_packing_score(const orc_node_resource* n, const orc_pod_resource* p, int* err);
 int64_t orc_clustering_score(const orc_node_resource* n, const orc_pod_resource* p, int pod_tag,
                              const int32_t* node_tag_counts);
@@ -158,7 +165,7 @@ enum { ORC_POL_FGD = 0, ORC_POL_BESTFIT = 1, ORC_POL_DOTPROD = 2, ORC_POL_PACKIN
        ORC_POL_CLUSTERING = 4, ORC_POL_RANDOM = 5,
        ORC_POL_PWR = 6,       /* PWRScore alone */
        ORC_POL_PWR_FGD = 7 }; /* PWRScore + FGDScore, weights orc_policy.w_pwr / w_fgd */
-enum { ORC_SEL_BEST = 0, ORC_SEL_WORST = 1, ORC_SEL_RANDOM = 2, ORC_SEL_FGD = 3, ORC_SEL_PWR = 4 };
+enum { ORC_SEL_BEST = 0, ORC_SEL_WORST = 1, ORC_SEL_RANDOM = 2, ORC_SEL_FGD = 3, ORC_SEL_PWR = 4, ORC_SEL_DOTPROD = 5 };
 
 typedef struct {
     char    name[64];              /* full node name, e.g. "0042-openb-node-0001" (tie-break key) */
@@ -203,6 +210,7 @@ typedef struct {
     uint64_t seed;                 /* Random policy: see DESIGN.md "Random contract" */
     int32_t threads;               /* >1: parallelize.Until-style worker fan-out over nodes */
     int32_t w_pwr, w_fgd;          /* ORC_POL_PWR_FGD plugin weights (scheduler config score weights) */
+    int32_t dim_ext, norm;         /* ORC_POL_DOTPROD GpuPluginCfg (ORC_DIM_*, ORC_NORM_*) */
 } orc_policy;
 
 /* Replays n events on a fresh cluster.  results[n]; reports[n] may be NULL. */

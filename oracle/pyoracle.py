@@ -13,7 +13,9 @@ _LIB = None
 MILLI = 1000
 Q1, Q2, Q3, Q4, XL, XR, NA = range(7)
 POL_FGD, POL_BESTFIT, POL_DOTPROD, POL_PACKING, POL_CLUSTERING, POL_RANDOM, POL_PWR, POL_PWR_FGD = range(8)
-SEL_BEST, SEL_WORST, SEL_RANDOM, SEL_FGD, SEL_PWR = range(5)
+SEL_BEST, SEL_WORST, SEL_RANDOM, SEL_FGD, SEL_PWR, SEL_DOTPROD = range(6)
+DIM_MERGE, DIM_SHARE, DIM_DIVIDE, DIM_EXTEND = range(4)
+NORM_MAX, NORM_NODE, NORM_POD = range(3)
 TYPE_LEN = 64
 MAX_GPU_LIST = 16
 
@@ -68,7 +70,7 @@ class Report(C.Structure):
 
 class Policy(C.Structure):
     _fields_ = [("policy", C.c_int32), ("gpu_sel", C.c_int32), ("seed", C.c_uint64), ("threads", C.c_int32),
-                ("w_pwr", C.c_int32), ("w_fgd", C.c_int32)]
+                ("w_pwr", C.c_int32), ("w_fgd", C.c_int32), ("dim_ext", C.c_int32), ("norm", C.c_int32)]
 
 
 class NodeState(C.Structure):
@@ -112,6 +114,14 @@ def lib():
         L.orc_best_fit_score.restype = C.c_int64
         L.orc_dot_product_score.argtypes = [P(NodeResource), P(PodResource)]
         L.orc_dot_product_score.restype = C.c_int64
+        L.orc_dot_product_score_cfg.argtypes = [P(NodeResource), P(PodResource), C.c_int, C.c_int, P(C.c_int)]
+        L.orc_dot_product_score_cfg.restype = C.c_int64
+        L.orc_vector_dot_product.argtypes = [P(C.c_double), C.c_int, P(C.c_double), C.c_int]
+        L.orc_vector_dot_product.restype = C.c_double
+        L.orc_normalize_vector.argtypes = [P(C.c_double), C.c_int, P(C.c_double), C.c_int]
+        L.orc_normalize_vector.restype = None
+        L.orc_go_tanh.argtypes = [C.c_double]
+        L.orc_go_tanh.restype = C.c_double
         L.orc_packing_score.argtypes = [P(NodeResource), P(PodResource), P(C.c_int)]
         L.orc_packing_score.restype = C.c_int64
         L.orc_clustering_score.argtypes = [P(NodeResource), P(PodResource), C.c_int, P(C.c_int32)]
@@ -152,6 +162,32 @@ def energy_node(node):
     c, g = C.c_double(0), C.c_double(0)
     rc = lib().orc_energy_node(C.byref(node), C.byref(c), C.byref(g))
     return rc, c.value, g.value
+
+
+def dot_product_score(node, pod, dim_ext=DIM_MERGE, norm=NORM_MAX):
+    """calculateDotProductScore: (score, best group's GPU mask)."""
+    g = C.c_int(0)
+    s = lib().orc_dot_product_score_cfg(C.byref(node), C.byref(pod), dim_ext, norm, C.byref(g))
+    return s, g.value
+
+
+def vector_dot_product(a, b):
+    """utils.go:1238-1248 CalculateVectorDotProduct."""
+    x = (C.c_double * max(1, len(a)))(*a)
+    y = (C.c_double * max(1, len(b)))(*b)
+    return lib().orc_vector_dot_product(x, len(a), y, len(b))
+
+
+def normalize_vector(v, nv):
+    """utils.go:1220-1236 NormalizeVector."""
+    x = (C.c_double * max(1, len(v)))(*v)
+    y = (C.c_double * max(1, len(nv)))(*nv)
+    lib().orc_normalize_vector(x, len(v), y, len(nv))
+    return list(x)[:len(v)]
+
+
+def go_tanh(x):
+    return lib().orc_go_tanh(x)
 
 
 def pwr_score(node, pod):
@@ -230,7 +266,7 @@ def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_w
 
 
 def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
-               with_report=False, w_pwr=0, w_fgd=0):
+               with_report=False, w_pwr=0, w_fgd=0, dim_ext=DIM_MERGE, norm=NORM_MAX):
     """nodes: list of dicts {name,cpu,mem,pods,gpu,model}; events: list of dicts
     {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]"""
     nn = len(nodes)
@@ -252,7 +288,7 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
     res = (Result * max(1, ne))()
     rep = (Report * max(1, ne))() if with_report else None
     st = (NodeState * nn)()
-    pol = Policy(policy, gpu_sel, seed, threads, w_pwr, w_fgd)
+    pol = Policy(policy, gpu_sel, seed, threads, w_pwr, w_fgd, dim_ext, norm)
     rc = lib().orc_run_events_state(ns, nn, tp, nt, pol, ev, ne, res, rep, st)
     assert rc == 0
     results = [(res[i].node, res[i].gpu_mask, res[i].score, res[i].n_feasible, res[i].status) for i in range(ne)]

@@ -10,6 +10,8 @@ Sources (reference tree Fr4nz83/kubernetes-scheduler-simulator @ 2024_08_07):
   pkg/utils/frag_test.go:165-185  TestGetGpuFragMilliByNodeResAndPodRes
   pkg/simulator/plugin/gpu_packing_score_test.go:9-35  TestGpuPackingScorePlugin_Score
   pkg/type/resource_test.go:9-41  Flatten / Add / Sub / Copy
+  pkg/utils/utils_test.go:25-55   TestCalculateVectorDotProduct (NormalizeVector + CalculateVectorDotProduct
+                                  of nodeRes.ToResourceVec / podRes.ToResourceVec; InDelta 1e-3)
 
 Percentages are Go untyped-constant expressions such as `9.33 / 100`; Go evaluates
 them exactly and rounds once, so they are stored as [numerator, denominator]
@@ -116,6 +118,15 @@ DATA = {
         dict(node=node("Hello", 1000, [200, 0, 0, 500], 4, "1080", 96000),
              pod=dict(cpu=100, milli=1000, num=2, type="1080"), idl=[1, 2],
              want_cpu_left=1100, want_gpu_left=[200, 1000, 1000, 500]),
+    ],
+    # utils_test.go:25-55: node [MilliCpuLeft, total GPU milli left], pod [MilliCpu, MilliGpu * GpuNumber],
+    # both normalized by cap, dot product within 1e-3 of want (the Go test's assert.InDelta)
+    "dot_product_cases": [
+        dict(node_vec=[1000, 200 + 600 + 350 + 0], pod_vec=[500, 500], cap=[2000, 4000], want=0.1609375),
+        dict(node_vec=[1000, 1000 + 150], pod_vec=[500, 500], cap=[2000, 4000], want=0.1609375),
+        dict(node_vec=[500, 500 + 75], pod_vec=[500, 500], cap=[2000, 4000], want=0.08046875),
+        dict(node_vec=[0, 2000], pod_vec=[1000, 20], cap=[2000, 2000], want=0.01),
+        dict(node_vec=[8000, 1000], pod_vec=[4000, 1000], cap=[8000, 1000], want=1.5),
     ],
     "sub_cases": [
         dict(node=node("Hello", 1000, [200, 1000, 1000, 500], 4, "1080", 96000),

@@ -10,6 +10,7 @@ using namespace ksim;
 extern "C" {
 
 double dm_go_exp(double x) { return go_exp(x); }
+double dm_go_tanh(double x) { return go_tanh(x); }
 
 // FGD score from delta = cur - new: direct, and through the threshold table k_memo uses
 int dm_score_of_delta(double delta) { return fgd_score_of_delta(delta); }
@@ -147,9 +148,12 @@ int dm_bestfit(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, in
   const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, 0, 1);
   return bestfit_score(n, pod(cpu, milli, num, ~0u), n.total());
 }
-int dm_dotprod(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num) {
+int dm_dotprod_mm(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num) {
+  return dotprod_merge_max(mk(cpu_left, 0, gl8, gpu_cnt, 0, 1), pod(cpu, milli, num, ~0u));
+}
+int dm_dotprod(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num, int cap, int cfg, int* gid) {
   const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, 0, 1);
-  return dotprod_score(n, pod(cpu, milli, num, ~0u), n.total());
+  return dotprod_cfg_score(n, pod(cpu, milli, num, ~0u), cap, cfg, gid);
 }
 int dm_packing(const int* gl8, int gpu_cnt, int cpu, int milli, int num, int* err) {
   bool e = false;

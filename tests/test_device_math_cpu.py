@@ -32,7 +32,10 @@ def dm():
     L.dm_filter.argtypes = [C.c_int, C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                             C.c_uint]
     L.dm_bestfit.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
-    L.dm_dotprod.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.dm_dotprod.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+    L.dm_dotprod_mm.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.dm_go_tanh.argtypes = [C.c_double]
+    L.dm_go_tanh.restype = C.c_double
     L.dm_packing.argtypes = [I8, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
     L.dm_clustering.argtypes = [C.c_int * 9, I8, C.c_int, C.c_int, C.c_int]
     L.dm_exclusive.argtypes = [I8, C.c_int, C.c_int, C.c_int]
@@ -124,8 +127,10 @@ def test_cheap_scores_and_exclusive_fuzz(dm):
         pr = O.pod_res(cpu, milli, num, "")
         g8 = (C.c_int * 8)(*gl)
         assert dm.dm_bestfit(cpu_left, g8, cnt, cpu, milli, num) == L.orc_best_fit_score(C.byref(node), C.byref(pr))
-        assert dm.dm_dotprod(cpu_left, g8, cnt, cpu, milli, num) == L.orc_dot_product_score(C.byref(node),
-                                                                                              C.byref(pr))
+        g = C.c_int(0)
+        want = L.orc_dot_product_score(C.byref(node), C.byref(pr))
+        assert dm.dm_dotprod(cpu_left, g8, cnt, cpu, milli, num, 128000, 0, C.byref(g)) == want
+        assert dm.dm_dotprod_mm(cpu_left, g8, cnt, cpu, milli, num) == want
         if milli > 0:
             e1, e2 = C.c_int(0), C.c_int(0)
             a = dm.dm_packing(g8, cnt, cpu, milli, num, C.byref(e1))
@@ -202,3 +207,35 @@ def test_fgd_score_threshold_table(dm):
         sig = 1.0 / (1.0 + L.orc_go_exp(-(x / 1000)))
         assert s == int(sig * 100)
     assert [direct(th[k]) for k in range(1, 101)] == list(range(1, 101))
+
+
+@pytest.mark.parametrize("dim", [O.DIM_MERGE, O.DIM_SHARE, O.DIM_DIVIDE, O.DIM_EXTEND])
+@pytest.mark.parametrize("norm", [O.NORM_MAX, O.NORM_NODE, O.NORM_POD])
+def test_dotprod_variants_fuzz(dm, dim, norm):
+    # every dimExtMethod x normMethod: the device's single-loop restatement against the oracle's
+    # literal GenerateSchedulingMatchGroups lists -- the score and the best group's GPU id
+    rnd = random.Random(100 + 4 * norm + dim)
+    for _ in range(6000):
+        cnt = rnd.choice([0, 1, 2, 4, 6, 8])
+        gl = rand_gl(rnd, cnt) if cnt else [0] * 8
+        cpu_left = rnd.choice([0, 100, 2000, 8000, 32000, 64000, 96000])
+        cap = rnd.choice([cpu_left, 96000, 128000])
+        cpu, milli, num = rand_pod(rnd)
+        cpu = max(cpu, 100)  # PodResource.MilliCpu carries the non-zero default
+        node = O.node_res(cpu_left, gl[:cnt], cnt, "G2", cap)
+        pr = O.pod_res(cpu, milli, num, "")
+        g = C.c_int(0)
+        s = dm.dm_dotprod(cpu_left, (C.c_int * 8)(*gl), cnt, cpu, milli, num, cap, dim | norm << 4, C.byref(g))
+        ws, wg = O.dot_product_score(node, pr, dim, norm)
+        assert (s, g.value) == (ws, wg), (cpu_left, gl[:cnt], cap, cpu, milli, num)
+
+
+def test_go_tanh_host_equals_oracle(dm):
+    rnd = random.Random(5)
+    xs = [0.0, -0.0, 1e-300, 0.1, 0.5, 0.6249999, 0.625, 0.7, 1.0, 2.0, 10.0, 44.0, 44.02, 45.0, 300.0]
+    xs += [rnd.uniform(-3, 3) for _ in range(4000)] + [rnd.uniform(0, 0.3) for _ in range(2000)]
+    for x in xs + [-x for x in xs]:
+        a, b = dm.dm_go_tanh(x), O.go_tanh(x)
+        assert a == b or (a != a and b != b), x
+    # Go's tanh: exact at 0 and saturated beyond 0.5 * log(2**127)
+    assert O.go_tanh(50.0) == 1.0 and O.go_tanh(-50.0) == -1.0

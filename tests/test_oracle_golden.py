@@ -157,3 +157,32 @@ def test_oracle_rejects_bad_deletions():
         with pytest.raises(AssertionError):
             O.run_events(nodes, tp, evs)
     O.run_events(nodes, tp, [pod, dict(pod, delete=1, ref=0)])  # a valid stream runs
+
+
+@pytest.mark.parametrize("case", GOLD["dot_product_cases"])
+def test_dot_product_vectors(case):
+    # utils_test.go:25-55: NormalizeVector then CalculateVectorDotProduct, InDelta 1e-3 as the Go test
+    nv = O.normalize_vector(case["node_vec"], case["cap"])
+    pv = O.normalize_vector(case["pod_vec"], case["cap"])
+    assert abs(O.vector_dot_product(nv, pv) - case["want"]) <= 1e-3
+
+
+def test_dot_product_vector_edges():
+    # CalculateVectorDotProduct: -1 on empty or unequal vectors; NormalizeVector: 0 where the norm is
+    # not positive, the input unchanged when the lengths differ
+    assert O.vector_dot_product([], [1.0]) == -1 and O.vector_dot_product([1.0, 2.0], [1.0]) == -1
+    assert O.normalize_vector([3.0, 4.0], [0.0, 2.0]) == [0.0, 2.0]
+    assert O.normalize_vector([3.0, 4.0], [2.0]) == [3.0, 4.0]
+
+
+def test_dot_product_variants_reference_examples():
+    # config.go:8-28 worked example: pod <100 CPU, 100 GPU>, node <3000 CPU, GPUs 200, 500, 1000 x 6>
+    n = O.node_res(3000, [200, 500] + [1000] * 6, 8, "", 3000)
+    p = O.pod_res(100, 100, 1, "")
+    # share: virtual nodes <3000, 200>, <3000, 500>, <3000, 6000>; divide scales the CPU by GPU share
+    for dim in (O.DIM_SHARE, O.DIM_DIVIDE, O.DIM_EXTEND):
+        for norm in (O.NORM_MAX, O.NORM_NODE, O.NORM_POD):
+            s, g = O.dot_product_score(n, p, dim, norm)
+            assert 0 <= s <= 100 and g in (1, 2, 4)  # a share GPU (0 or 1) or the first idle GPU (2)
+    # merge has no GPU id: the DotProduct selector cannot place a GPU pod with it
+    assert O.dot_product_score(n, p, O.DIM_MERGE, O.NORM_MAX)[1] == 0
