@@ -643,12 +643,19 @@ KSIM_HD int dotprod_cfg_score(const NodeV& n, const PodDev& p, int cap, int cfg,
     // left scaled by that GPU's share of the GPU left), then the idle GPUs; merge: one group.
     // Candidates j = 0..7 are GPU j, j = 8 the idle group (merge: j = 8 is the merged node).
     const int len = dim == DIM_EXTEND ? 1 + part + (idle > 0 ? 1 : 0) : 2;
+    // GPU j's milli left is the low half of w0 at iteration j (the words shift down by 16 bits per
+    // iteration: a runtime index into the packed words would put them in scratch)
+    uint32_t w0 = n.g[0], w1 = n.g[1], w2 = n.g[2], w3 = n.g[3];
 #pragma unroll 1
     for (int j = (dim == DIM_MERGE ? kMaxGpu : 0); j <= kMaxGpu; ++j) {
       bool use;
       int v1, g_id;
       if (j < kMaxGpu) {
-        const int l = n.gl(j);
+        const int l = (int)(w0 & 0xffffu);
+        w0 = (w0 >> 16) | (w1 << 16);
+        w1 = (w1 >> 16) | (w2 << 16);
+        w2 = (w2 >> 16) | (w3 << 16);
+        w3 >>= 16;
         use = j < cnt && l < kMilli && l >= req && (dim == DIM_EXTEND ? l > 0 : req < kMilli);
         v1 = l;
         g_id = 1 << j;

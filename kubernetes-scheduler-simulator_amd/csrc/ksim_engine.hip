@@ -681,14 +681,19 @@ struct GranV {
   unsigned long long g0[kSub], g1[kSub], g2[kSub];
 };
 
-// kSub = ceil(K / 64): 1 for K <= 64, 4 for K <= 256 (one wave-0 lane polls kSub workgroups).
+// kSub = ceil(K / 64): 1 for K <= 64, 4 for K <= 256 (one wave-0 lane polls kSub workgroups); 0 for
+// K = 1 (no exchange), where the cheap policies are built for two 1024-thread workgroups per CU (64
+// VGPRs: 8 waves per SIMD), so the paper sweep's single-workgroup replicas pack two to a CU.
 // kGeneral: the KSIM_PROFILE timers, the cluster-report stores and delete events (bind history);
 // the lean instantiation (none of them: the bench, the paper sweeps, C5) compiles them out of the
 // step loop, as k_memo's does.
 template <int kPol, int kSub, bool kGeneral>
-__global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::ReplayArgs a,
+__global__ __launch_bounds__(ksim_replay::kRBlock, (kSub == 0 && kPol >= POL_BESTFIT && kPol <= POL_RANDOM &&
+                                                     kPol != POL_DOTPROD) ? 8 : 1)
+void k_replay(ksim_replay::ReplayArgs a,
                                                                  const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
+  constexpr int kS = kSub > 0 ? kSub : 1;  // granule columns per polling lane (K = 1 polls none)
   constexpr bool kPwr = kPol == POL_PWR;
   constexpr bool kPF = kPol == POL_PWR_FGD;
   constexpr bool kFgd = kPol == POL_FGD || kPF;  // the FGD candidate evaluation
@@ -704,19 +709,22 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int n_lo = w * a.S;
   const int ns = max(0, min(a.S, a.N - n_lo));
-  const int S1 = a.S + 1;  // slots incl. the virtual node
-  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(ReplayShared));
-  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(ReplayShared) + (size_t)S1 * sizeof(NodeRec));
-  double* s_F0 = reinterpret_cast<double*>(smem + sizeof(ReplayShared) +
-                                           (size_t)S1 * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t)));
+  constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
+  const RLayout L = replay_layout(a.S, kPol, kGeneral);
+  ReplayFgd& fs = *reinterpret_cast<ReplayFgd*>(smem + L.fgd);  // FGD launches only
+  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + L.nodes);
+  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + L.tags);  // kTags only
+  // the other policies keep the slice's tag counts in HBM (changed by a Bind / delete, read by none)
+  uint16_t* g_tags = rp.tags + (size_t)n_lo * kTagStride;
+  double* s_F0 = reinterpret_cast<double*>(smem + L.F0);
   // PWR policies: the cached energy of each slot's current state (kEnergyStale: recompute) and the
   // node's static energy terms {rc, ncpus << 3 | CPU model} (energy_static)
-  double* s_E0 = s_F0 + S1;
-  int2* s_pe = reinterpret_cast<int2*>(s_E0 + S1);
+  double* s_E0 = reinterpret_cast<double*>(smem + L.E0);
+  int2* s_pe = reinterpret_cast<int2*>(smem + L.pe);
   // cluster report: the last event that changed each slot (-1: none yet)
-  int* s_last = reinterpret_cast<int*>(s_pe + S1);
-  int* s_praw = s_last + S1;  // PWR+FGD per-slot scratch of the current step
-  int* s_pinf = s_praw + S1;
+  int* s_last = reinterpret_cast<int*>(smem + L.last);
+  int* s_praw = reinterpret_cast<int*>(smem + L.praw);  // PWR+FGD per-slot scratch of the current step
+  int* s_pinf = reinterpret_cast<int*>(smem + L.pinf);
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   // (null when no replica of the launch has a delete event: nothing ever reads it)
   int2* hist = (kGeneral && a.hist) ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
@@ -724,8 +732,10 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * kGranW;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
-  for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
-  for (int i = tid; i <= ns; i += kRBlock) s_last[i] = -1;
+  if (kTags)
+    for (int i = tid; i < ns * kTagStride; i += kRBlock) s_tags[i] = rp.tags[(size_t)n_lo * kTagStride + i];
+  if (kGeneral)
+    for (int i = tid; i <= ns; i += kRBlock) s_last[i] = -1;
   if (kPwr || kPF) {
     for (int i = tid; i < (int)(sizeof(PowerDev) / 8); i += kRBlock)
       reinterpret_cast<unsigned long long*>(&sh.pw)[i] = reinterpret_cast<const unsigned long long*>(rp.pw)[i];
@@ -735,7 +745,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   if (kFgd) {
     for (int i = tid; i <= ns; i += kRBlock) s_F0[i] = -1.0;  // every cached F stale
     for (int i = tid; i < rp.nt * 2; i += kRBlock)
-      reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
+      reinterpret_cast<uint4*>(fs.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   }
   auto reset_agg = [&]() {
     sh.agg_key = 0ull;
@@ -748,6 +758,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
 
   // wave 0's copy of the pending exchange (the previous pod step, published, not committed)
   int p_step = 0, p_seq = 0, p_b = -1, p_mask = -1, seq = 0;
+  int p_tag = -1;  // the pending Bind's affinity tag (policies keeping the tag counts in HBM)
   unsigned long long p_key = 0ull;
   int p_st0 = 0, p_st1 = 0, p_st2 = 0, p_st3 = 0;  // K == 1: the step's own totals
 
@@ -766,10 +777,10 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
 
   // Wave 0, lane k: the granules of workgroups k, k+64, .. (< K) of the pending exchange
   // (relaxed agent-scope loads).
-  auto poll_once = [&](GranV<kSub>& g) {
+  auto poll_once = [&](GranV<kS>& g) {
     const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) {
+    for (int j = 0; j < kS; ++j) {
       const int k = lane + 64 * j;
       if (k < a.K) {
         g.g0[j] = gload(slot + (size_t)k * kGranW + 0);
@@ -789,10 +800,10 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
       gstore(slot + (size_t)w * kGranW + 5, tag | (unsigned)h);
       gstore(slot + (size_t)w * kGranW + 6, tag | ((unsigned)e << 31) | ((unsigned)c & 0x7fffffffu));
     }
-    unsigned long long x0[kSub], x1[kSub], x2[kSub];
+    unsigned long long x0[kS], x1[kS], x2[kS];
     auto load = [&]() {
 #pragma unroll
-      for (int j = 0; j < kSub; ++j) {
+      for (int j = 0; j < kS; ++j) {
         const int k = lane + 64 * j;
         if (k < a.K) {
           x0[j] = gload(slot + (size_t)k * kGranW + 4);
@@ -804,7 +815,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     auto ready = [&]() {
       bool r = true;
 #pragma unroll
-      for (int j = 0; j < kSub; ++j)
+      for (int j = 0; j < kS; ++j)
         r = r && (lane + 64 * j >= a.K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag &&
                                           (x2[j] & ~0xffffffffull) == tag));
       return r;
@@ -820,7 +831,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     int cs = 0, lo = INT_MAX, hi = INT_MIN;
     bool e1 = false;
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) {
+    for (int j = 0; j < kS; ++j) {
       if (lane + 64 * j < a.K) {
         const unsigned st = (unsigned)(x2[j] & 0xffffffffull);
         cs += (int)(st & 0x7fffffffu);
@@ -837,7 +848,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   };
   // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
   // this workgroup's own totals (K == 1); g holds an earlier poll.  Returns the winning key.
-  auto exchange = [&](GranV<kSub> g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
+  auto exchange = [&](GranV<kS> g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
     *ok = true;
     if (a.K == 1) {
       *gc = p_st0; *ge = p_st1; *gl = p_st2; *gh = p_st3;
@@ -847,7 +858,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     auto ready = [&]() {
       bool r = true;
 #pragma unroll
-      for (int j = 0; j < kSub; ++j)
+      for (int j = 0; j < kS; ++j)
         r = r && (lane + 64 * j >= a.K || ((g.g0[j] & ~0xffffffffull) == tag && (g.g1[j] & ~0xffffffffull) == tag &&
                                           (g.g2[j] & ~0xffffffffull) == tag));
       return r;
@@ -863,7 +874,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     bool e1 = false;
     unsigned long long best = 0ull;
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) {
+    for (int j = 0; j < kS; ++j) {
       const bool in = lane + 64 * j < a.K;
       const unsigned st = in ? (unsigned)(g.g2[j] & 0xffffffffull) : 0u;
       const int cj = (int)(st & 0x1ffff);
@@ -907,9 +918,10 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
             hrec.x = -3;
           } else {
             if (lane < 2) reinterpret_cast<uint4*>(&s_nodes[p_b])[lane] = reinterpret_cast<const uint4*>(&s_nodes[ns])[lane];
-            else if (lane < 6)
+            else if (lane < 6 && kTags)
               reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
                   reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
+            else if (lane == 2 && !kTags && p_tag >= 0) g_tags[(size_t)p_b * kTagStride + p_tag] += 1;
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
             else if (lane == 8 && kPF) { s_praw[p_b] = s_praw[ns]; s_pinf[p_b] = s_pinf[ns]; }
             else if (lane == 9 && (kPwr || kPF)) s_E0[p_b] = s_E0[ns];
@@ -934,7 +946,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   // Finish the pending step with nothing to overlap (before a delete / at the end).
   auto finish_pending = [&]() {
     if (wv == 0) {
-      GranV<kSub> g{};
+      GranV<kS> g{};
       if (a.K > 1) poll_once(g);
       int gc, ge, gl, gh;
       bool ok;
@@ -972,7 +984,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         if (h.x >= 0) {
           const PodDev cp = rp.ev[p.ref];
           const int loc = h.x - n_lo;
-          apply_bind(&s_nodes[loc], &s_tags[(size_t)loc * kTagStride], cp, h.y - 1, -1);
+          apply_bind(&s_nodes[loc], kTags ? &s_tags[(size_t)loc * kTagStride] : g_tags + (size_t)loc * kTagStride, cp,
+                     h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
           if (kPwr || kPF) s_E0[loc] = kEnergyStale;
           if (snap) {
@@ -996,7 +1009,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
     const int vb = pend ? __builtin_amdgcn_readfirstlane(pvb.y) : -1;
     const int nsv = ns + (vb >= 0 ? 1 : 0);
     // early poll of the pending exchange by wave 0 (consumed after the evaluation)
-    GranV<kSub> pg{};
+    GranV<kS> pg{};
     // one node's packed key into the workgroup aggregate (LDS atomics), or the excluded pair
     auto route = [&](bool leader, int i, bool feas, bool e1, int raw, unsigned long long k) {
       const bool excl = leader && (i == vb || i == ns);
@@ -1062,30 +1075,30 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         int my_item = -1;
         if (cand) {
           my_item = base + lanes_below(cm);
-          sh.item_node[my_item] = (uint16_t)i;
-          sh.item_code[my_item] = (uint8_t)(share ? 1 + g : 9);
+          fs.item_node[my_item] = (uint16_t)i;
+          fs.item_code[my_item] = (uint8_t)(share ? 1 + g : 9);
         }
         if (cur) {
           const int o = base + __popcll(cm) + lanes_below(um);
-          sh.item_node[o] = (uint16_t)i;
-          sh.item_code[o] = 0;
+          fs.item_node[o] = (uint16_t)i;
+          fs.item_code[o] = 0;
         }
         __syncthreads();
         mark(1);
         const int tot = sh.nitems;
         const int q = tid & 3;
         for (int j = tid >> 2; j < tot; j += kRBlock / 4) {  // one quad per item
-          const int loc = sh.item_node[j], code = sh.item_code[j];
+          const int loc = fs.item_node[j], code = fs.item_code[j];
           const NodeV m = load_node(&s_nodes[loc]);
           int cpuL, total;
           uint32_t gs[4];
           fgd_candidate(m, code, p, &cpuL, gs, &total);
           const uint32_t tb = 1u << m.gpu_type();
-          const double F = rp.typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
-                                    : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          const double F = rp.typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, fs.tp, rp.ncpu, rp.nt, q)
+                                    : frag_F_quad<false>(cpuL, gs, total, tb, tp, fs.tp, rp.ncpu, rp.nt, q);
           if (q == 0) {
             if (code == 0) s_F0[loc] = F;
-            else sh.F[j] = F;
+            else fs.F[j] = F;
           }
         }
         __syncthreads();
@@ -1095,7 +1108,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         // fgd_score.go:100-141: every candidate lane scores itself; the node keeps the max,
         // ties to the lowest GPU index (fgd_score.go:128 keeps the first max)
         int v = -1;
-        if (cand) v = fgd_frag_score(s_F0[i], sh.F[my_item]) * 16 + (15 - g);
+        if (cand) v = fgd_frag_score(s_F0[i], fs.F[my_item]) * 16 + (15 - g);
         v = group8_max(v);
         // PWR + FGD: the node's raw PWR score and GPU choice by the same 8 lanes
         int pv = -1;
@@ -1180,7 +1193,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
           feas = filter_node(n, p);
           if (feas) {
             const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[n_lo + (i == ns ? vb : i)] : 0;
-            raw = cheap_score<kPol>(n, p, rp.seed, &s_tags[(size_t)i * kTagStride], step, &e1, rp.dpcfg, cap);
+            raw = cheap_score<kPol>(n, p, rp.seed, kTags ? &s_tags[(size_t)i * kTagStride] : nullptr, step, &e1,
+                                    rp.dpcfg, cap);
           }
         }
         const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, -1, i == ns ? vb : i) : 0ull;
@@ -1262,7 +1276,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
                              step);
           if (mask >= 0) bind_node(bn, p, mask, +1);
           if (lane == 0) store_node(&s_nodes[ns], bn);
-          else if (lane >= 2 && lane < 6) {
+          else if (kTags && lane >= 2 && lane < 6) {
             uint2 t = reinterpret_cast<const uint2*>(&s_tags[(size_t)mloc * kTagStride])[lane - 2];
             if (mask >= 0 && p.tag >= 0 && (p.tag >> 2) == lane - 2) {
               const uint32_t inc = 1u << (16 * (p.tag & 1));
@@ -1281,6 +1295,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         p_b = mk != 0ull ? mloc : -1;
         p_key = mk;
         p_mask = mask;
+        p_tag = mask >= 0 ? (int)p.tag : -1;
         ++seq;
         if (lane == 0) { sh.pend_valid = 1; sh.pend_b = p_b; }
       }
@@ -1333,7 +1348,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
                              step);
           if (mask >= 0) bind_node(bn, p, mask, +1);
           if (lane == 0) store_node(&s_nodes[ns], bn);
-          else if (lane >= 2 && lane < 6) {
+          else if (kTags && lane >= 2 && lane < 6) {
             uint2 t = reinterpret_cast<const uint2*>(&s_tags[(size_t)mloc * kTagStride])[lane - 2];
             if (mask >= 0 && p.tag >= 0 && (p.tag >> 2) == lane - 2) {
               // +1 on u16 tag p.tag (counts stay far below 2^16, no carry across halves)
@@ -1353,6 +1368,7 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
         p_b = mk != 0ull ? mloc : -1;
         p_key = mk;
         p_mask = mask;
+        p_tag = mask >= 0 ? (int)p.tag : -1;
         p_st0 = c; p_st1 = e; p_st2 = l; p_st3 = h;
         ++seq;
         if (lane == 0) { sh.pend_valid = 1; sh.pend_b = p_b; }
@@ -1375,7 +1391,8 @@ __global__ __launch_bounds__(ksim_replay::kRBlock) void k_replay(ksim_replay::Re
   if (prof && tid < kProfPhases) a.prof[(size_t)blockIdx.x * kProfPhases + tid] = sh.prof[tid];
   // write the slice back (final cluster state)
   for (int i = tid; i < ns; i += kRBlock) store_node(rp.nodes + n_lo + i, load_node(&s_nodes[i]));
-  for (int i = tid; i < ns * kTagStride; i += kRBlock) rp.tags[(size_t)n_lo * kTagStride + i] = s_tags[i];
+  if (kTags)
+    for (int i = tid; i < ns * kTagStride; i += kRBlock) rp.tags[(size_t)n_lo * kTagStride + i] = s_tags[i];
 }
 
 __global__ void k_advance(int* base, int k) { *base += k; }
@@ -1637,7 +1654,7 @@ static int launch_persistent(const void* f, int grid, int block, size_t lds, hip
 
 template <int P, bool G>
 static const void* replay_fn(int K) {
-  return K <= 64 ? (const void*)k_replay<P, 1, G> : (const void*)k_replay<P, 4, G>;
+  return K == 1 ? (const void*)k_replay<P, 0, G> : K <= 64 ? (const void*)k_replay<P, 1, G> : (const void*)k_replay<P, 4, G>;
 }
 template <int P>
 static const void* replay_fn(int K, bool general) {
@@ -3048,10 +3065,8 @@ static int resident_cap(const ksim_engine* e, const void* f, size_t lds) {
   return nb * e->cus;
 }
 
-static size_t replay_lds(int S) {  // S real slots + the virtual node
-  return sizeof(ksim_replay::ReplayShared) +
-         (size_t)(S + 1) * (sizeof(NodeRec) + kTagStride * sizeof(uint16_t) + 2 * sizeof(double) + sizeof(int2) +
-                            3 * sizeof(int));
+static size_t replay_lds(int S, int pol, bool general) {  // S real slots + the virtual node
+  return ksim_replay::replay_layout(S, pol, general).total;
 }
 
 
@@ -3080,6 +3095,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
   // profile timers) keeps the launches back to back on the engine stream.
   bool concurrent = !profile && groups.size() >= 2;
+  const bool gen_any = profile || e->report || any_delete;
   for (const auto& gp : groups) {
     if (!concurrent) break;
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
@@ -3089,7 +3105,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     int K = choose_wgs(e, gp.second);
     int S = (e->N + K - 1) / K;
-    while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && gp.second * (K + 1) <= e->cus) {
+    while (replay_lds(S, gp.first, gen_any) > 160 * 1024 && K < ksim_replay::kMaxK && gp.second * (K + 1) <= e->cus) {
       ++K;
       S = (e->N + K - 1) / K;
     }
@@ -3140,20 +3156,20 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
-    while (replay_lds(S) > 160 * 1024 && K < ksim_replay::kMaxK && Rg * (K + 1) <= e->cus) {
+    const bool general = profile || e->report || any_delete;
+    while (replay_lds(S, gp.first, general) > 160 * 1024 && K < ksim_replay::kMaxK && Rg * (K + 1) <= e->cus) {
       ++K;
       S = (e->N + K - 1) / K;
     }
-    if (replay_lds(S) > 160 * 1024) return KSIM_ERANGE;
-    const bool general = profile || e->report || any_delete;
+    if (replay_lds(S, gp.first, general) > 160 * 1024) return KSIM_ERANGE;
     if (K > 1) {
       // the occupancy query bounds the co-resident grid: fewer, larger slices when it is short
-      const int cap = resident_cap(e, replay_kernel(gp.first, K, general), replay_lds(S));
+      const int cap = resident_cap(e, replay_kernel(gp.first, K, general), replay_lds(S, gp.first, general));
       if (Rg * K > cap) {
         if (e->wgs_req > 0 && cap < Rg) return KSIM_ERANGE;
         K = std::max(1, std::min(K, cap / Rg));
         S = (e->N + K - 1) / K;
-        if (replay_lds(S) > 160 * 1024) {
+        if (replay_lds(S, gp.first, general) > 160 * 1024) {
           std::fprintf(stderr, "ksim: k_replay needs %d co-resident workgroups; the device holds %d\n", Rg * K, cap);
           return KSIM_ERANGE;
         }
@@ -3165,7 +3181,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
       e->hist_cap = need;
     }
-    const size_t lds = replay_lds(S);
+    const size_t lds = replay_lds(S, gp.first, general);
     ksim_replay::ReplayArgs ra;
     ra.reps = e->d_reps;
     ra.rep_list = e->d_replist + first;

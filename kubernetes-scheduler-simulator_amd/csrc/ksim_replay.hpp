@@ -64,14 +64,17 @@ struct ReplayArgs {
 };
 constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 
-// Per-workgroup state at the start of the dynamic LDS region (16-B aligned).  After it:
-// NodeRec nodes[S+1], u16 tags[S+1][16], double F0[S+1] (cached F of the current state,
-// < 0 = stale), i32 last[S+1] (cluster report), i32 praw[S+1] + i32 pinf[S+1] (PWR+FGD: the
-// step's raw PWR score and packed FGD score / GPU choices of every slot).  Slot ns (one past the slice) is the VIRTUAL node: the pending step's
-// local best node with that step's Bind already applied (see the pipelining note).
+// Per-workgroup state at the start of the dynamic LDS region (16-B aligned); after it, only what the
+// launch's policy reads (replay_layout): the FGD evaluation scratch, NodeRec nodes[S+1], u16
+// tags[S+1][16] (GpuClustering; the other policies keep the tag counts in HBM), double F0[S+1]
+// (FGD: cached F of the current state, < 0 = stale), double E0[S+1] + int2 pe[S+1] (PWR: cached
+// energy, static energy terms), i32 last[S+1] (cluster report), i32 praw[S+1] + i32 pinf[S+1]
+// (PWR+FGD: the step's raw PWR score and packed FGD score / GPU choices of every slot).  A lean
+// BestFit / DotProd / GpuPacking / Random workgroup of C2 / C4 is about 44 KB, so several share a
+// CU.  Slot ns (one past the slice) is the VIRTUAL node: the pending step's local best node with
+// that step's Bind already applied (see the pipelining note).
 struct __align__(16) ReplayShared {
   PodDev ev[kEvBuf];
-  TypDev tp[kMaxTypical];  // the replica's typical table (per-lane reads in the quad evaluator)
   // the step's local aggregate (LDS atomics), the pending best node b and the virtual node excluded
   unsigned long long agg_key;
   int agg_cnt, agg_err, agg_lo, agg_hi;
@@ -87,11 +90,41 @@ struct __align__(16) ReplayShared {
   unsigned long long prof[kProfPhases];  // KSIM_PROFILE phase sums (thread 0)
   unsigned long long prof_pad[4];
   PowerDev pw;                  // PWR policies: the replica's energy model
+};
+static_assert(sizeof(ReplayShared) % 16 == 0, "keep the node records 16-B aligned");
+
+// FGD evaluation scratch (FGD, PWR+FGD launches only).
+struct __align__(16) ReplayFgd {
+  TypDev tp[kMaxTypical];  // the replica's typical table (per-lane reads in the quad evaluator)
   double F[kFChunk * kRMaxCand];
   uint16_t item_node[kFChunk * kRMaxCand];
   uint8_t item_code[kFChunk * kRMaxCand];
+  uint8_t pad_[(16 - (kFChunk * kRMaxCand * 3) % 16) % 16];
 };
-static_assert(sizeof(ReplayShared) % 16 == 0, "keep the node records 16-B aligned");
+static_assert(sizeof(ReplayFgd) % 16 == 0, "keep the node records 16-B aligned");
+
+// The dynamic LDS layout of one k_replay workgroup (host and device).
+struct RLayout {
+  size_t fgd, nodes, tags, F0, E0, pe, last, praw, pinf, total;
+};
+__host__ __device__ inline RLayout replay_layout(int S, int pol, bool general) {
+  const bool tags = pol == POL_CLUSTERING, fgd = pol == POL_FGD || pol == POL_PWR_FGD;
+  const bool pwr = pol == POL_PWR || pol == POL_PWR_FGD, pf = pol == POL_PWR_FGD;
+  const size_t S1 = (size_t)S + 1;
+  RLayout L;
+  size_t o = sizeof(ReplayShared);
+  L.fgd = o;   o += fgd ? sizeof(ReplayFgd) : 0;
+  L.nodes = o; o += S1 * sizeof(NodeRec);
+  L.tags = o;  o += tags ? S1 * kTagStride * sizeof(uint16_t) : 0;
+  L.F0 = o;    o += fgd ? S1 * sizeof(double) : 0;
+  L.E0 = o;    o += pwr ? S1 * sizeof(double) : 0;
+  L.pe = o;    o += pwr ? S1 * sizeof(int2) : 0;
+  L.last = o;  o += general ? S1 * sizeof(int) : 0;
+  L.praw = o;  o += pf ? S1 * sizeof(int) : 0;
+  L.pinf = o;  o += pf ? S1 * sizeof(int) : 0;
+  L.total = o;
+  return L;
+}
 
 __device__ __forceinline__ unsigned long long gload(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
