@@ -1833,17 +1833,23 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
   pl.nb = pl.Npad / kFan;
   // one workgroup per replica while one L1 level covers the cluster; wider clusters are sliced over
   // K co-resident workgroups (at most 64: one granule column per polling lane), S a multiple of 64
-  if (e->N <= kMaxNb * kFan && e->wgs_req <= 1) {
-    pl.K = 1;
-    pl.S = e->N;
-    pl.nbw = pl.nb;
-  } else {
+  // (run_mode 5 with wgs_per_replica > 1 asks for the wide form on a small cluster too; when the
+  // wide grid would not fit the usable CUs a small cluster keeps one workgroup per replica)
+  const bool small = e->N <= kMaxNb * kFan;
+  pl.K = 1;
+  pl.S = e->N;
+  pl.nbw = pl.nb;
+  if (!small || (e->run_mode == 5 && e->wgs_req > 1)) {
     const int want = e->wgs_req > 1 ? e->wgs_req : 64;
-    pl.S = std::max(kFan, (e->N + want - 1) / want + kFan - 1) / kFan * kFan;
-    if (pl.S > kMaxNb * kFan) return false;
-    pl.K = (e->N + pl.S - 1) / pl.S;
-    pl.nbw = pl.S / kFan;
-    if ((size_t)Rg * pl.K > (size_t)e->cus) return false;
+    const int S = std::max(kFan, (e->N + want - 1) / want + kFan - 1) / kFan * kFan;
+    const int K = (e->N + S - 1) / S;
+    if (S <= kMaxNb * kFan && (size_t)Rg * K <= (size_t)e->cus) {
+      pl.S = S;
+      pl.K = K;
+      pl.nbw = S / kFan;
+    } else if (!small) {
+      return false;
+    }
   }
   std::vector<std::vector<int>> ord(Rg), gof(Rg), slot(Rg), gfirst(Rg), sof(Rg);
   std::vector<std::vector<NodeRec>> sts(Rg);
