@@ -147,6 +147,41 @@ __device__ __forceinline__ void gst1(unsigned* p, unsigned v) {
   *(__attribute__((address_space(1))) unsigned*)(p) = v;
 }
 
+// A node record reduced to what filter_node reads per class (computed once per refresh), and the
+// Filter from it: the same decisions as filter_node (ksim_device.hpp; fit.go:230-290,
+// open_gpu_share.go:81-118) with the per-GPU scans done once instead of once per class.  The
+// multi-GPU request with a partial milli (no trace has one) takes filter_node itself.
+struct NodeSum {
+  int pods_left, cpu_left, mem_left, cnt, type_bit, max_left, free_cnt;
+};
+__device__ __forceinline__ NodeSum node_sum(const NodeV& n) {
+  NodeSum s;
+  s.pods_left = n.pods_left();
+  s.cpu_left = n.cpu_left;
+  s.mem_left = n.mem_left;
+  s.cnt = n.gpu_cnt();
+  s.type_bit = 1 << n.gpu_type();
+  int mx = 0, fr = 0;
+#pragma unroll
+  for (int g = 0; g < kMaxGpu; ++g) {
+    const int l = g < s.cnt ? n.gl(g) : 0;
+    mx = l > mx ? l : mx;
+    fr += l == kMilli ? 1 : 0;
+  }
+  s.max_left = mx;
+  s.free_cnt = fr;
+  return s;
+}
+__device__ __forceinline__ bool filter_sum(const NodeSum& s, const NodeV& n, const PodDev& p) {
+  if (s.pods_left < 1) return false;
+  if (!(p.cpu_req == 0 && p.mem == 0) && (s.cpu_left < p.cpu_req || s.mem_left < p.mem)) return false;
+  if (p.milli <= 0) return true;
+  if (s.cnt == 0 || (p.tmask & (unsigned)s.type_bit) == 0u || p.num <= 0) return false;
+  if (p.num == 1) return s.max_left >= p.milli;
+  if (p.milli == kMilli) return s.free_cnt >= p.num;
+  return filter_node(n, p);
+}
+
 // Row (16-lane) max of unsigned values below 2^31: every lane of the row ends with it.
 __device__ __forceinline__ int row_max16(int v) {
   using ksim_replay::dpp_i;
@@ -306,10 +341,11 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         // Filter on d's new and old records (feasible counts), and which classes had d as the max of
         // d's block (flagged: their block max must be recomputed without d)
         const NodeV dold = uniform_node(&sh.dold);
+        const NodeSum sn = node_sum(dn), so = node_sum(dold);
         for (int c = tid - 64; c < C; c += kHBlock - 64) {
           const PodDev q = s_cls[c];
-          s_fnew[c] = filter_node(dn, q) ? 1 : 0;
-          s_fold[c] = filter_node(dold, q) ? 1 : 0;
+          s_fnew[c] = filter_sum(sn, dn, q) ? 1 : 0;
+          s_fold[c] = filter_sum(so, dold, q) ? 1 : 0;
           const unsigned old = s_l1[c * nb + b];
           const bool fl = old != 0u && hkey_rank(old) == d;
           const unsigned long long fm = __ballot(fl);
