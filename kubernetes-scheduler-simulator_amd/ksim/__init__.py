@@ -43,7 +43,7 @@ DEFAULT_GPUSEL = {"FGD": "FGD", "BestFit": "best", "DotProd": "best", "GpuPackin
 def parse_policy(name):
     """generate_run_scripts.py policy strings: "FGD", "PWR", "PWR 500 FGD 500", ... ->
     (POLICY key, weights or None)."""
-    parts = name.split()
+    parts = name.replace("_", " ").split()  # the directory form "PWR_500_FGD_500" too (get_dir_name_from_method)
     if len(parts) == 4 and parts[0] == "PWR" and parts[2] == "FGD":
         return "PWR+FGD", (int(parts[1]), int(parts[3]))
     return name, None

@@ -11,6 +11,8 @@ for name in "$@"; do
     c2-rm2) a="--run-mode 2";;
     c2-BestFit) a="--policy BestFit";;
     c2-PWR) a="--policy PWR";;
+    c2-PWR_500_FGD_500) a="--policy PWR_500_FGD_500";;
+    c2-DotProd) a="--policy DotProd";;
     c2-report) a="--report";;
     c4) a="--config c4";;
     c5) a="--config c5";;

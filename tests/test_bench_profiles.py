@@ -28,8 +28,9 @@ def test_profile_keys():
     assert bench.profile_key(_args(config="c5", sharded=True)) == "c5-sharded"
 
 
-@pytest.mark.parametrize("key,path", [("c2", "k_memo"), ("c4", "memo+k_replay"), ("c5", "k_replay"),
-                                      ("c2-rm5", "k_hmemo"), ("c2-BestFit", "k_replay")])
+@pytest.mark.parametrize("key,path", [("c2", "k_memo"), ("c4", "memo+k_replay"), ("c5", "k_hmemo"),
+                                      ("c2-rm5", "k_hmemo"), ("c2-BestFit", "k_replay"), ("c2-DotProd", "k_replay"),
+                                      ("c2-PWR", "k_replay"), ("c2-PWR_500_FGD_500", "k_replay")])
 def test_committed_profiles_feed_the_bench_line(key, path):
     import bench
     pf = os.path.join(bench.PROF_DIR, key, "pmc.json")
@@ -37,7 +38,7 @@ def test_committed_profiles_feed_the_bench_line(key, path):
         dom = json.load(f)["dominant"]
     assert dom["hbm_bytes_per_dispatch"] > 0 and dom["mean_duration_ns"] > 0
     # the fp64 split of the VALU issue: both parts present and within the whole
-    assert 0 < dom["f64_share"] < 1 and 0 < dom["valu_frac"] < 1
+    assert 0 <= dom["f64_share"] < 1 and 0 < dom["valu_frac"] < 1
     assert dom["f64_frac"] / 2 + dom["nonf64_frac"] >= dom["valu_frac"] * 0.999
     ns = _args()
     ns.config, rest = key.split("-")[0], key.split("-")[1:]
@@ -45,7 +46,7 @@ def test_committed_profiles_feed_the_bench_line(key, path):
         if r.startswith("rm"):
             ns.run_mode = int(r[2:])
         else:
-            ns.policy = r
+            ns.policy = r.replace("_", " ")
     assert bench.profile_key(ns) == key
     traffic, src, valu = bench.profile_rooflines(ns, path)
     assert traffic == dom["hbm_bytes_per_dispatch"] and src.endswith(key + "/pmc.json")
