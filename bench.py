@@ -285,6 +285,11 @@ def main():
     # executed work (the memoised paths skip most node evaluations): feasible (pod, node) score evaluations
     # of the reference's Score phase, and the (class, node) keys the memoised FGD replicas recomputed
     score_evals, key_refreshes = eng.work(getattr(eng, "memo_replicas", None))
+    # pods scheduled/s counts every pod event, failed ones included; report the failures
+    failed = 0
+    for r in range(eng.R):
+        st = eng.results_array(r)["status"]
+        failed += int(((st == ksim.UNSCHEDULABLE) | (st == ksim.ERROR)).sum())
     line = {
         "metric": "pods scheduled/sec + node-score evals/sec (FGD, openb trace) at 1/2/4/8 MI355X",
         "value": value,
@@ -303,6 +308,7 @@ def main():
                    "replicas_per_gpu": args.replicas, "events_per_gpu": total_events,
                    "parallelism": "replicas%d" % world},
         "node_evals_per_s": value * trace.num_nodes,
+        "failed_pods_per_step": failed * (1 if args.sharded else world),
         "score_evals_per_s": score_evals * args.steps * world / dt,
         "key_refreshes_per_s": key_refreshes * args.steps * world / dt if "memo" in kernel else None,
         "device_ms_per_step": dev_ms / args.steps,
