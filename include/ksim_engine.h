@@ -223,6 +223,15 @@ int  ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t
  * reference harness sets alike: generate_config_and_run.py:269-277).  Replaces
  * GenerateSchedulingMatchGroups' cfg arguments (pkg/utils/utils.go:1274-1342). */
 int  ksim_engine_set_plugin_cfg(ksim_engine* e, int replica, int dim_ext, int norm);
+/* KSIM_POLICY_RANDOM on Go's math/rand stream: ksim_engine_run replays the reference's draw
+ * structure from this source state (rng.go rngSource: vec[607], tap, feed; e.g. from
+ * ksim_trace_replay_go_state) -- per creation event Intn(100) (scheduler.go:464), Int31n(#nodes)
+ * when none is feasible (default_preemption.go:183), Intn(#feasible) when two or more are
+ * (random_score.go:44; the pick indexes the feasible list in node order), and the random GPU
+ * selector's Intn(k) per fitting GPU (open_gpu_share.go:333).  vec == NULL restores the default
+ * hash contract (DESIGN.md "Random contract").  Persistent path, one cluster per GPU engine, GPU
+ * selectors best / worst / random; other combinations make ksim_engine_run return KSIM_ENOTSUP. */
+int  ksim_engine_set_go_stream(ksim_engine* e, int replica, const uint64_t* vec, int tap, int feed);
 
 /* Plugin-level entry points (no state change).  For one pod, Filter + Score
  * every node of the replica: feasible[n] (0/1), score[n] (the plugin's Score
@@ -272,12 +281,20 @@ int  ksim_engine_last_report_ms(ksim_engine* e, double* ms);
  * authoritative (others hold gpu_mask 0 and a provisional status).
  *   comm_id != NULL  one process per GPU, exchange = ncclAllGather over RCCL (comm_id from
  *                    ksim_shard_comm_id on one rank, broadcast by the caller); ksim_engine_run.
- *   comm_id == NULL  world == 1, or an in-process group on one device run by ksim_shard_group_run
- *                    (validation / tests). */
+ *   comm_id == NULL  world == 1, an in-process group on one device run by ksim_shard_group_run
+ *                    (validation / tests), or a host exchange (below).
+ * Host exchange (comm_id == NULL, world >= 1): ksim_engine_run hands each step's record to `fn`,
+ * which must gather the `world` shards' records in rank order into `recv` (this shard's own at
+ * recv[4*rank]) over the caller's transport (gloo, MPI, sockets: shards on hosts or GPUs RCCL does
+ * not connect) and return 0; a non-zero return or a gather without this shard's record at its rank
+ * ends the run with KSIM_ESTATE.  One host round trip per pod step: a correctness and portability
+ * path, not the fast one.  fn == NULL clears it. */
 #define KSIM_SHARD_ID_BYTES 128
+typedef int (*ksim_shard_exchange_fn)(const uint64_t* send /* 4 */, uint64_t* recv /* 4 * world */, void* user);
 int  ksim_shard_comm_id(uint8_t* out /* KSIM_SHARD_ID_BYTES */);
 int  ksim_engine_set_shard(ksim_engine* e, int rank, int world, int node_offset, int n_global,
                            const uint8_t* comm_id);
+int  ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, void* user);
 int  ksim_shard_group_run(ksim_engine* const* engines, int world);
 
 /* Measurement.  Restarts from the set_nodes state and runs the first `n_steps`

@@ -99,6 +99,11 @@ int  ksim_trace_typical(const ksim_trace* t, const ksim_typical_cfg* cfg, ksim_t
  * Returns KSIM_ERANGE if cap is too small (*n_events holds the size needed). */
 int  ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
                        int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix);
+/* Go's global math/rand source as the first scheduling cycle of that replay finds it (every draw
+ * of ksim_trace_replay made): vec[607], tap_feed[2] = {tap, feed} (rng.go rngSource), *draws
+ * (nullable) = Uint64 draws since rand.Seed.  Input of ksim_engine_set_go_stream. */
+int  ksim_trace_replay_go_state(const ksim_trace* t, const ksim_replay_cfg* cfg, uint64_t* vec,
+                                int32_t* tap_feed, int64_t* draws);
 
 /* The PWR energy model of the reference (const.go:41-124) for this trace's GPU-model
  * vocabulary: models named in MapGpuTypeModelEnergy get their idle / full watts (G2 -> A10,

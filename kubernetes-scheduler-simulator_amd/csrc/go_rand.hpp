@@ -27,6 +27,7 @@ class Rand {
   void Seed(int64_t seed) {  // rng.go rngSource.Seed
     tap_ = 0;
     feed_ = kLen - kTap;
+    draws_ = 0;
     seed = seed % kInt32Max;
     if (seed < 0) seed += kInt32Max;
     if (seed == 0) seed = 89482311;
@@ -46,6 +47,7 @@ class Rand {
   }
 
   uint64_t Uint64() {  // rng.go rngSource.Uint64
+    ++draws_;
     if (--tap_ < 0) tap_ += kLen;
     if (--feed_ < 0) feed_ += kLen;
     const uint64_t x = vec_[feed_] + vec_[tap_];
@@ -115,6 +117,15 @@ class Rand {
     for (; i > 0; --i) swap(i, (int64_t)int31n((int32_t)(i + 1)));
   }
 
+  // the source's state (the Random draw structure continues the stream on the device) and the
+  // number of Uint64 draws since Seed
+  void State(uint64_t* vec, int* tap, int* feed) const {
+    for (int i = 0; i < kLen; ++i) vec[i] = vec_[i];
+    *tap = tap_;
+    *feed = feed_;
+  }
+  uint64_t Draws() const { return draws_; }
+
  private:
   static constexpr int kLen = 607, kTap = 273;
   static constexpr int64_t kInt32Max = 2147483647;
@@ -127,6 +138,7 @@ class Rand {
     return x;
   }
   int tap_ = 0, feed_ = 0;
+  uint64_t draws_ = 0;
   uint64_t vec_[kLen];
 };
 

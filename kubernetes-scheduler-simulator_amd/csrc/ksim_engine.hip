@@ -687,6 +687,8 @@ struct GranV {
 // kGeneral: the KSIM_PROFILE timers, the cluster-report stores and delete events (bind history);
 // the lean instantiation (none of them: the bench, the paper sweeps, C5) compiles them out of the
 // step loop, as k_memo's does.
+#include "ksim_random_go.hpp"
+
 template <int kPol, int kSub, bool kGeneral>
 __global__ __launch_bounds__(ksim_replay::kRBlock, (kSub == 0 && kPol >= POL_BESTFIT && kPol <= POL_RANDOM &&
                                                      kPol != POL_DOTPROD) ? 8 : 1)
@@ -1607,6 +1609,14 @@ struct ksim_engine {
   unsigned long long* d_send = nullptr;  // this shard's record {best, nfeas, err, lo|hi}
   unsigned long long* d_recv = nullptr;  // [world][4] gathered records
   unsigned long long** d_ptrs = nullptr; // group mode: send / recv pointer tables
+  ksim_shard_exchange_fn xfn = nullptr;  // host exchange (ksim_engine_set_shard_exchange)
+  void* xuser = nullptr;
+  std::vector<uint64_t> h_send, h_recv;  // its staging records
+  // the Random draw structure on Go's math/rand stream (ksim_engine_set_go_stream): per replica the
+  // source state {vec[607], tap, feed}, empty = the hash contract
+  std::vector<std::vector<unsigned long long>> go_state;
+  unsigned long long* d_go = nullptr;
+  size_t go_cap = 0;
   int64_t last_steps = 0;
 };
 
@@ -2399,6 +2409,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
   e->has_delete.assign(n_replicas, 0);
+  e->go_state.assign(n_replicas, {});
   e->h_cls.resize(n_replicas);
   e->h_cls_n.resize(n_replicas);
   e->h_ev_cls.resize(n_replicas);
@@ -2448,7 +2459,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist};
+                  e->d_h_hist, e->d_go};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -2624,6 +2635,26 @@ int ksim_engine_set_plugin_cfg(ksim_engine* e, int replica, int dim_ext, int nor
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
   return KSIM_OK;
+}
+
+int ksim_engine_set_go_stream(ksim_engine* e, int replica, const uint64_t* vec, int tap, int feed) {
+  if (!e || replica < 0 || replica >= e->R) return KSIM_EINVAL;
+  if (!vec) {
+    e->go_state[replica].clear();
+    return KSIM_OK;
+  }
+  if (tap < 0 || tap >= ksim_random_go::kLen || feed < 0 || feed >= ksim_random_go::kLen) return KSIM_EINVAL;
+  std::vector<unsigned long long>& s = e->go_state[replica];
+  s.assign(vec, vec + ksim_random_go::kLen);
+  s.push_back((unsigned long long)tap);
+  s.push_back((unsigned long long)feed);
+  return KSIM_OK;
+}
+
+// Replicas replaying the Random draw structure on Go's stream (k_random_go): policy Random with a
+// source state set.
+static bool go_random(const ksim_engine* e, int r) {
+  return e->reps[r].policy == POL_RANDOM && !e->go_state[r].empty();
 }
 
 int ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t w_fgd) {
@@ -2964,8 +2995,23 @@ static int shard_exchange(ksim_engine* e, hipStream_t st) {
 // Sharded run over RCCL (or a world of one): steps captured K at a time into a hipGraph when the
 // stream capture accepts the collective, else enqueued eagerly.
 static int run_sharded(ksim_engine* e, int max_ev) {
-  if (e->shard_world > 1 && !e->comm) return KSIM_ESTATE;  // in-process group: ksim_shard_group_run
   int rc;
+  if (e->xfn) {  // host exchange: the record goes through the caller's transport, one step at a time
+    const size_t rec = 4 * sizeof(unsigned long long);
+    for (int s = 0; s < max_ev; ++s) {
+      if ((rc = shard_local(e, e->stream, nullptr, s))) return rc;
+      KSIM_HIP(hipMemcpyAsync(e->h_send.data(), e->d_send, rec, hipMemcpyDeviceToHost, e->stream));
+      KSIM_HIP(hipStreamSynchronize(e->stream));
+      if (e->xfn(e->h_send.data(), e->h_recv.data(), e->xuser) != 0) return KSIM_ESTATE;
+      // the caller's gather must hold this shard's own record at its rank
+      if (std::memcmp(e->h_recv.data() + 4 * (size_t)e->shard_rank, e->h_send.data(), rec) != 0) return KSIM_ESTATE;
+      KSIM_HIP(hipMemcpyAsync(e->d_recv, e->h_recv.data(), rec * (size_t)e->shard_world, hipMemcpyHostToDevice,
+                              e->stream));
+      if ((rc = shard_commit(e, e->stream, nullptr, s))) return rc;
+    }
+    return KSIM_OK;
+  }
+  if (e->shard_world > 1 && !e->comm) return KSIM_ESTATE;  // in-process group: ksim_shard_group_run
   hipGraph_t g = nullptr;
   hipGraphExec_t ge = nullptr;
   const int K = std::min(e->K, std::max(max_ev, 1));
@@ -3078,14 +3124,36 @@ static size_t replay_lds(int S, int pol, bool general) {  // S real slots + the 
 
 // One k_replay launch per policy present (the kernel is specialised on the policy);
 // launches of different policies run back to back on the engine stream.
+constexpr int kPolRandomGo = 64;  // run_persistent's group id of the k_random_go replicas
+
 static int run_persistent(ksim_engine* e, int max_ev) {
   std::vector<int> order;
   std::vector<std::pair<int, int>> groups;  // (policy, count) in `order`
   for (int pol = POL_FGD; pol <= POL_PWR_FGD; ++pol) {
     int c = 0;
     for (int r = 0; r < e->R; ++r)
-      if (e->reps[r].policy == pol) { order.push_back(r); ++c; }
+      if (e->reps[r].policy == pol && !go_random(e, r)) { order.push_back(r); ++c; }
     if (c) groups.push_back({pol, c});
+  }
+  {  // Random on Go's stream: one k_random_go workgroup per replica, last
+    int c = 0;
+    for (int r = 0; r < e->R; ++r)
+      if (go_random(e, r)) { order.push_back(r); ++c; }
+    if (c) {
+      groups.push_back({kPolRandomGo, c});
+      const size_t words = (size_t)e->R * ksim_random_go::kStateWords;
+      if (words > e->go_cap) {
+        if (e->d_go) KSIM_HIP(hipFree(e->d_go));
+        KSIM_HIP(hipMalloc(&e->d_go, sizeof(unsigned long long) * words));
+        e->go_cap = words;
+      }
+      std::vector<unsigned long long> h(words, 0ull);
+      for (int r = 0; r < e->R; ++r)
+        if (go_random(e, r))
+          std::copy(e->go_state[r].begin(), e->go_state[r].end(), h.begin() + (size_t)r * ksim_random_go::kStateWords);
+      KSIM_HIP(hipMemcpyAsync(e->d_go, h.data(), sizeof(unsigned long long) * words, hipMemcpyHostToDevice, e->stream));
+      KSIM_HIP(hipStreamSynchronize(e->stream));  // h is a local
+    }
   }
   KSIM_HIP(hipMemcpyAsync(e->d_replist, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
@@ -3104,6 +3172,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   const bool gen_any = profile || e->report || any_delete;
   for (const auto& gp : groups) {
     if (!concurrent) break;
+    if (gp.first == kPolRandomGo) continue;  // one workgroup per replica
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
     if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) {
       if (e->hplan->K > 1) { concurrent = false; break; }  // a co-resident wide launch
@@ -3135,6 +3204,22 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       if (gidx < ksim_engine::kSide) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));
     }
     ++gidx;
+    if (gp.first == kPolRandomGo) {
+      ksim_random_go::RandGoArgs ga{e->d_reps, e->d_replist + first, e->d_go, e->N};
+      const bool in_lds = ksim_random_go::lds_bytes(e->N, true) <= 160 * 1024;
+      const size_t lds = ksim_random_go::lds_bytes(e->N, in_lds);
+      if (in_lds) {
+        KSIM_HIP(hipFuncSetAttribute((const void*)ksim_random_go::k_random_go<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(ksim_random_go::k_random_go<true>, dim3(Rg), dim3(ksim_random_go::kBlock), lds, gs, ga);
+      } else {
+        hipLaunchKernelGGL(ksim_random_go::k_random_go<false>, dim3(Rg), dim3(ksim_random_go::kBlock), lds, gs, ga);
+      }
+      KSIM_HIP(hipGetLastError());
+      e->last_groups = (int)groups.size();
+      first += Rg;
+      continue;
+    }
     // FGD: the memoised replay when the cluster and the classes fit (run_mode 0 / 3)
     if (gp.first == POL_FGD && e->run_mode != 2) {
       if (e->mplan_ok) {  // prepared by prepare_memo (the FGD replicas are the first group of `order`)
@@ -3262,6 +3347,10 @@ int ksim_engine_run(ksim_engine* e) {
   const bool step_path = e->run_mode == 1;
   for (int r = 0; r < e->R; ++r)
     if (is_pwr_policy(e->reps[r].policy) && !e->pw_set[r]) return KSIM_ESTATE;
+  for (int r = 0; r < e->R; ++r)  // Go-stream Random: the persistent path, best / worst / random selectors
+    if (go_random(e, r) && (step_path || e->shard_world > 0 ||
+                            (e->reps[r].gpusel != SEL_BEST && e->reps[r].gpusel != SEL_WORST && e->reps[r].gpusel != SEL_RANDOM)))
+      return KSIM_ENOTSUP;
   if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
   else rc = step_path ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
@@ -3330,13 +3419,24 @@ int ksim_engine_set_shard(ksim_engine* e, int rank, int world, int node_offset, 
   return KSIM_OK;
 }
 
+int ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, void* user) {
+  if (!e) return KSIM_EINVAL;
+  if (e->shard_world < 1 || e->comm) return KSIM_ESTATE;  // after set_shard, and not beside RCCL
+  e->xfn = fn;
+  e->xuser = user;
+  e->h_send.assign(4, 0);
+  e->h_recv.assign(4 * (size_t)e->shard_world, 0);
+  return KSIM_OK;
+}
+
 int ksim_shard_group_run(ksim_engine* const* engines, int world) {
   if (!engines || world < 1 || world > 16) return KSIM_EINVAL;
   ksim_engine* e0 = engines[0];
   int max_ev = 0;
   for (int k = 0; k < world; ++k) {
     ksim_engine* e = engines[k];
-    if (!e || e->shard_world != world || e->shard_rank != k || e->comm || e->device != e0->device || !e->d_ev[0])
+    if (!e || e->shard_world != world || e->shard_rank != k || e->comm || e->xfn || e->device != e0->device ||
+        !e->d_ev[0])
       return KSIM_EINVAL;
     if (e->n_events[0] != e0->n_events[0]) return KSIM_EINVAL;  // every shard sees the same events
     max_ev = std::max(max_ev, e->n_events[0]);

@@ -368,9 +368,8 @@ int ksim_trace_typical(const ksim_trace* t, const ksim_typical_cfg* cfg, ksim_ty
   return KSIM_OK;
 }
 
-int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
-                      int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix) {
-  if (!t || !cfg || !n_events || !nodes) return KSIM_EINVAL;
+static int replay_impl(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
+                       int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix, ksim_go::Rand* rng_out) {
   // Go's global math/rand, seeded as core.go:115 does; the draws below are every draw the
   // reference makes from it between rand.Seed and the first scheduling cycle.
   ksim_go::Rand rng((int64_t)cfg->seed);
@@ -449,11 +448,34 @@ int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod*
   }
   if (name_prefix)
     for (int i = 0; i < nn; ++i) name_prefix[i] = perm[i];
+  if (rng_out) *rng_out = rng;  // the stream as the first scheduling cycle finds it
   if ((int)ev.size() > cap || !events) return KSIM_ERANGE;
   for (size_t k = 0; k < ev.size(); ++k) {
     events[k] = to_engine_pod(t->pods[ev[k]], t->pod_mask[ev[k]]);
     if (pod_index) pod_index[k] = ev[k];
   }
+  return KSIM_OK;
+}
+
+int ksim_trace_replay(const ksim_trace* t, const ksim_replay_cfg* cfg, ksim_pod* events, int cap, int* n_events,
+                      int32_t* pod_index, ksim_node* nodes, int32_t* name_prefix) {
+  if (!t || !cfg || !n_events || !nodes) return KSIM_EINVAL;
+  return replay_impl(t, cfg, events, cap, n_events, pod_index, nodes, name_prefix, nullptr);
+}
+
+int ksim_trace_replay_go_state(const ksim_trace* t, const ksim_replay_cfg* cfg, uint64_t* vec, int32_t* tap_feed,
+                               int64_t* draws) {
+  if (!t || !cfg || !vec || !tap_feed) return KSIM_EINVAL;
+  int n = 0;
+  std::vector<ksim_node> nodes(t->nodes.size() + 1);
+  ksim_go::Rand rng(0);
+  const int rc = replay_impl(t, cfg, nullptr, 0, &n, nullptr, nodes.data(), nullptr, &rng);
+  if (rc != KSIM_OK && rc != KSIM_ERANGE) return rc;  // (ERANGE: no event buffer was asked for)
+  int tap = 0, feed = 0;
+  rng.State(vec, &tap, &feed);
+  tap_feed[0] = tap;
+  tap_feed[1] = feed;
+  if (draws) *draws = (int64_t)rng.Draws();
   return KSIM_OK;
 }
 

@@ -163,6 +163,7 @@ SIGNATURES = {
     "ksim_shard_comm_id": (C.c_int, [_P(C.c_uint8)]),
     "ksim_engine_set_shard": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _P(C.c_uint8)]),
     "ksim_shard_group_run": (C.c_int, [_P(_VP), C.c_int]),
+    "ksim_engine_set_shard_exchange": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),
     "ksim_engine_set_plugin_cfg": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
     "ksim_trace_synthetic": (C.c_int, [_VP, C.c_int, C.c_int, C.c_uint64, _P(_VP)]),
@@ -177,6 +178,8 @@ SIGNATURES = {
     "ksim_trace_replay": (C.c_int, [_VP, _P(ReplayCfg), _P(Pod), C.c_int, _P(C.c_int), _P(C.c_int32), _P(Node),
                                     _P(C.c_int32)]),
     "ksim_go_rand": (C.c_int, [C.c_int64, C.c_int, C.c_int64, C.c_int, _P(C.c_int64)]),
+    "ksim_trace_replay_go_state": (C.c_int, [_VP, _P(ReplayCfg), _P(C.c_uint64), _P(C.c_int32), _P(C.c_int64)]),
+    "ksim_engine_set_go_stream": (C.c_int, [_VP, C.c_int, _P(C.c_uint64), C.c_int, C.c_int]),
 }
 
 
@@ -317,6 +320,17 @@ class Trace:
         return Replay(events, n.value, np.ctypeslib.as_array(pidx)[: n.value].copy(), nodes,
                       np.ctypeslib.as_array(prefix).copy())
 
+    def go_state(self, seed, tune_ratio=1.3, shuffle=True, informer_draws=-1):
+        """Go's math/rand source after that replay's draws (ksim_trace_replay_go_state):
+        (vec[607] list, tap, feed, draws since rand.Seed)."""
+        cfg = ReplayCfg(seed, tune_ratio, 1 if shuffle else 0, informer_draws)
+        vec = (C.c_uint64 * 607)()
+        tf = (C.c_int32 * 2)()
+        draws = C.c_int64(0)
+        check(lib().ksim_trace_replay_go_state(self.h, C.byref(cfg), vec, tf, C.byref(draws)),
+              "ksim_trace_replay_go_state")
+        return list(vec), tf[0], tf[1], draws.value
+
 
 class Replay:
     def __init__(self, events, n, pod_index, nodes, prefix):
@@ -450,6 +464,29 @@ class Engine:
         set_nodes.  comm_id: bytes from shard_comm_id() (RCCL, one process per GPU) or None."""
         cid = None if comm_id is None else (C.c_uint8 * SHARD_ID_BYTES).from_buffer_copy(bytes(comm_id))
         check(lib().ksim_engine_set_shard(self.h, rank, world, node_offset, n_global, cid), "set_shard")
+        self._shard = (rank, world)
+
+    def set_go_stream(self, r, state):
+        """Random on Go's math/rand stream (ksim_engine_set_go_stream) from state = (vec[607], tap,
+        feed[, ...]) as Trace.go_state returns it; None restores the hash contract."""
+        if state is None:
+            check(lib().ksim_engine_set_go_stream(self.h, r, None, 0, 0), "set_go_stream")
+            return
+        vec = (C.c_uint64 * 607)(*state[0])
+        check(lib().ksim_engine_set_go_stream(self.h, r, vec, state[1], state[2]), "set_go_stream")
+
+    def set_shard_exchange(self, gather):
+        """Host exchange of a sharded engine (ksim_engine_set_shard_exchange): per pod step run()
+        calls gather(record) with this shard's 4-word record (a list of ints) and expects the
+        `world` shards' records in rank order (a flat list of 4 * world ints).  None clears it."""
+        if gather is None:
+            self._xfn = None
+            check(lib().ksim_engine_set_shard_exchange(self.h, None, None), "set_shard_exchange")
+            return
+        world = getattr(self, "_shard", (0, 0))[1]  # (set_shard first: the engine refuses otherwise)
+        self._xfn = exchange_cfunc(gather, world)  # kept alive as long as the engine may call it
+        check(lib().ksim_engine_set_shard_exchange(self.h, C.cast(self._xfn, C.c_void_p), None),
+              "set_shard_exchange")
 
     def set_report(self, enable=True):
         """Per-event cluster report (analysis.go:59-119) computed on the device by run()."""
@@ -524,6 +561,26 @@ class Engine:
 
 
 SHARD_ID_BYTES = 128
+# ksim_shard_exchange_fn
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p)
+
+
+def exchange_cfunc(gather, world):
+    """Wrap gather(record: 4 ints) -> 4 * world ints as a ksim_shard_exchange_fn; any exception or
+    a wrong-sized gather returns 1 (the engine then ends the run with KSIM_ESTATE)."""
+    def fn(send, recv, _user):
+        try:
+            out = gather([send[i] for i in range(4)])
+            if len(out) != 4 * world:
+                return 1
+            for i, v in enumerate(out):
+                recv[i] = int(v) & 0xFFFFFFFFFFFFFFFF
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the engine, which ends the run
+            import traceback
+            traceback.print_exc()
+            return 1
+    return EXCHANGE_FN(fn)
 
 
 def shard_comm_id():

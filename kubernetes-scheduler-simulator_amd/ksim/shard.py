@@ -78,19 +78,46 @@ class ShardGroup:
             e.close()
 
 
-def run_distributed(nodes, typical, events, n, dist, policy="FGD", seed=0, device=0, engine_cls=None):
+def host_gather(dist, group=None):
+    """A ksim_shard_exchange_fn body over torch.distributed (any backend with CPU tensors, e.g.
+    gloo): all-gather of the 4-word shard record, returned flat in rank order."""
+    import torch
+    world = dist.get_world_size(group)
+
+    def signed(v):
+        return v - (1 << 64) if v >= 1 << 63 else v
+
+    def gather(record):
+        t = torch.tensor([signed(v) for v in record], dtype=torch.int64)
+        out = [torch.empty(4, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return [int(v) & 0xFFFFFFFFFFFFFFFF for o in out for v in o.tolist()]
+    return gather
+
+
+def run_distributed(nodes, typical, events, n, dist, policy="FGD", seed=0, device=0, engine_cls=None,
+                    exchange="rccl"):
     """One shard per process (torchrun; backend nccl = RCCL for the launcher's own collectives):
     rank 0 makes the RCCL id of the shards' exchange, every rank builds its shard engine on
     `device`, replays the events, and the per-shard results are gathered and merged on every rank.
+    exchange="host": no RCCL communicator; every pod step's record goes through `dist` (host_gather),
+    e.g. shards sharing one GPU, or hosts without a common RCCL fabric.
     Returns (merged results, device ms of this rank's run)."""
     engine_cls = engine_cls or ksim.Engine
     rank, world = dist.get_rank(), dist.get_world_size()
     parts = partition(nodes, world)
     off, local, idx = parts[rank]
-    box = [shard_comm_id_for(engine_cls) if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
+    if exchange == "rccl":
+        box = [shard_comm_id_for(engine_cls) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+    elif exchange == "host":
+        box = [None]
+    else:
+        raise ValueError("exchange must be 'rccl' or 'host'")
     e = engine_cls(len(idx), 1, device=device)
     e.set_shard(rank, world, off, len(nodes), box[0])
+    if exchange == "host":
+        e.set_shard_exchange(host_gather(dist))
     e.set_nodes(0, local)
     arr, nt = typical
     e.set_typical(0, arr, nt)

@@ -49,7 +49,10 @@ class Sweep:
     policies (k_memo / k_replay) and, when the plan has PWR experiments, one for those (k_step +
     k_step_pwr per pod)."""
 
-    def __init__(self, experiments, device=0, report=True, wgs=0, fgd_batch=0):
+    def __init__(self, experiments, device=0, report=True, wgs=0, fgd_batch=0, random_stream="hash"):
+        """random_stream: "hash" (the Random contract) or "go" (the reference's draw
+        structure on Go's math/rand stream, k_random_go: ksim_engine_set_go_stream)."""
+        assert random_stream in ("hash", "go")
         self.exps = list(experiments)
         traces = {}
         for (t, _, _, _) in self.exps:
@@ -84,6 +87,8 @@ class Sweep:
                 eng.set_policy(r, ALL_POLICY_DIRS[p], seed=s)
                 if p in PWR_POLICY_DIRS:
                     eng.set_power_model(r, traces[t].power_model())
+                if p == "01-Random" and random_stream == "go":
+                    eng.set_go_stream(r, traces[t].go_state(seed=s, tune_ratio=tune, shuffle=True))
                 eng.load_events(r, rp.events, rp.n)
                 self.total_events += rp.n
             self.groups.append((eng, idx))

@@ -928,6 +928,60 @@ static uint64_t rand_node_key(uint64_t seed, int step, uint32_t rank) {
 }
 static uint64_t rand_gpu_key(uint64_t node_key, int g) { return orc_mix64(node_key ^ (uint64_t)(0x100 + g)); }
 
+/* Go math/rand (Go stdlib src/math/rand, outside the reference tree; go.mod:4 go 1.15): the global
+ * source the Random draw structure consumes.  rng.go rngSource: Seed expands the seed with the
+ * Park-Miller step seedrand and XORs rngCooked; Uint64 is the additive lagged Fibonacci generator
+ * (length 607, tap 273).  rand.go: Int63 = Uint64 masked to 63 bits, Int31 = Int63 >> 32, Int31n
+ * by rejection above the largest multiple of n (a power of two masks Int31, n = 1 included: it
+ * still draws), Intn(n <= 2^31-1) = Int31n.  The rngCooked data table is the one
+ * tools/gen_go_rng_cooked.c recomputes (tests/test_go_rand.py pins it against Go's published
+ * rand.Seed(1) outputs, for this restatement too). */
+static const int64_t orc_rng_cooked[ORC_GO_LEN] = {
+#include "../kubernetes-scheduler-simulator_amd/csrc/go_rng_cooked.inc"
+};
+static int32_t go_seedrand(int32_t x) { /* rng.go seedrand: x * 48271 mod (2^31 - 1), Schrage */
+    const int32_t a = 48271, q = 44488, r = 3399;
+    int32_t hi = x / q, lo = x % q;
+    x = a * lo - r * hi;
+    if (x < 0) x += 2147483647;
+    return x;
+}
+void orc_go_seed(orc_go_rng* g, int64_t seed) {
+    g->tap = 0;
+    g->feed = ORC_GO_LEN - ORC_GO_TAP;
+    seed %= 2147483647;
+    if (seed < 0) seed += 2147483647;
+    if (seed == 0) seed = 89482311;
+    int32_t x = (int32_t)seed;
+    for (int i = -20; i < ORC_GO_LEN; i++) {
+        x = go_seedrand(x);
+        if (i >= 0) {
+            uint64_t u = (uint64_t)(int64_t)x << 40;
+            x = go_seedrand(x);
+            u ^= (uint64_t)(int64_t)x << 20;
+            x = go_seedrand(x);
+            u ^= (uint64_t)(int64_t)x;
+            u ^= (uint64_t)orc_rng_cooked[i];
+            g->vec[i] = u;
+        }
+    }
+}
+uint64_t orc_go_uint64(orc_go_rng* g) {
+    if (--g->tap < 0) g->tap += ORC_GO_LEN;
+    if (--g->feed < 0) g->feed += ORC_GO_LEN;
+    g->vec[g->feed] += g->vec[g->tap];
+    return g->vec[g->feed];
+}
+static int32_t go_int31(orc_go_rng* g) { return (int32_t)((orc_go_uint64(g) & 0x7fffffffffffffffULL) >> 32); }
+int32_t orc_go_int31n(orc_go_rng* g, int32_t n) {
+    if (n <= 0) return -1; /* Go panics */
+    if ((n & (n - 1)) == 0) return go_int31(g) & (n - 1);
+    const int32_t max = (int32_t)((1u << 31) - 1 - (1u << 31) % (uint32_t)n);
+    int32_t v = go_int31(g);
+    while (v > max) v = go_int31(g);
+    return v % n;
+}
+
 typedef struct {
     int64_t cpu_req, mem_req;  /* nodeInfo.Requested */
     int32_t pods;
@@ -1138,6 +1192,12 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
 
     int64_t arrived_gpu = 0, arrived_cpu = 0;
     int threads = pol.threads > 1 ? pol.threads : 1;
+    /* the Random draw structure: a private copy of the Go stream (orc_policy.go_stream) */
+    orc_go_rng* go = NULL;
+    if (pol.go_stream) {
+        go = (orc_go_rng*)malloc(sizeof *go);
+        *go = *pol.go_stream;
+    }
     for (int s = 0; s < n_ev; s++) {
         const orc_event* e = &ev[s];
         orc_result* R = &res[s];
@@ -1163,6 +1223,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
             }
         } else {
             orc_pod_resource pr = pod_res_of(e);
+            if (go) (void)orc_go_int31n(go, 100); /* scheduler.go:464 SetRecordPluginMetrics(rand.Intn(100) < ..) */
             arrived_gpu += pr.milli_gpu * pr.gpu_number;  /* simulator.go:401-402 */
             arrived_cpu += pr.milli_cpu;
             memset(err, 0, (size_t)n_nodes * sizeof(int32_t));
@@ -1187,6 +1248,10 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
             int64_t wscore = 0;
             if (nf == 0) {
                 R->status = 1;
+                /* scheduler.go:474-480 PostFilter -> DefaultPreemption.FindCandidates: every node is
+                 * Unschedulable (not ...AndUnresolvable), so the offset draw is over all of them
+                 * (default_preemption.go:197-212,183) */
+                if (go && n_nodes > 0) (void)orc_go_int31n(go, n_nodes);
             } else if (nf == 1) {
                 winner = fidx[0]; /* generic_scheduler.go:158-164 */
             } else {
@@ -1196,7 +1261,14 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                     fs2[k] = raw2[fidx[k]];
                     if (err[fidx[k]]) anyerr = 1;
                 }
-                if (pol.policy == ORC_POL_RANDOM) {
+                /* random_score.go:42-51: RandomScorePlugin.PreScore is enabled for every policy
+                 * (utils.go:241-248) and runs after Filter when two or more nodes are feasible */
+                const int go_pick = go ? (int)orc_go_int31n(go, nf) : -1;
+                if (pol.policy == ORC_POL_RANDOM && go) {
+                    /* random_score.go:53-68: MaxNodeScore for the PreScore pick, MinNodeScore else; the
+                     * feasible list in node order (one filter worker: parallelize.Until's order) */
+                    for (int k = 0; k < nf; k++) fs[k] = k == go_pick ? 100 : 0;
+                } else if (pol.policy == ORC_POL_RANDOM) {
                     /* random_score.go:42-68: PreScore picks one feasible node (Random contract) */
                     int pick = -1;
                     uint64_t best = 0;
@@ -1267,7 +1339,14 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                         break;
                     }
                     case ORC_SEL_RANDOM:
-                        if (pr.milli_gpu < ORC_MILLI) {
+                        if (go && pr.milli_gpu < ORC_MILLI) {
+                            /* open_gpu_share.go:274-276 panic first; :325-343 reservoir draw per fitting GPU */
+                            int pick = -1, cnt = 0;
+                            if (pr.gpu_number > 1) { mask = -1; break; }
+                            for (int g = 0; g < nr.n_gpu_left; g++)
+                                if (nr.milli_gpu_left[g] >= pr.milli_gpu && orc_go_int31n(go, ++cnt) == 0) pick = g;
+                            mask = pick < 0 ? -1 : (1 << pick);
+                        } else if (pr.milli_gpu < ORC_MILLI) {
                             uint64_t nk = rand_node_key(pol.seed, s, rank[winner]);
                             int pick = -1;
                             uint64_t best = 0;
@@ -1341,6 +1420,7 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
         }
     }
     free(dyn); free(feas); free(raw); free(gm); free(err); free(fidx); free(fs); free(rank); free(order); free(raw2); free(fs2);
+    free(go);
     return 0;
 }
 

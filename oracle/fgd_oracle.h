@@ -204,6 +204,17 @@ typedef struct {
                                            orc_fix80 in fgd_oracle.c; the product's contract) */
 } orc_report;
 
+/* Go math/rand's global source (rng.go rngSource), for the Random draw structure */
+#define ORC_GO_LEN 607
+#define ORC_GO_TAP 273
+typedef struct {
+    int32_t tap, feed;
+    uint64_t vec[ORC_GO_LEN];
+} orc_go_rng;
+void     orc_go_seed(orc_go_rng* g, int64_t seed);      /* rand.Seed */
+uint64_t orc_go_uint64(orc_go_rng* g);                  /* rngSource.Uint64 */
+int32_t  orc_go_int31n(orc_go_rng* g, int32_t n);       /* Rand.Int31n (= Intn for n < 2^31) */
+
 typedef struct {
     int32_t policy;
     int32_t gpu_sel;
@@ -211,6 +222,13 @@ typedef struct {
     int32_t threads;               /* >1: parallelize.Until-style worker fan-out over nodes */
     int32_t w_pwr, w_fgd;          /* ORC_POL_PWR_FGD plugin weights (scheduler config score weights) */
     int32_t dim_ext, norm;         /* ORC_POL_DOTPROD GpuPluginCfg (ORC_DIM_*, ORC_NORM_*) */
+    /* non-NULL: the Random draw structure on Go's global math/rand stream, starting from this
+     * state (the stream after the replay's own draws; copied, not modified).  Per creation event:
+     * scheduler.go:464 Intn(100); no feasible node: default_preemption.go:183 Int31n(#nodes);
+     * two or more: random_score.go:44 Intn(#feasible), the node at that index of the feasible list
+     * in node order (PreScore runs for every policy; Random's Score picks that node); Reserve with
+     * the random GPU selector: open_gpu_share.go:333 Intn(k) at the k-th fitting GPU. */
+    const orc_go_rng* go_stream;
 } orc_policy;
 
 /* Replays n events on a fresh cluster.  results[n]; reports[n] may be NULL. */

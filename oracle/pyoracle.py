@@ -68,9 +68,30 @@ class Report(C.Structure):
                 ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64), ("frag_bins_exact", C.c_double * 7)]
 
 
+class GoRng(C.Structure):
+    """orc_go_rng: Go math/rand's rngSource state (rng.go)."""
+    _fields_ = [("tap", C.c_int32), ("feed", C.c_int32), ("vec", C.c_uint64 * 607)]
+
+
 class Policy(C.Structure):
     _fields_ = [("policy", C.c_int32), ("gpu_sel", C.c_int32), ("seed", C.c_uint64), ("threads", C.c_int32),
-                ("w_pwr", C.c_int32), ("w_fgd", C.c_int32), ("dim_ext", C.c_int32), ("norm", C.c_int32)]
+                ("w_pwr", C.c_int32), ("w_fgd", C.c_int32), ("dim_ext", C.c_int32), ("norm", C.c_int32),
+                ("go_stream", C.POINTER(GoRng))]
+
+
+def go_seed(seed):
+    """rand.Seed(seed): a GoRng (the oracle's restatement)."""
+    g = GoRng()
+    lib().orc_go_seed(C.byref(g), C.c_int64(seed))
+    return g
+
+
+def go_uint64(g, n=1):
+    return [lib().orc_go_uint64(C.byref(g)) for _ in range(n)]
+
+
+def go_int31n(g, n):
+    return lib().orc_go_int31n(C.byref(g), n)
 
 
 class NodeState(C.Structure):
@@ -100,6 +121,12 @@ def lib():
         L.orc_frag_amount_sum_except_q3.restype = C.c_double
         L.orc_node_gpu_share_frag_amount_score.argtypes = [P(NodeResource), P(TargetPod), C.c_int]
         L.orc_node_gpu_share_frag_amount_score.restype = C.c_double
+        L.orc_go_seed.argtypes = [P(GoRng), C.c_int64]
+        L.orc_go_seed.restype = None
+        L.orc_go_uint64.argtypes = [P(GoRng)]
+        L.orc_go_uint64.restype = C.c_uint64
+        L.orc_go_int31n.argtypes = [P(GoRng), C.c_int32]
+        L.orc_go_int31n.restype = C.c_int32
         L.orc_go_exp.argtypes = [C.c_double]
         L.orc_go_exp.restype = C.c_double
         L.orc_sigmoid.argtypes = [C.c_double]
@@ -266,9 +293,10 @@ def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_w
 
 
 def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
-               with_report=False, w_pwr=0, w_fgd=0, dim_ext=DIM_MERGE, norm=NORM_MAX):
+               with_report=False, w_pwr=0, w_fgd=0, dim_ext=DIM_MERGE, norm=NORM_MAX, go_stream=None):
     """nodes: list of dicts {name,cpu,mem,pods,gpu,model}; events: list of dicts
-    {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]"""
+    {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]
+    go_stream: a GoRng (or (vec, tap, feed)) = the Random draw structure on Go's stream from that state"""
     nn = len(nodes)
     ns = (NodeSpec * nn)()
     for i, d in enumerate(nodes):
@@ -288,7 +316,15 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
     res = (Result * max(1, ne))()
     rep = (Report * max(1, ne))() if with_report else None
     st = (NodeState * nn)()
-    pol = Policy(policy, gpu_sel, seed, threads, w_pwr, w_fgd, dim_ext, norm)
+    gs = None
+    if go_stream is not None:
+        if isinstance(go_stream, GoRng):
+            gs = go_stream
+        else:
+            vec, tap, feed = go_stream
+            gs = GoRng(tap, feed, (C.c_uint64 * 607)(*vec))
+    pol = Policy(policy, gpu_sel, seed, threads, w_pwr, w_fgd, dim_ext, norm,
+                 C.pointer(gs) if gs is not None else None)
     rc = lib().orc_run_events_state(ns, nn, tp, nt, pol, ev, ne, res, rep, st)
     assert rc == 0
     results = [(res[i].node, res[i].gpu_mask, res[i].score, res[i].n_feasible, res[i].status) for i in range(ne)]

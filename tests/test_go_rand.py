@@ -130,3 +130,28 @@ def test_informer_draws_are_what_pins_the_node_names():
     assert a.n == b.n and list(a.pod_index[:a.n]) == list(b.pod_index[:b.n])
     assert list(a.prefix) != list(b.prefix)
     assert list(t.replay(seed=42, informer_draws=10).prefix) == list(a.prefix)
+
+
+def test_oracle_go_source_published_outputs():
+    # the oracle's own restatement of the source (fgd_oracle.c orc_go_*), which checks the Random
+    # draw structure on the device: Go's seed-1 outputs, Int63 and Intn(100) (= Int31n)
+    import pyoracle as O
+    g = O.go_seed(1)
+    assert [v & ((1 << 63) - 1) for v in O.go_uint64(g, 10)] == SEED1_INT63
+    g = O.go_seed(1)
+    assert [O.go_int31n(g, 100) for _ in range(10)] == SEED1_INTN100
+    g = O.go_seed(1)
+    assert [O.go_int31n(g, 1 << 20) for _ in range(10)] == [(x >> 32) & ((1 << 20) - 1) for x in SEED1_INT63]
+
+
+@pytest.mark.parametrize("trace,seed,tune", [("default", 42, 1.3), ("multigpu50", 51, 1.3), ("default", 7, 0.0)])
+def test_replay_go_state_is_seed_plus_the_replays_draws(trace, seed, tune):
+    # ksim_trace_replay_go_state (the stream the first scheduling cycle finds) == rand.Seed(seed)
+    # advanced by exactly the replay's draw count, by the oracle's restatement
+    import pyoracle as O
+    t = ksim.Trace.openb(trace)
+    vec, tap, feed, draws = t.go_state(seed=seed, tune_ratio=tune)
+    assert draws > 1000  # rand.Int, the shuffle, the tuning draws, the informers' and rand.Perm
+    g = O.go_seed(seed)
+    O.go_uint64(g, draws)
+    assert (list(g.vec), g.tap, g.feed) == (vec, tap, feed)

@@ -102,3 +102,99 @@ def test_rccl_world1(default_trace):
     e.close()
     assert got == unsharded(default_trace, rp.nodes, rp.events, n_ev, "FGD")
     print("sharded world 1 over RCCL: %d steps in %.1f ms (%.1f us/step)" % (n_ev, ms, ms * 1e3 / n_ev))
+
+
+def _host_shard_engine(trace, nodes, n_ev, events, gather, policy="FGD"):
+    arr, n = trace.typical()
+    parts = SH.partition(nodes, 1)
+    e = ksim.Engine(len(nodes), 1)
+    e.set_shard(0, 1, 0, len(nodes))
+    e.set_shard_exchange(gather)
+    e.set_nodes(0, parts[0][1])
+    e.set_typical(0, arr, n)
+    e.set_policy(0, policy)
+    e.load_events(0, events, n_ev)
+    return e, parts
+
+
+def test_host_exchange_world1(default_trace):
+    # the host exchange (ksim_engine_set_shard_exchange) with the identity gather of a world of one
+    rp = default_trace.replay(seed=42)
+    n_ev = 800
+    calls = []
+
+    def gather(rec):
+        calls.append(rec)
+        return list(rec)
+    e, parts = _host_shard_engine(default_trace, rp.nodes, n_ev, rp.events, gather)
+    e.run()
+    got = SH.merge_results([e.results(0)], parts)
+    e.close()
+    assert len(calls) == n_ev
+    assert got == unsharded(default_trace, rp.nodes, rp.events, n_ev, "FGD")
+
+
+@pytest.mark.parametrize("bad", ["raise", "size", "foreign"])
+def test_host_exchange_bad_gather_fails(default_trace, bad):
+    rp = default_trace.replay(seed=42)
+
+    def gather(rec):
+        if bad == "raise":
+            raise RuntimeError("transport down")
+        if bad == "size":
+            return list(rec) + [0]
+        return [rec[0] ^ 1] + list(rec[1:])  # not this shard's record at its rank
+    e, _ = _host_shard_engine(default_trace, rp.nodes, 50, rp.events, gather)
+    with pytest.raises(ksim.KsimError) as ei:
+        e.run()
+    e.close()
+    assert ei.value.code == ksim.KSIM_ESTATE
+
+
+def _host_rank_main(rank, world, port, policy, n_ev, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = ksim.Trace.openb("default")
+    rp = t.replay(seed=7)
+    nodes = helpers.subset_nodes(rp, list(range(1, t.num_nodes, 5)))
+    merged, ms = SH.run_distributed(nodes, t.typical(), rp.events, n_ev, dist, policy=policy, seed=3,
+                                    exchange="host")
+    q.put((rank, merged, ms))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("name,pol,sel", [POLICIES[0], POLICIES[1]], ids=["FGD", "BestFit"])
+def test_host_exchange_two_processes(default_trace, name, pol, sel):
+    # two shard processes on the one GPU, their per-step records exchanged over gloo: the shard
+    # kernels and the commit of the multi-process mode with a real cross-process exchange (RCCL
+    # refuses two ranks on one device, so the ncclAllGather itself stays world-1 here)
+    # stdlib multiprocessing: torch (which carries its own HIP runtime) is imported by the ranks
+    # only, never into this process, whose engines already hold /opt/rocm's
+    import multiprocessing as mp
+    import socket
+    n_ev = 600
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_host_rank_main, args=(r, 2, port, name, n_ev, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=200) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    rp = default_trace.replay(seed=7)
+    keep = list(range(1, default_trace.num_nodes, 5))
+    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    want, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
+                              helpers.oracle_events(default_trace, rp, n_ev), policy=pol, gpu_sel=sel, seed=3,
+                              threads=16)
+    assert res[0][1] == want and res[1][1] == want
+    print("host exchange world 2 (%s): %d steps, rank times %.1f / %.1f ms" % (name, n_ev, res[0][2], res[1][2]))

@@ -143,3 +143,38 @@ def test_gloo_world2_sharded_protocol():
         p.join(30)
         assert p.exitcode == 0
     assert [r[1] for r in res] == [True, True] and res[0][2] > 100
+
+
+def _gather_main(rank, world, port, q):
+    import ctypes as C
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fn = ksim.exchange_cfunc(SH.host_gather(dist), world)
+    send = (C.c_uint64 * 4)(0xFFFFFFFFFFFFFFFF - rank, rank, 1 << 63 | rank, 12345 + rank)
+    recv = (C.c_uint64 * (4 * world))()
+    rc = fn(send, recv, None)  # called through the C function pointer, as the engine calls it
+    bad = ksim.exchange_cfunc(lambda rec: rec, world)(send, recv, None)  # a wrong-sized gather
+    q.put((rank, rc, bad, list(recv)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_host_gather():
+    # the host-exchange transport of ksim.shard.run_distributed(exchange="host"): the 4-word u64
+    # records of both ranks, high bit included, in rank order on every rank
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    want = [0xFFFFFFFFFFFFFFFF, 0, 1 << 63, 12345, 0xFFFFFFFFFFFFFFFE, 1, (1 << 63) | 1, 12346]
+    for rank, rc, bad, recv in res:
+        assert rc == 0 and bad == 1 and recv == want
