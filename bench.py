@@ -48,6 +48,8 @@ def profile_key(args):
         k += "-report"
     if args.sharded:
         k += "-sharded"
+    if getattr(args, "random_stream", "hash") == "go":
+        k += "-go"
     return k
 
 
@@ -203,6 +205,9 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="c5 only: ONE cluster node-sharded over the ranks (RCCL exchange per pod; strong "
                          "scaling) instead of one replica per rank")
+    ap.add_argument("--random-stream", default="hash", choices=["hash", "go"],
+                    help="Random policy: the hash contract (default) or the reference's draw structure on Go's "
+                         "math/rand stream (k_random_go)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,7 +232,7 @@ def main():
     if args.config == "c4":
         import ksim.sweep as SW
         exps = SW.shard(SW.plan(), rank, world)
-        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs)
+        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs, random_stream=args.random_stream)
         eng = sweep.eng
         eng.total_events = sweep.total_events
         eng.memo_replicas = sweep.fgd_replicas()
@@ -244,11 +249,11 @@ def main():
         args.replicas = 1
         seeds = [2 * rank + 1]
         eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
-                         tune=0.0, shuffle=False, report=args.report)
+                         tune=0.0, shuffle=False, report=args.report, random_stream=args.random_stream)
     else:
         seeds = seeds_for_rank(rank, args.replicas)
         eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
-                         report=args.report)
+                         report=args.report, random_stream=args.random_stream)
     total_events = eng.total_events
 
     for _ in range(args.warmup):
@@ -340,6 +345,8 @@ def main():
         line["config"]["workload"] = line["config"]["workload"].replace("FGD", args.policy)
     if args.report:
         line["config"]["report"] = True
+    if args.random_stream == "go":
+        line["config"]["random_stream"] = "go"  # Random replicas on Go's math/rand draw structure
     if args.config == "c4" or args.report:
         line["report_ms_per_step"] = eng.last_report_ms()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
@@ -374,7 +381,7 @@ def _sharded_engine(device, rank, world, trace, dist):
 
 
 def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_mode=0, tune=1.3, shuffle=True,
-               report=False):
+               report=False, random_stream="hash"):
     arr, n = trace.typical()
     eng = ksim.Engine(trace.num_nodes, len(seeds), device=device, nodes_per_block=nodes_per_block,
                       wgs_per_replica=wgs, run_mode=run_mode)
@@ -388,6 +395,8 @@ def _engine_on(device, trace, seeds, nodes_per_block, policy="FGD", wgs=0, run_m
         eng.set_policy(r, policy)
         if ksim.parse_policy(policy)[0] in ("PWR", "PWR+FGD"):
             eng.set_power_model(r, trace.power_model())
+        if policy == "Random" and random_stream == "go":
+            eng.set_go_stream(r, trace.go_state(seed=s, tune_ratio=tune, shuffle=shuffle))
         eng.load_events(r, rp.events, rp.n)
         total += rp.n
     eng.total_events = total

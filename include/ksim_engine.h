@@ -310,13 +310,15 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 /* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),
  * KSIM_PATH_MEMO (k_memo, memoised FGD keys), KSIM_PATH_MIXED (a memoised kernel for the FGD replicas,
  * k_replay for the others), KSIM_PATH_STEP (k_step per pod, hipGraph), KSIM_PATH_SHARDED (node-sharded),
- * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica). */
+ * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica), KSIM_PATH_RANDOM_GO
+ * (k_random_go: every replica Random on Go's stream, ksim_engine_set_go_stream). */
 #define KSIM_PATH_REPLAY  0
 #define KSIM_PATH_MEMO    1
 #define KSIM_PATH_MIXED   2
 #define KSIM_PATH_STEP    3
 #define KSIM_PATH_SHARDED 4
 #define KSIM_PATH_HMEMO   5
+#define KSIM_PATH_RANDOM_GO 6
 int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus

@@ -1577,6 +1577,7 @@ struct ksim_engine {
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
   size_t h_cap[14] = {};
   int last_hmemo = 0;
+  int last_rgo = 0;  // replicas the last run replayed on k_random_go
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
   bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
@@ -3164,6 +3165,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   int first = 0;
   e->last_memo = 0;
   e->last_hmemo = 0;
+  e->last_rgo = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
   // co-residency needed) run concurrently on side streams: a paper-sweep group fills 170 of 256 CUs,
   // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
@@ -3217,6 +3219,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       }
       KSIM_HIP(hipGetLastError());
       e->last_groups = (int)groups.size();
+      e->last_rgo += Rg;
       first += Rg;
       continue;
     }
@@ -3535,6 +3538,7 @@ int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   if (!e || !path) return KSIM_EINVAL;
   if (e->shard_world > 0) *path = KSIM_PATH_SHARDED;
   else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
+  else if (e->last_rgo == e->R) *path = KSIM_PATH_RANDOM_GO;
   else if (e->last_memo == 0 && e->last_hmemo == 0) *path = KSIM_PATH_REPLAY;
   else if (e->last_memo == e->R) *path = KSIM_PATH_MEMO;
   else if (e->last_hmemo == e->R) *path = KSIM_PATH_HMEMO;

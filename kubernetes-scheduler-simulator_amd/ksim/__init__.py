@@ -525,11 +525,11 @@ class Engine:
         return s.value
 
     def last_run_path(self):
-        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo': the kernels the last run()
+        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go': the kernels the last run()
         used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
-        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo"][k.value]
+        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)

@@ -14,6 +14,7 @@ for name in "$@"; do
     c2-PWR_500_FGD_500) a="--policy PWR_500_FGD_500";;
     c2-DotProd) a="--policy DotProd";;
     c2-report) a="--report";;
+    c2-Random-go) a="--policy Random --random-stream go";;
     c4) a="--config c4";;
     c5) a="--config c5";;
     *) echo "unknown configuration $name"; exit 2;;
