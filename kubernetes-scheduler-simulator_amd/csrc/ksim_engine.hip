@@ -2274,7 +2274,8 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     const int nwg = Rg * pl.K;
     std::vector<unsigned long long> h((size_t)nwg * kHProf);
     KSIM_HIP(hipMemcpy(h.data(), e->d_h_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    static const char* names[] = {"list | class pass", "-", "F + flagged blocks", "-", "keys + class update", "decide+bind"};
+    static const char* names[] = {"list | class pass", "(wave 0 F, inside the next)", "F + flagged blocks", "-", "-",
+                                   "class update | decide+bind"};
     std::fprintf(stderr, "ksim hmemo profile: %d replicas x K=%d (S %d), LDS %zu B, Cmax %d Gmax %d Smax %d; us/step mean [max]:",
                  Rg, pl.K, pl.S, pl.lds, pl.Cmax, pl.Gmax, pl.Smax);
     const double steps = std::max(max_ev, 1);

@@ -384,7 +384,10 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
                                  : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
           if (q == 0) s_F[j] = F;
         }
-        if (prof && tid == 0) { sh.prof[7] += (unsigned long long)nit; sh.prof[8] += (unsigned long long)nflag; sh.prof[9] += 1ull; }
+        if (prof && tid == 0) {
+          sh.prof[7] += (unsigned long long)nit; sh.prof[8] += (unsigned long long)nflag; sh.prof[9] += 1ull;
+          sh.prof[1] += __builtin_amdgcn_s_memrealtime() - t_last;  // wave 0's own F evaluations (inside phase 2)
+        }
       }
       if (qid < nflag) {
         const unsigned m = block_max_excl(bv, (b0 + b) * kFan, l16, d);
@@ -398,43 +401,62 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       }
       __syncthreads();
       mark(2);
-      // ---- 3. every class: its group's key on d (if d passes the class's Filter), the key, its L1
-      //         entry, its feasible count
-      {
-        const double F0 = s_F[0];
-        const int nit = sh.nitems;
-        for (int c = tid; c < C; c += kHBlock) {
-          const bool fn = s_fnew[c] != 0;
-          unsigned k = 0u;
-          if (fn) {
-            const int g = s_cgrp[c];
-            const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
-            if (is_share_pod(s_gpod[g])) {
-              k = hkey(0, d, 0);  // feasible with no fitting GPU
-              for (int i = o; i < oe; ++i) {
-                const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
-                k = x > k ? x : k;
-              }
-            } else {
-              k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
+    }
+    // ---- 3 + 4. the class update beside the event: wave 0 updates the event's own class (the only
+    //      one the decision reads) and then decides, while waves 1-15 update every other class
+    const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);  // the event's class, -1 delete
+    const int own = d >= 0 ? cs : -1;                            // the class wave 0 updates itself
+    if (d >= 0) {
+      const int b = d / kFan - b0;
+      const double F0 = s_F[0];
+      const int nit = sh.nitems;
+      // the group's key on d (if d passes the class's Filter: fn), from its candidates' F
+      auto class_key = [&](int c, bool fn, int i0) -> unsigned {
+        unsigned k = 0u;
+        if (fn) {
+          const int g = s_cgrp[c];
+          const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
+          if (is_share_pod(s_gpod[g])) {
+            k = hkey(0, d, 0);  // feasible with no fitting GPU
+            for (int i = o + (i0 < 0 ? 0 : i0); i < oe; i += (i0 < 0 ? 1 : 64)) {  // i0 < 0: all, serially
+              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
+              k = x > k ? x : k;
             }
+          } else if (i0 <= 0) {
+            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
           }
-          gst1(keys + (size_t)c * a.Npad + d, k);
-          s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
-          unsigned* l = &s_l1[c * nb + b];
-          const unsigned old = *l;
-          if (k > old) *l = k;
-          else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
         }
+        return k;
+      };
+      // its key, L1 entry and feasible count
+      auto class_store = [&](int c, bool fn, unsigned k) {
+        gst1(keys + (size_t)c * a.Npad + d, k);
+        s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
+        unsigned* l = &s_l1[c * nb + b];
+        const unsigned old = *l;
+        if (k > old) *l = k;
+        else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
+      };
+      if (wv != 0) {
+        for (int c = tid - 64; c < C; c += kHBlock - 64) {
+          if (c == own) continue;
+          const bool fn = s_fnew[c] != 0;
+          class_store(c, fn, class_key(c, fn, -1));
+        }
+      } else if (own >= 0) {
+        // lane i scores candidate i of the group (<= 8), the wave keeps the max; lane 0 stores
+        const bool fn = s_fnew[own] != 0;
+        const unsigned k = (unsigned)wave_max_dpp((int)class_key(own, fn, lane));
+        if (lane == 0) class_store(own, fn, k);
+        // the decision below reads this class's L1 row and count: the wave's LDS operations in order
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
       }
       if (tid == 0) sh.nflag = 0;
-      __syncthreads();
-      mark(4);
     }
     // ---- 4. the event: the winner of its class (create) or the unbind (delete); wave 0
     if (wv == 0) {
       const PodDev p = uniform_pod(&sh.ev[eb]);
-      const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
       int rk = -1, mask = 0;
       bool write = false;
       NodeV before{}, after{};

@@ -288,52 +288,69 @@ __device__ __forceinline__ void fgd_candidate(const NodeV& m, int code, const Po
 
 // F = NodeGpuShareFragAmountScore of one state (frag.go:148-203, 411-418, 460-493),
 // evaluated by the 4 lanes of a quad (q = lane & 3); every lane returns the same F.
-//   CPU-only typical pods [0, ncpu): scalar table loads; lane 0 folds XL, lane 1 XR.
-//   GPU typical pods [ncpu, nt): lane q classifies t = tb+q from the LDS table --
-//     cnt / frag over the 8 packed GPUs with v_pk_sub_i16 + v_pk_lshrrev_b16 +
-//     v_dot2_u32_u16 -- into (bin, value); the quad then folds t = tb..tb+3 in order
-//     and lane q keeps bin q (0 = Q1, 1 = Q2 + Q3's frag part, 2 = Q4, 3 = NA).
+//   Rounds of four typical pods: lane q classifies t = tb+q from the LDS table `ltp`, the
+//   quad then folds t = tb..tb+3 in order (DPP quad broadcasts) and lane q keeps bin q.
+//   CPU-only typical pods [0, ncpu): lane 0 keeps XL, lane 1 XR.
+//   GPU typical pods [ncpu, nt): cnt / frag over the 8 packed GPUs with v_pk_sub_i16 +
+//     v_pk_lshrrev_b16 + v_dot2_u32_u16, bins 0 = Q1, 1 = Q2 + Q3's frag part, 2 = Q4,
+//     3 = NA; two rounds per loop iteration, so both rounds' LDS loads are in flight at once.
+//   `tp` (the global copy of the table) is unused.
 // Every bin is the same sequence of fp64 adds as frag_F's (adding +0.0 for the
 // typical pods that do not touch it), so F is bit-identical.
 template <bool kTyped>
 __device__ __forceinline__ double frag_F_quad(int cpuL, const uint32_t (&g)[4], int total, uint32_t typebit,
                                               const TypDev* __restrict__ tp, const TypDev* ltp, int ncpu, int nt,
                                               int q) {
+  (void)tp;
   const double dtot = (double)total;
+  // CPU-only typical pods, four per round like the GPU ones below: lane q classifies t = tb+q from
+  // the LDS table, the quad folds the round in order, lane 0 keeps XL and lane 1 XR
   double bc = 0.0;
-  for (int t = 0; t < ncpu; ++t) {
-    const double x = tp[t].freq * dtot;  // freq * float64(gpuMilliLeftTotal)
-    const bool cpu_ok = cpuL >= tp[t].cpu;
-    bc += (cpu_ok == (q == 0)) ? x : 0.0;
+  for (int tb = 0; tb < ncpu; tb += 4) {
+    const int t = min(tb + q, max(nt - 1, 0));
+    const double x = ltp[t].freq * dtot;  // freq * float64(gpuMilliLeftTotal)
+    int code = cpuL >= ltp[t].cpu ? 0 : 1;
+    code = tb + q < ncpu ? code : 4;
+    int cj;
+    double vj;
+    cj = qbc<0>(code); vj = qbc_d<0>(x); bc += (cj == q) ? vj : 0.0;
+    cj = qbc<1>(code); vj = qbc_d<1>(x); bc += (cj == q) ? vj : 0.0;
+    cj = qbc<2>(code); vj = qbc_d<2>(x); bc += (cj == q) ? vj : 0.0;
+    cj = qbc<3>(code); vj = qbc_d<3>(x); bc += (cj == q) ? vj : 0.0;
   }
   double bg = 0.0;
-  TypDev en = ltp[min(ncpu + q, nt - 1)];
-  for (int tb = ncpu; tb < nt; tb += 4) {
-    const TypDev e = en;
-    en = ltp[min(tb + 4 + q, nt - 1)];  // prefetch the next round's entry
-    const uint32_t mp = (uint32_t)e.milli * 0x10001u;
-    uint32_t frag = 0u, nlt = 0u;
+  // two rounds per iteration: both rounds' table entries are loaded before the first is classified
+  const int tmax = max(nt - 1, 0);
+  for (int tb0 = ncpu; tb0 < nt; tb0 += 8) {
+    const TypDev e2[2] = {ltp[min(tb0 + q, tmax)], ltp[min(tb0 + 4 + q, tmax)]};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
-      const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
-      frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
-      nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
+    for (int h = 0; h < 2; ++h) {
+      const int tb = tb0 + 4 * h;
+      const TypDev e = e2[h];
+      const uint32_t mp = (uint32_t)e.milli * 0x10001u;
+      uint32_t frag = 0u, nlt = 0u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u16x2 gv = __builtin_bit_cast(u16x2, g[i]);
+        const u16x2 lt = (u16x2)(gv - __builtin_bit_cast(u16x2, mp)) >> (u16x2){15, 15};  // left < milli
+        frag = __builtin_amdgcn_udot2(gv, lt, frag, false);  // GetGpuFragMilliByNodeResAndPodRes (frag.go:205-213)
+        nlt = __builtin_amdgcn_udot2(lt, (u16x2){1, 1}, nlt, false);
+      }
+      const bool gpu_ok = kMaxGpu - (int)nlt >= e.num_eff;  // CanNodeHostPodOnGpuMemory (frag.go:447-458)
+      const bool cpu_ok = cpuL >= e.cpu;
+      const bool acc = !kTyped || (e.tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
+      const double x = e.freq * dtot;
+      const double y = e.freq * (double)(int)frag;           // freq * float64(gpuFragMilli)
+      int code = acc ? (cpu_ok ? 1 : (gpu_ok ? 2 : 0)) : 3;
+      code = tb + q < nt ? code : 4;
+      const double v = (acc && cpu_ok && gpu_ok) ? y : x;
+      double vj;
+      int cj;
+      cj = qbc<0>(code); vj = qbc_d<0>(v); bg += (cj == q) ? vj : 0.0;
+      cj = qbc<1>(code); vj = qbc_d<1>(v); bg += (cj == q) ? vj : 0.0;
+      cj = qbc<2>(code); vj = qbc_d<2>(v); bg += (cj == q) ? vj : 0.0;
+      cj = qbc<3>(code); vj = qbc_d<3>(v); bg += (cj == q) ? vj : 0.0;
     }
-    const bool gpu_ok = kMaxGpu - (int)nlt >= e.num_eff;  // CanNodeHostPodOnGpuMemory (frag.go:447-458)
-    const bool cpu_ok = cpuL >= e.cpu;
-    const bool acc = !kTyped || (e.tmask & typebit) != 0u;  // IsNodeAccessibleToPod (utils.go:957-1006)
-    const double x = e.freq * dtot;
-    const double y = e.freq * (double)(int)frag;           // freq * float64(gpuFragMilli)
-    int code = acc ? (cpu_ok ? 1 : (gpu_ok ? 2 : 0)) : 3;
-    code = tb + q < nt ? code : 4;
-    const double v = (acc && cpu_ok && gpu_ok) ? y : x;
-    double vj;
-    int cj;
-    cj = qbc<0>(code); vj = qbc_d<0>(v); bg += (cj == q) ? vj : 0.0;
-    cj = qbc<1>(code); vj = qbc_d<1>(v); bg += (cj == q) ? vj : 0.0;
-    cj = qbc<2>(code); vj = qbc_d<2>(v); bg += (cj == q) ? vj : 0.0;
-    cj = qbc<3>(code); vj = qbc_d<3>(v); bg += (cj == q) ? vj : 0.0;
   }
   const double b0 = qbc_d<0>(bg), b1 = qbc_d<1>(bg), b3 = qbc_d<2>(bg), b6 = qbc_d<3>(bg);
   const double b4 = qbc_d<0>(bc), b5 = qbc_d<1>(bc);
