@@ -311,7 +311,9 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
  * KSIM_PATH_MEMO (k_memo, memoised FGD keys), KSIM_PATH_MIXED (a memoised kernel for the FGD replicas,
  * k_replay for the others), KSIM_PATH_STEP (k_step per pod, hipGraph), KSIM_PATH_SHARDED (node-sharded),
  * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica), KSIM_PATH_RANDOM_GO
- * (k_random_go: every replica Random on Go's stream, ksim_engine_set_go_stream). */
+ * (k_random_go: every replica Random on Go's stream, ksim_engine_set_go_stream), KSIM_PATH_SCAN1
+ * (k_scan1: every replica a cheap policy on one 256-thread workgroup, every node scanned per pod;
+ * a mix of k_scan1 and k_replay groups reports KSIM_PATH_REPLAY). */
 #define KSIM_PATH_REPLAY  0
 #define KSIM_PATH_MEMO    1
 #define KSIM_PATH_MIXED   2
@@ -319,6 +321,7 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 #define KSIM_PATH_SHARDED 4
 #define KSIM_PATH_HMEMO   5
 #define KSIM_PATH_RANDOM_GO 6
+#define KSIM_PATH_SCAN1   7
 int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus

@@ -688,6 +688,7 @@ struct GranV {
 // the lean instantiation (none of them: the bench, the paper sweeps, C5) compiles them out of the
 // step loop, as k_memo's does.
 #include "ksim_random_go.hpp"
+#include "ksim_scan1.hpp"
 
 template <int kPol, int kSub, bool kGeneral>
 __global__ __launch_bounds__(ksim_replay::kRBlock, (kSub == 0 && kPol >= POL_BESTFIT && kPol <= POL_RANDOM &&
@@ -1578,6 +1579,8 @@ struct ksim_engine {
   size_t h_cap[14] = {};
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
+  int last_scan1 = 0;  // replicas the last run replayed on k_scan1
+  bool scan1 = true;   // single-workgroup cheap-policy groups on k_scan1 (KSIM_SCAN1=0: k_replay)
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
   bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
@@ -1662,6 +1665,20 @@ static int launch_persistent(const void* f, int grid, int block, size_t lds, hip
   KSIM_HIP(r);
   return KSIM_OK;
 }
+
+// k_scan1 for the policies it serves, else null
+template <bool R>
+static const void* scan1_fn(int pol) {
+  switch (pol) {
+    case POL_BESTFIT: return (const void*)ksim_scan1::k_scan1<POL_BESTFIT, R>;
+    case POL_DOTPROD: return (const void*)ksim_scan1::k_scan1<POL_DOTPROD, R>;
+    case POL_PACKING: return (const void*)ksim_scan1::k_scan1<POL_PACKING, R>;
+    case POL_CLUSTERING: return (const void*)ksim_scan1::k_scan1<POL_CLUSTERING, R>;
+    case POL_RANDOM: return (const void*)ksim_scan1::k_scan1<POL_RANDOM, R>;
+    default: return nullptr;
+  }
+}
+static const void* scan1_fn(int pol, bool report) { return report ? scan1_fn<true>(pol) : scan1_fn<false>(pol); }
 
 template <int P, bool G>
 static const void* replay_fn(int K) {
@@ -2362,6 +2379,8 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     // the profiler passes of scripts/profile_config.sh use it -- rocprofv3 7.2 faults at process exit
     // after a cooperative launch
     if (const char* c = std::getenv("KSIM_COOP")) e->coop = std::atoi(c) != 0;
+    // KSIM_SCAN1=0: single-workgroup cheap-policy groups on k_replay instead of k_scan1 (A/B)
+    if (const char* c = std::getenv("KSIM_SCAN1")) e->scan1 = std::atoi(c) != 0;
   }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
@@ -3167,6 +3186,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   e->last_memo = 0;
   e->last_hmemo = 0;
   e->last_rgo = 0;
+  e->last_scan1 = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
   // co-residency needed) run concurrently on side streams: a paper-sweep group fills 170 of 256 CUs,
   // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
@@ -3252,6 +3272,21 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
     const bool general = profile || e->report || any_delete;
+    // one workgroup per replica, create-only, a cheap policy: the 256-thread k_scan1 (ksim_scan1.hpp)
+    if (K == 1 && !profile && !any_delete && e->scan1 && e->N <= kMaxSlice && scan1_fn(gp.first, e->report) &&
+        ksim_scan1::scan1_lds(e->N, gp.first, e->report) <= 160 * 1024) {
+      const void* f = scan1_fn(gp.first, e->report);
+      const size_t lds = ksim_scan1::scan1_lds(e->N, gp.first, e->report);
+      ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N};
+      KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      void* params[] = {(void*)&sa};
+      KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
+      e->last_K = 1;
+      e->last_groups = (int)groups.size();
+      e->last_scan1 += Rg;
+      first += Rg;
+      continue;
+    }
     while (replay_lds(S, gp.first, general) > 160 * 1024 && K < ksim_replay::kMaxK && Rg * (K + 1) <= e->cus) {
       ++K;
       S = (e->N + K - 1) / K;
@@ -3540,6 +3575,7 @@ int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   if (e->shard_world > 0) *path = KSIM_PATH_SHARDED;
   else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
   else if (e->last_rgo == e->R) *path = KSIM_PATH_RANDOM_GO;
+  else if (e->last_scan1 == e->R) *path = KSIM_PATH_SCAN1;
   else if (e->last_memo == 0 && e->last_hmemo == 0) *path = KSIM_PATH_REPLAY;
   else if (e->last_memo == e->R) *path = KSIM_PATH_MEMO;
   else if (e->last_hmemo == e->R) *path = KSIM_PATH_HMEMO;

@@ -1,0 +1,164 @@
+// ksim_scan1.hpp -- single-workgroup replay of a cheap-policy replica (k_scan1<policy>).
+//
+// The paper sweep (C4) runs 170 replicas per policy, one workgroup each (K = 1), beside the FGD
+// group; the whole sweep is bound by how many replicas the CUs hold at once, not by one chain.
+// k_replay's K = 1 workgroup is 1024 threads (16 waves) with a pipelined exchange it does not need
+// at K = 1.  k_scan1 is the K = 1 form for BestFit, DotProduct, GpuPacking, GpuClustering and the
+// hash-contract Random: 256 threads (4 waves), so a CU holds as many replicas as its LDS allows,
+// and ONE workgroup barrier per pod step:
+//   - thread t scans the node slots t, t + 256, ... (Filter, the policy's Score, the packed key
+//     max-score / smallest-name, the feasible count, Score errors, BestFit's raw min / max) into
+//     registers, each wave reduces them (DPP) into its slot of a double-buffered partial table;
+//   - barrier;
+//   - every wave reads the four partials and takes the same cycle decision (selectHost over the
+//     packed keys, the single-feasible shortcut, the Score-error abort: k_replay's commit);
+//   - the wave whose threads scan the winner's slot runs Reserve's GPU selector and the Bind on it
+//     and reports; slot s is only ever read by thread s % 256, so the Bind needs no second barrier.
+// Create-only streams without a profile (the host takes k_replay for anything else); with the
+// per-event cluster report (kReport) the Bind also records the node's new record and the previous
+// event that changed it (snap / prev, ksim_report.hpp), as k_replay's general form does.  Same
+// device functions as k_replay / k_step / the oracle, so the same bits.
+#pragma once
+
+namespace ksim_scan1 {
+
+using namespace ksim;
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr int kEvBuf = 128;
+
+struct Scan1Args {
+  ReplicaDev* reps;
+  const int* rep_list;  // replica of each workgroup
+  int N;
+};
+
+struct __align__(16) Scan1Part {
+  unsigned long long key;  // the wave's best packed key (0: nothing feasible)
+  int cnt;                 // feasible nodes
+  int err;                 // a feasible node's Score failed
+  int lo, hi;              // raw score min / max over the feasible nodes (BestFit's NormalizeScore)
+  int pad[2];
+};
+
+struct __align__(16) Scan1Shared {
+  PodDev ev[kEvBuf];
+  Scan1Part part[2][kWaves];  // by step parity: a wave may write step s+1's while another reads step s's
+};
+static_assert(sizeof(Scan1Shared) % 16 == 0, "keep the node records 16-B aligned");
+
+// Dynamic LDS: Scan1Shared | NodeRec nodes[N] | u16 tags[N][16] (GpuClustering) | i32 last[N] (report)
+__host__ __device__ inline size_t scan1_lds(int N, int pol, bool report) {
+  return sizeof(Scan1Shared) + (size_t)N * sizeof(NodeRec) +
+         (pol == POL_CLUSTERING ? (size_t)N * kTagStride * sizeof(uint16_t) : 0) + (report ? (size_t)N * 4 : 0);
+}
+
+template <int kPol, bool kReport>
+__global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
+  using namespace ksim_replay;
+  constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
+  constexpr bool kMinMax = kPol == POL_BESTFIT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Scan1Shared& sh = *reinterpret_cast<Scan1Shared*>(smem);
+  NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(Scan1Shared));
+  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(Scan1Shared) + (size_t)a.N * sizeof(NodeRec));
+  int* s_last = reinterpret_cast<int*>(smem + scan1_lds(a.N, kPol, false));  // report: last event per slot
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
+  const int N = a.N;
+  for (int i = tid; i < N; i += kBlock) store_node(&s_nodes[i], load_node(rp.nodes + i));
+  if (kTags)
+    for (int i = tid; i < N * kTagStride; i += kBlock) s_tags[i] = rp.tags[i];
+  if (kReport)
+    for (int i = tid; i < N; i += kBlock) s_last[i] = -1;
+
+  for (int step = 0; step < rp.n_events; ++step) {
+    const int eb = step & (kEvBuf - 1);
+    if (eb == 0) {
+      // every thread has passed the previous step's barrier, so nobody reads the old window
+      const int nl = min(kEvBuf, rp.n_events - step) * 2;
+      const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+      for (int i = tid; i < nl; i += kBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
+      __syncthreads();
+    }
+    const PodDev p = uniform_pod(&sh.ev[eb]);
+    // ---- scan: Filter + Score of this thread's slots
+    unsigned long long best = 0ull;
+    int cnt = 0, lo = 0x7fffffff, hi = -1;
+    bool err = false;
+    for (int i = tid; i < N; i += kBlock) {
+      const NodeV n = load_node(&s_nodes[i]);
+      if (filter_node(n, p)) {
+        bool e1 = false;
+        const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[i] : 0;
+        const int raw = cheap_score<kPol>(n, p, rp.seed, kTags ? &s_tags[(size_t)i * kTagStride] : nullptr, step, &e1,
+                                          rp.dpcfg, cap);
+        const unsigned long long k = pack_key((unsigned)raw, n.name_rank, -1, i);
+        best = k > best ? k : best;
+        ++cnt;
+        err = err || e1;
+        if (kMinMax) { lo = min(lo, raw); hi = max(hi, raw); }
+      }
+    }
+    best = wave_max_u64_dpp(best);
+    cnt = wave_sum_dpp(cnt);
+    const bool werr = __any(err);
+    if (kMinMax) { lo = wave_min_dpp(lo); hi = wave_max_dpp(hi); }
+    Scan1Part* pt = sh.part[step & 1];
+    if (lane == 0) pt[wv] = Scan1Part{best, cnt, werr ? 1 : 0, lo, hi, {0, 0}};
+    __syncthreads();
+    // ---- the cycle decision, by every wave (the same values): k_replay's commit at K = 1
+    unsigned long long W = 0ull;
+    int nfeas = 0, gerr = 0, glo = 0x7fffffff, ghi = -1;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) {
+      const Scan1Part q = pt[k];
+      W = q.key > W ? q.key : W;
+      nfeas += q.cnt;
+      gerr |= q.err;
+      if (kMinMax) { glo = min(glo, q.lo); ghi = max(ghi, q.hi); }
+    }
+    const int loc = key_loc(W);
+    const int owner = W != 0ull ? (loc % kBlock) / 64 : 0;  // the wave that scans the winner's slot
+    if (wv == owner) {
+      ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
+      if (nfeas > 0) {
+        out.status = (nfeas > 1 && gerr) ? ST_ERROR : ST_OK;  // a Score error aborts the cycle
+        if (out.status == ST_OK) {
+          out.score = result_score(rp, nfeas, key_score(W), glo, ghi);
+          NodeV bn = uniform_node(&s_nodes[loc]);
+          const int mask = select_gpus(bn, p, rp.gpusel, sel_arg<kPol == POL_DOTPROD>(rp, bn, p, loc, key_gpu(W)),
+                                       rp.seed, step);
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+            out.score = 0;
+          } else {
+            bind_node(bn, p, mask, +1);
+            if (lane == 0) {
+              store_node(&s_nodes[loc], bn);
+              if (kReport) {  // cluster report: the state this event left, the previous change of the node
+                store_node(rp.snap + step, bn);
+                rp.prev[step] = s_last[loc];
+                s_last[loc] = step;
+              }
+              if (p.tag >= 0) {
+                uint16_t* t = kTags ? &s_tags[(size_t)loc * kTagStride] : rp.tags + (size_t)loc * kTagStride;
+                t[p.tag] = (uint16_t)(t[p.tag] + 1);
+              }
+            }
+            out.node = loc;
+            out.gpu_mask = mask;
+          }
+        }
+      }
+      if (lane == 0) rp.res[step] = out;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < N; i += kBlock) store_node(rp.nodes + i, load_node(&s_nodes[i]));
+  if (kTags)
+    for (int i = tid; i < N * kTagStride; i += kBlock) rp.tags[i] = s_tags[i];
+}
+
+}  // namespace ksim_scan1

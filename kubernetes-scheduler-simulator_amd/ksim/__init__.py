@@ -529,7 +529,7 @@ class Engine:
         used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
-        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go"][k.value]
+        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)

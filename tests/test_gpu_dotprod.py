@@ -26,7 +26,7 @@ DIMS = ["merge", "share", "divide", "extend"]
 NORMS = ["max", "node", "pod"]
 ODIM = {"merge": O.DIM_MERGE, "share": O.DIM_SHARE, "divide": O.DIM_DIVIDE, "extend": O.DIM_EXTEND}
 ONORM = {"max": O.NORM_MAX, "node": O.NORM_NODE, "pod": O.NORM_POD}
-PATHS = {"k_replay": dict(), "k_replay-K1": dict(wgs_per_replica=1), "k_step": dict(run_mode=1)}
+PATHS = {"k_replay": dict(), "k_scan1-K1": dict(wgs_per_replica=1), "k_step": dict(run_mode=1)}
 
 
 @pytest.fixture(scope="module")

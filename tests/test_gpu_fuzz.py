@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 # (seed, nodes, creations, delete probability)
 CASES = [(1, 40, 500, 0.0), (2, 97, 900, 0.25), (3, 250, 1200, 0.1), (4, 7, 300, 0.4), (5, 1, 60, 0.3),
          (6, 600, 2000, 0.0)]
-PATHS = [(0, "auto"), (2, "replay"), (1, "step"), (5, "hmemo")]
+PATHS = [(0, "auto"), (2, "replay"), (1, "step"), (5, "hmemo"), (2, "replay-K1")]  # K1: k_scan1 when lean
 
 
 def run_engine(case, policy, run_mode, seed=5, wgs=0):
@@ -51,7 +51,7 @@ def test_fuzz_all_paths_vs_oracle(case, name, pol, sel):
     want, want_state, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=pol, gpu_sel=sel,
                                        seed=5, threads=16)
     for mode, label in PATHS:
-        got, state = run_engine(case, name, mode)
+        got, state = run_engine(case, name, mode, wgs=1 if label == "replay-K1" else 0)
         bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
         assert len(got) == len(want) and not bad, \
             "%s/%s: first mismatch at event %d: gpu %s oracle %s" % (name, label, bad[0], got[bad[0]], want[bad[0]])

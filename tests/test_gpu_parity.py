@@ -348,3 +348,24 @@ def test_full_openb_baselines(default_trace, name, pol, sel):
     res, state = engine_run(default_trace, rp, None, rp.n, name, seed=3)
     want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, pol, sel, seed=3)
     assert_same(res, want, state, want_state, None)
+
+
+@pytest.mark.parametrize("name,pol,sel", POLICIES[1:], ids=[p[0] for p in POLICIES[1:]])
+def test_full_openb_baselines_single_workgroup(default_trace, name, pol, sel):
+    # one workgroup per replica, create-only stream, no report: the 256-thread k_scan1 (the paper
+    # sweep's cheap-policy groups); bit-exact per event and in the final state
+    rp = default_trace.replay(seed=44)
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(default_trace.num_nodes, 1, wgs_per_replica=1)
+    try:
+        eng.set_nodes(0, rp.nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, name, seed=2)
+        eng.load_events(0, rp.events, rp.n)
+        eng.run()
+        res, state = eng.results(0), eng.nodes(0)
+        assert eng.last_run_path() == "k_scan1"
+    finally:
+        eng.close()
+    want, want_state, _ = oracle_run(default_trace, rp, None, rp.n, pol, sel, seed=2)
+    assert_same(res, want, state, want_state, None)
