@@ -1580,7 +1580,8 @@ struct ksim_engine {
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
-  bool scan1 = true;   // single-workgroup cheap-policy groups on k_scan1 (KSIM_SCAN1=0: k_replay)
+  int scan1 = 2;       // single-workgroup cheap-policy groups on k_scan1, node records in VGPRs where they fit
+                       // (KSIM_SCAN1=1: records in LDS; 0: k_replay)
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
   bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
   std::vector<int> nt;
@@ -1666,19 +1667,22 @@ static int launch_persistent(const void* f, int grid, int block, size_t lds, hip
   return KSIM_OK;
 }
 
-// k_scan1 for the policies it serves, else null
-template <bool R>
+// k_scan1 for the policies it serves, else null (reg: the node records in VGPRs)
+template <bool R, bool G>
 static const void* scan1_fn(int pol) {
   switch (pol) {
-    case POL_BESTFIT: return (const void*)ksim_scan1::k_scan1<POL_BESTFIT, R>;
-    case POL_DOTPROD: return (const void*)ksim_scan1::k_scan1<POL_DOTPROD, R>;
-    case POL_PACKING: return (const void*)ksim_scan1::k_scan1<POL_PACKING, R>;
-    case POL_CLUSTERING: return (const void*)ksim_scan1::k_scan1<POL_CLUSTERING, R>;
-    case POL_RANDOM: return (const void*)ksim_scan1::k_scan1<POL_RANDOM, R>;
+    case POL_BESTFIT: return (const void*)ksim_scan1::k_scan1<POL_BESTFIT, R, G>;
+    case POL_DOTPROD: return (const void*)ksim_scan1::k_scan1<POL_DOTPROD, R, G>;
+    case POL_PACKING: return (const void*)ksim_scan1::k_scan1<POL_PACKING, R, G>;
+    case POL_CLUSTERING: return (const void*)ksim_scan1::k_scan1<POL_CLUSTERING, R, G>;
+    case POL_RANDOM: return (const void*)ksim_scan1::k_scan1<POL_RANDOM, R, G>;
     default: return nullptr;
   }
 }
-static const void* scan1_fn(int pol, bool report) { return report ? scan1_fn<true>(pol) : scan1_fn<false>(pol); }
+static const void* scan1_fn(int pol, bool report, bool reg) {
+  return report ? (reg ? scan1_fn<true, true>(pol) : scan1_fn<true, false>(pol))
+                : (reg ? scan1_fn<false, true>(pol) : scan1_fn<false, false>(pol));
+}
 
 template <int P, bool G>
 static const void* replay_fn(int K) {
@@ -2379,8 +2383,9 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     // the profiler passes of scripts/profile_config.sh use it -- rocprofv3 7.2 faults at process exit
     // after a cooperative launch
     if (const char* c = std::getenv("KSIM_COOP")) e->coop = std::atoi(c) != 0;
-    // KSIM_SCAN1=0: single-workgroup cheap-policy groups on k_replay instead of k_scan1 (A/B)
-    if (const char* c = std::getenv("KSIM_SCAN1")) e->scan1 = std::atoi(c) != 0;
+    // KSIM_SCAN1: single-workgroup cheap-policy groups on k_scan1 with the records in VGPRs (2, default),
+    // in LDS (1), or on k_replay (0) -- A/B switches
+    if (const char* c = std::getenv("KSIM_SCAN1")) e->scan1 = std::atoi(c);
   }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
@@ -3273,10 +3278,11 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     int S = (e->N + K - 1) / K;
     const bool general = profile || e->report || any_delete;
     // one workgroup per replica, create-only, a cheap policy: the 256-thread k_scan1 (ksim_scan1.hpp)
-    if (K == 1 && !profile && !any_delete && e->scan1 && e->N <= kMaxSlice && scan1_fn(gp.first, e->report) &&
-        ksim_scan1::scan1_lds(e->N, gp.first, e->report) <= 160 * 1024) {
-      const void* f = scan1_fn(gp.first, e->report);
-      const size_t lds = ksim_scan1::scan1_lds(e->N, gp.first, e->report);
+    const bool reg = e->scan1 == 2 && e->N <= ksim_scan1::kBlock * ksim_scan1::kRegSlots;
+    if (K == 1 && !profile && !any_delete && e->scan1 && e->N <= kMaxSlice && scan1_fn(gp.first, e->report, reg) &&
+        ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg) <= 160 * 1024) {
+      const void* f = scan1_fn(gp.first, e->report, reg);
+      const size_t lds = ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg);
       ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N};
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       void* params[] = {(void*)&sa};

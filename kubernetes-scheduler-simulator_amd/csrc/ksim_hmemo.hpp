@@ -172,14 +172,15 @@ __device__ __forceinline__ NodeSum node_sum(const NodeV& n) {
   s.free_cnt = fr;
   return s;
 }
+// Branch-free except for the partial-milli multi-GPU request (the class pass runs it for every class
+// of the replica, one class per thread, so a divergent early-return chain would serialise the wave).
 __device__ __forceinline__ bool filter_sum(const NodeSum& s, const NodeV& n, const PodDev& p) {
-  if (s.pods_left < 1) return false;
-  if (!(p.cpu_req == 0 && p.mem == 0) && (s.cpu_left < p.cpu_req || s.mem_left < p.mem)) return false;
-  if (p.milli <= 0) return true;
-  if (s.cnt == 0 || (p.tmask & (unsigned)s.type_bit) == 0u || p.num <= 0) return false;
-  if (p.num == 1) return s.max_left >= p.milli;
-  if (p.milli == kMilli) return s.free_cnt >= p.num;
-  return filter_node(n, p);
+  const bool res_ok = (p.cpu_req == 0 && p.mem == 0) || (s.cpu_left >= p.cpu_req && s.mem_left >= p.mem);
+  const bool dev_ok = s.cnt != 0 && (p.tmask & (unsigned)s.type_bit) != 0u && p.num > 0;
+  const bool fits = p.num == 1 ? s.max_left >= p.milli : s.free_cnt >= p.num;  // whole GPUs when num > 1
+  bool ok = s.pods_left >= 1 && res_ok && (p.milli <= 0 || (dev_ok && fits));
+  if (p.milli > 0 && p.num > 1 && p.milli != kMilli) ok = filter_node(n, p);  // partial multi-GPU: no trace has one
+  return ok;
 }
 
 // Row (16-lane) max of unsigned values below 2^31: every lane of the row ends with it.

@@ -27,6 +27,7 @@ using namespace ksim;
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 constexpr int kEvBuf = 128;
+constexpr int kRegSlots = 5;  // kReg: node slots per thread held in VGPRs (N <= 1280, the openb clusters)
 
 struct Scan1Args {
   ReplicaDev* reps;
@@ -48,13 +49,26 @@ struct __align__(16) Scan1Shared {
 };
 static_assert(sizeof(Scan1Shared) % 16 == 0, "keep the node records 16-B aligned");
 
-// Dynamic LDS: Scan1Shared | NodeRec nodes[N] | u16 tags[N][16] (GpuClustering) | i32 last[N] (report)
-__host__ __device__ inline size_t scan1_lds(int N, int pol, bool report) {
-  return sizeof(Scan1Shared) + (size_t)N * sizeof(NodeRec) +
+// Dynamic LDS: Scan1Shared | NodeRec nodes[N] (not with kReg) | u16 tags[N][16] (GpuClustering) |
+// i32 last[N] (report)
+__host__ __device__ inline size_t scan1_lds(int N, int pol, bool report, bool reg = false) {
+  return sizeof(Scan1Shared) + (reg ? 0 : (size_t)N * sizeof(NodeRec)) +
          (pol == POL_CLUSTERING ? (size_t)N * kTagStride * sizeof(uint16_t) : 0) + (report ? (size_t)N * 4 : 0);
 }
 
-template <int kPol, bool kReport>
+// x = c ? y : x field by field (a select of whole structs would take the array's address)
+__device__ __forceinline__ void sel_node(NodeV& x, const NodeV& y, bool c) {
+  x.cpu_left = c ? y.cpu_left : x.cpu_left;
+  x.mem_left = c ? y.mem_left : x.mem_left;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x.g[i] = c ? y.g[i] : x.g[i];
+  x.meta = c ? y.meta : x.meta;
+  x.name_rank = c ? y.name_rank : x.name_rank;
+}
+
+// kReg: thread t keeps the records of its slots t + 256 k (k < kRegSlots) in VGPRs instead of LDS, so
+// a workgroup needs only a few KB of LDS and a CU holds as many replicas as its registers allow.
+template <int kPol, bool kReport, bool kReg>
 __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
   using namespace ksim_replay;
   constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
@@ -62,12 +76,21 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Scan1Shared& sh = *reinterpret_cast<Scan1Shared*>(smem);
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(Scan1Shared));
-  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(Scan1Shared) + (size_t)a.N * sizeof(NodeRec));
-  int* s_last = reinterpret_cast<int*>(smem + scan1_lds(a.N, kPol, false));  // report: last event per slot
+  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(Scan1Shared) + (kReg ? 0 : (size_t)a.N * sizeof(NodeRec)));
+  int* s_last = reinterpret_cast<int*>(smem + scan1_lds(a.N, kPol, false, kReg));  // report: last event per slot
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
   const int N = a.N;
-  for (int i = tid; i < N; i += kBlock) store_node(&s_nodes[i], load_node(rp.nodes + i));
+  NodeV rn[kReg ? kRegSlots : 1];  // kReg: the records of slots tid + 256 k
+  if (kReg) {
+#pragma unroll
+    for (int k = 0; k < kRegSlots; ++k) {
+      rn[k] = NodeV{};
+      if (tid + kBlock * k < N) rn[k] = load_node(rp.nodes + tid + kBlock * k);
+    }
+  } else {
+    for (int i = tid; i < N; i += kBlock) store_node(&s_nodes[i], load_node(rp.nodes + i));
+  }
   if (kTags)
     for (int i = tid; i < N * kTagStride; i += kBlock) s_tags[i] = rp.tags[i];
   if (kReport)
@@ -87,8 +110,7 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     unsigned long long best = 0ull;
     int cnt = 0, lo = 0x7fffffff, hi = -1;
     bool err = false;
-    for (int i = tid; i < N; i += kBlock) {
-      const NodeV n = load_node(&s_nodes[i]);
+    auto visit = [&](const NodeV& n, int i) {
       if (filter_node(n, p)) {
         bool e1 = false;
         const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[i] : 0;
@@ -100,6 +122,13 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
         err = err || e1;
         if (kMinMax) { lo = min(lo, raw); hi = max(hi, raw); }
       }
+    };
+    if (kReg) {
+#pragma unroll
+      for (int k = 0; k < kRegSlots; ++k)
+        if (tid + kBlock * k < N) visit(rn[k], tid + kBlock * k);
+    } else {
+      for (int i = tid; i < N; i += kBlock) visit(load_node(&s_nodes[i]), i);
     }
     best = wave_max_u64_dpp(best);
     cnt = wave_sum_dpp(cnt);
@@ -127,7 +156,21 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
         out.status = (nfeas > 1 && gerr) ? ST_ERROR : ST_OK;  // a Score error aborts the cycle
         if (out.status == ST_OK) {
           out.score = result_score(rp, nfeas, key_score(W), glo, ghi);
-          NodeV bn = uniform_node(&s_nodes[loc]);
+          NodeV bn;
+          if (kReg) {  // the record from the register slot loc / 256 of lane loc % 64
+            const int ks = loc / kBlock, src = loc & 63;
+            NodeV x = rn[0];
+#pragma unroll
+            for (int k = 1; k < kRegSlots; ++k) sel_node(x, rn[k], ks == k);  // field-wise: rn stays in VGPRs
+            bn.cpu_left = __builtin_amdgcn_readlane(x.cpu_left, src);
+            bn.mem_left = __builtin_amdgcn_readlane(x.mem_left, src);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bn.g[i] = (uint32_t)__builtin_amdgcn_readlane((int)x.g[i], src);
+            bn.meta = (uint32_t)__builtin_amdgcn_readlane((int)x.meta, src);
+            bn.name_rank = (uint32_t)__builtin_amdgcn_readlane((int)x.name_rank, src);
+          } else {
+            bn = uniform_node(&s_nodes[loc]);
+          }
           const int mask = select_gpus(bn, p, rp.gpusel, sel_arg<kPol == POL_DOTPROD>(rp, bn, p, loc, key_gpu(W)),
                                        rp.seed, step);
           if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
@@ -135,8 +178,15 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
             out.score = 0;
           } else {
             bind_node(bn, p, mask, +1);
+            if (kReg) {
+              if (tid == loc % kBlock) {
+#pragma unroll
+                for (int k = 0; k < kRegSlots; ++k)
+                  if (loc / kBlock == k) rn[k] = bn;
+              }
+            }
             if (lane == 0) {
-              store_node(&s_nodes[loc], bn);
+              if (!kReg) store_node(&s_nodes[loc], bn);
               if (kReport) {  // cluster report: the state this event left, the previous change of the node
                 store_node(rp.snap + step, bn);
                 rp.prev[step] = s_last[loc];
@@ -156,7 +206,13 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     }
   }
   __syncthreads();
-  for (int i = tid; i < N; i += kBlock) store_node(rp.nodes + i, load_node(&s_nodes[i]));
+  if (kReg) {
+#pragma unroll
+    for (int k = 0; k < kRegSlots; ++k)
+      if (tid + kBlock * k < N) store_node(rp.nodes + tid + kBlock * k, rn[k]);
+  } else {
+    for (int i = tid; i < N; i += kBlock) store_node(rp.nodes + i, load_node(&s_nodes[i]));
+  }
   if (kTags)
     for (int i = tid; i < N * kTagStride; i += kBlock) rp.tags[i] = s_tags[i];
 }

@@ -350,10 +350,13 @@ def test_full_openb_baselines(default_trace, name, pol, sel):
     assert_same(res, want, state, want_state, None)
 
 
+@pytest.mark.parametrize("scan1", ["1", "2"], ids=["lds", "vgpr"])
 @pytest.mark.parametrize("name,pol,sel", POLICIES[1:], ids=[p[0] for p in POLICIES[1:]])
-def test_full_openb_baselines_single_workgroup(default_trace, name, pol, sel):
+def test_full_openb_baselines_single_workgroup(default_trace, name, pol, sel, scan1, monkeypatch):
     # one workgroup per replica, create-only stream, no report: the 256-thread k_scan1 (the paper
-    # sweep's cheap-policy groups); bit-exact per event and in the final state
+    # sweep's cheap-policy groups), node records in LDS or (KSIM_SCAN1=2) in VGPRs; bit-exact per
+    # event and in the final state
+    monkeypatch.setenv("KSIM_SCAN1", scan1)
     rp = default_trace.replay(seed=44)
     arr, n = default_trace.typical()
     eng = ksim.Engine(default_trace.num_nodes, 1, wgs_per_replica=1)

@@ -68,9 +68,13 @@ def test_default_trace_rows_identical_to_expected_results(default_sweep):
         assert not bad, (kind, sorted(bad.items())[:5])
 
 
-def test_full_paper_sweep_vs_expected_results():
+@pytest.mark.parametrize("scan1", ["1", "2"], ids=["scan1-lds", "scan1-vgpr"])
+def test_full_paper_sweep_vs_expected_results(scan1, monkeypatch):
     # C4: all 1020 experiments (17 traces x 6 policies x 10 seeds) as replicas of one engine;
     # every (trace, policy) 10-seed mean curve near the reference's, at every arrived-GPU %.
+    # The cheap-policy groups run on k_scan1 (one workgroup per replica), node records in LDS or
+    # (KSIM_SCAN1=2) in VGPRs.
+    monkeypatch.setenv("KSIM_SCAN1", scan1)
     sw = SW.Sweep(SW.plan())
     dev_ms, wall = sw.run()
     curves = sw.curves()
