@@ -2277,7 +2277,9 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     KSIM_HIP(hipMemsetAsync(e->d_h_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * kHProf, st));
     ma.prof = e->d_h_prof;
   }
-  const void* f = pl.K <= 64 ? (const void*)k_hmemo<1> : (const void*)k_hmemo<4>;
+  const void* f = pl.K == 1 ? (profile ? (const void*)k_hmemo<0, true> : (const void*)k_hmemo<0, false>)
+                  : pl.K <= 64 ? (profile ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
+                               : (profile ? (const void*)k_hmemo<4, true> : (const void*)k_hmemo<4, false>);
   if (pl.K > 1 && Rg * pl.K > resident_cap(e, f, pl.lds)) {
     std::fprintf(stderr, "ksim: k_hmemo needs %d co-resident workgroups\n", Rg * pl.K);
     return KSIM_ERANGE;

@@ -205,8 +205,10 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
   return (unsigned)row_max16((int)m);
 }
 
-// kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1).
-template <int kSub>
+// kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1); kSub = 0: the lean one-
+// workgroup form (K = 1, the exchange compiled out).  kProf: the KSIM_PROFILE phase timers (compiled
+// out of the lean launches, as k_memo's: the step loop's scalar registers are what it runs short of).
+template <int kSub, bool kProf>
 __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
   using ksim_memo::gget;
@@ -214,7 +216,8 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   using ksim_memo::gput_node;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HShared& sh = *reinterpret_cast<HShared*>(smem);
-  const int K = a.K;
+  constexpr int kS = kSub > 0 ? kSub : 1;
+  const int K = kSub == 0 ? 1 : a.K;
   const int gi = (int)blockIdx.x / K, w = (int)blockIdx.x % K;
   const int r = a.rep_list[gi];
   const ReplicaDev rp = a.reps[r];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
   if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; sh.stop = 0; }
-  const bool prof = a.prof != nullptr;
+  const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
   unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -474,10 +477,10 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
             ksim_replay::gstore(slot + (size_t)w * 2 + 0, tag | W);
             ksim_replay::gstore(slot + (size_t)w * 2 + 1, tag | (unsigned)nfeas);
           }
-          unsigned long long x0[kSub], x1[kSub];
+          unsigned long long x0[kS], x1[kS];
           auto load = [&]() {
 #pragma unroll
-            for (int j = 0; j < kSub; ++j) {
+            for (int j = 0; j < kS; ++j) {
               const int k = lane + 64 * j;
               if (k < K) {
                 x0[j] = ksim_replay::gload(slot + (size_t)k * 2 + 0);
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           auto ready = [&]() {
             bool ok = true;
 #pragma unroll
-            for (int j = 0; j < kSub; ++j)
+            for (int j = 0; j < kS; ++j)
               ok = ok && (lane + 64 * j >= K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
             return ok;
           };
@@ -505,7 +508,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           unsigned m = 0u;
           int c = 0;
 #pragma unroll
-          for (int j = 0; j < kSub; ++j) {
+          for (int j = 0; j < kS; ++j) {
             if (lane + 64 * j < K) {
               const unsigned kj = (unsigned)(x0[j] & 0xffffffffull);
               m = kj > m ? kj : m;
