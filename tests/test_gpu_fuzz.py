@@ -191,3 +191,26 @@ def test_fuzz_pwr(policy, seed, n, e, pdel):
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert len(got) == len(want) and not bad, "first mismatch at %d: %s vs %s" % (bad[0], got[bad[0]], want[bad[0]])
     check_state(state, want_state)
+
+
+@pytest.mark.parametrize("name,pol,sel", POLICIES[1:], ids=[p[0] for p in POLICIES[1:]])
+def test_fuzz_scan1_records_in_lds(name, pol, sel):
+    # one workgroup per replica on a cluster past the VGPR form's 1280 nodes: k_scan1 with the node
+    # records in LDS (the record placement k_scan1 picks above 1280 nodes)
+    case = make_case(11, 2000, 1500)
+    want, want_state, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=pol, gpu_sel=sel,
+                                       seed=5, threads=16)
+    eng = ksim.Engine(2000, 1, wgs_per_replica=1)
+    try:
+        eng.set_nodes(0, case["nodes"])
+        eng.set_typical(0, case["typical"], case["typical_n"])
+        eng.set_policy(0, name, seed=5)
+        eng.load_events(0, case["events"], case["n_events"])
+        eng.run()
+        got, state = eng.results(0), eng.nodes(0)
+        assert eng.last_run_path() == "k_scan1"
+    finally:
+        eng.close()
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert len(got) == len(want) and not bad, "first mismatch at event %d" % bad[0]
+    check_state(state, want_state)
