@@ -300,7 +300,8 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
     const int np = (min(64, nt - t0) + 1) >> 1;
     if (lane < kFoldRows) {
       const double2* rw = reinterpret_cast<const double2*>(buf + lane * kFoldStride);
-      for (int k0 = 0; k0 < np; k0 += 8) {
+      int k0 = 0;
+      for (; k0 + 8 <= np; k0 += 8) {
         double2 v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = rw[k0 + i];
@@ -309,6 +310,14 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
           acc += v[i].x;
           acc += v[i].y;
         }
+      }
+      // the chunk's last pairs two at a time (openb: 18 pairs -> 8 + 8 + 2, not 24 with 12 +0.0 adds)
+      for (; k0 < np; k0 += 2) {
+        const double2 v0 = rw[k0], v1 = rw[k0 + 1];
+        acc += v0.x;
+        acc += v0.y;
+        acc += v1.x;
+        acc += v1.y;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
