@@ -1,0 +1,13 @@
+#!/bin/bash
+# Final tree: whole GPU suite, smoke(), the default bench line and its kernel profile (k_memo changed).
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/suite
+timeout -k 10 900 python3 -u -m pytest -q --timeout 400 --timeout-method thread -m gpu -p no:cacheprovider tests > gpurun_out/suite/pytest_gpu.log 2>&1; rc=$?
+tail -3 gpurun_out/suite/pytest_gpu.log; grep -E "FAILED|ERROR" gpurun_out/suite/pytest_gpu.log | head
+[ $rc = 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/suite/smoke.log 2>&1 || exit 1
+tail -1 gpurun_out/suite/smoke.log
+bash scripts/profile_all.sh c2 || exit 1
+timeout -k 10 300 python3 bench.py > gpurun_out/suite/bench.json 2> gpurun_out/suite/bench.err || exit 1
+python3 -c "import json;d=json.load(open('gpurun_out/suite/bench.json'));print('c2', d['value'], d['ms_per_step'], d['roofline']['frac'])"
