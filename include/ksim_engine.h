@@ -185,6 +185,19 @@ typedef struct {
     int64_t arrived_cpu_milli;     /* Σ PodResource.MilliCpu of the creation events so far (:408) */
 } ksim_report;
 
+/* The power report the reference logs right after it (simulator.go:427, analysis.go:24-56
+ * ClusterPowerConsumptionReport -> "[Power]; cluster: ..; ClusterCPU: ..; ClusterGPU: .." line):
+ * Σ over nodes of GetEnergyConsumptionNode's CPU and GPU terms (resource.go:536-563) with the
+ * replica's ksim_power_model, as exact sums rounded once (every term of the reference's tables is a
+ * small integer in fp64, so its own Go-map-order sums are the same values). */
+typedef struct {
+    double  cluster_w;             /* cpu_w + gpu_w (analysis.go:54) */
+    double  cpu_w;
+    double  gpu_w;
+    int64_t invalid_nodes;         /* nodes whose GPU / CPU model has no energy model: the reference's
+                                      report calls a nil func there (its line would not be printed) */
+} ksim_power_report;
+
 typedef struct ksim_engine ksim_engine;
 
 /* Engine configuration (0 = default). */
@@ -268,6 +281,9 @@ int  ksim_engine_get_nodes(ksim_engine* e, int replica, ksim_node* out);
  * get_reports).  Disabled by default; enabling it adds two short kernels after the replay. */
 int  ksim_engine_set_report(ksim_engine* e, int enable);
 int  ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int n);
+/* The per-event power report of a replica with an energy model (ksim_engine_set_power_model, any
+ * policy); KSIM_ESTATE without one or while the report is disabled. */
+int  ksim_engine_get_power_reports(ksim_engine* e, int replica, ksim_power_report* out, int n);
 /* Device time of the report kernels of the last run (ms; part of last_run_ms). */
 int  ksim_engine_last_report_ms(ksim_engine* e, double* ms);
 

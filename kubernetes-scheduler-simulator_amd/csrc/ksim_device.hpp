@@ -144,15 +144,19 @@ struct ReplicaDev {
   const uint8_t* cpum;   // [N]
   int2* pws;             // [N]
   int32_t w_pwr, w_fgd;
+  int32_t has_pw;        // an energy model was given: the cluster report adds the [Power] terms
+  int32_t pad_pw;
 };
 
-// Per-event cluster report, exact (fixed point 2^-80 for the fp64 bins; see fix80).
-// cnt: used nodes, used GPUs, used GPU milli, used CPU milli, arrived GPU milli, arrived CPU milli.
+// Per-event cluster report, exact (fixed point 2^-80 for the fp64 terms; see fix80).
+// fx: the 7 frag bins, then the cluster's CPU and GPU power (ClusterPowerConsumptionReport, W).
+// cnt: used nodes, used GPUs, used GPU milli, used CPU milli, arrived GPU milli, arrived CPU milli,
+//      nodes without an energy model (the reference's power report would fail on them), pad.
 struct __align__(16) RepAcc {
-  __int128 bins[7];
-  long long cnt[6];
+  __int128 fx[9];
+  long long cnt[8];
 };
-static_assert(sizeof(RepAcc) == 160, "RepAcc layout");
+static_assert(sizeof(RepAcc) == 208, "RepAcc layout");
 
 // Per-replica cross-workgroup accumulators for one step (reset by the last block).
 struct __align__(64) Accum {
@@ -527,6 +531,35 @@ KSIM_HD bool node_energy(int cpuL, int cap, int cm, const int (&gl)[kMaxGpu], in
   const double num_idle_cpus = num_cpus - num_active;
   const double cpu = (pw.cidle[cm] * num_idle_cpus) + (pw.cfull[cm] * num_active);
   *energy = cpu + gpu;  // pwr_score.go:147 old_CPU_energy + old_GPU_energy
+  return true;
+}
+
+// GetEnergyConsumptionNode (resource.go:536-563) split into its CPU and GPU terms, for the per-event
+// [Power] report (analysis.go:24-56 ClusterPowerConsumptionReport sums each over the nodes).  Same
+// expressions as node_energy; false where the reference would fail (no energy model for the node's
+// GPU model: a nil func call; an unknown CPU model).
+KSIM_HD bool node_power(int cpuL, int cap, int cm, const int (&gl)[kMaxGpu], int cnt, int gtype, const PowerDev& pw,
+                        double* cpu_w, double* gpu_w) {
+  double gpu = 0;
+  if (!((pw.gnone >> gtype) & 1u)) {
+    if (!((pw.gvalid >> gtype) & 1u)) return false;
+    int free_gpus = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGpu; ++g) free_gpus += (g < cnt && gl[g] == kMilli) ? 1 : 0;
+    const double num_idle = (double)free_gpus;
+    const double num_working = (double)cnt - num_idle;
+    gpu = (pw.gidle[gtype] * num_idle) + (pw.gfull[gtype] * num_working);
+  }
+  if (!((pw.cvalid >> cm) & 1u)) return false;
+  const double real_cores = ceil((double)cap / (double)kMilli / 2);
+  const double idle_cores = floor((double)cpuL / (double)kMilli / 2);
+  const double working_cores = real_cores - idle_cores;
+  const double nc = pw.cnc[cm];
+  const double num_cpus = ceil(real_cores / nc);
+  const double num_active = ceil(working_cores / nc);
+  const double num_idle_cpus = num_cpus - num_active;
+  *cpu_w = (pw.cidle[cm] * num_idle_cpus) + (pw.cfull[cm] * num_active);
+  *gpu_w = gpu;
   return true;
 }
 

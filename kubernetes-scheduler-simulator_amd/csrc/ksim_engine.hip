@@ -2708,6 +2708,10 @@ int ksim_engine_set_power_model(ksim_engine* e, int replica, const ksim_power_mo
   KSIM_HIP(hipMemcpyAsync(e->d_pw + replica, pm, sizeof(PowerDev), hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipStreamSynchronize(e->stream));
   e->pw_set[replica] = 1;
+  e->reps[replica].has_pw = 1;
+  int rc = upload_reps(e);
+  if (rc) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
   return KSIM_OK;
 }
 
@@ -3554,7 +3558,7 @@ int ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int n
     ksim_report& o = out[i];
     // exact fixed-point sum -> nearest double (the int128 -> double conversion rounds to nearest
     // even; the 2^-80 scaling is exact)
-    for (int k = 0; k < 7; ++k) o.frag_bins[k] = std::ldexp((double)h[i].bins[k], -80);
+    for (int k = 0; k < 7; ++k) o.frag_bins[k] = std::ldexp((double)h[i].fx[k], -80);
     o.used_nodes = h[i].cnt[0];
     o.used_gpus = h[i].cnt[1];
     o.used_gpu_milli = h[i].cnt[2];
@@ -3562,6 +3566,24 @@ int ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int n
     o.arrived_gpu_milli = h[i].cnt[4];
     o.used_cpu_milli = h[i].cnt[3];
     o.arrived_cpu_milli = h[i].cnt[5];
+  }
+  return KSIM_OK;
+}
+
+int ksim_engine_get_power_reports(ksim_engine* e, int replica, ksim_power_report* out, int n) {
+  if (!e || !out || replica < 0 || replica >= e->R || n < 0 || n > e->n_events[replica]) return KSIM_EINVAL;
+  if (!e->report || !e->d_rep[replica] || !e->pw_set[replica]) return KSIM_ESTATE;
+  if (n == 0) return KSIM_OK;
+  std::vector<RepAcc> h((size_t)n);
+  KSIM_HIP(hipSetDevice(e->device));
+  KSIM_HIP(hipMemcpyAsync(h.data(), e->d_rep[replica], sizeof(RepAcc) * n, hipMemcpyDeviceToHost, e->stream));
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  for (int i = 0; i < n; ++i) {
+    ksim_power_report& o = out[i];
+    o.cpu_w = std::ldexp((double)h[i].fx[7], -80);
+    o.gpu_w = std::ldexp((double)h[i].fx[8], -80);
+    o.cluster_w = o.cpu_w + o.gpu_w;  // analysis.go:54 powerCPUCluster + powerGPUCluster
+    o.invalid_nodes = h[i].cnt[6];
   }
   return KSIM_OK;
 }

@@ -5,6 +5,9 @@
 //   bins[7]   Σ over nodes of NodeGpuShareFragAmount (frag.go:148-188), Go-map node order
 //   used nodes / GPUs / GPU milli / CPU milli   (analysis.go:88-95)
 //   arrived GPU / CPU milli                      (simulator.go:405-408)
+// and, when the replica has an energy model, the "[Power]" report that follows it
+// (simulator.go:427 -> analysis.go:24-56 ClusterPowerConsumptionReport): Σ over nodes of the CPU and
+// GPU terms of GetEnergyConsumptionNode (resource.go:536-563).
 // Those lines are the input of the fragmentation / allocation curves (scripts/analysis.py:202-264,
 // experiments/analysis/merge_*_discrete.py).
 //
@@ -25,11 +28,15 @@ using namespace ksim;
 
 constexpr int kDeltaBlock = 256;
 constexpr int kScanBlock = 1024;
-constexpr int kFields = 13;  // 7 bins + 6 counters
+// Fields: 0-6 frag bins, 7-8 CPU / GPU power (fix80), 9-12 used nodes / GPUs / GPU milli / CPU milli,
+// 13-14 arrived GPU / CPU milli, 15 nodes without an energy model.
+constexpr int kFx = 9;
+constexpr int kFields = 16;
 
-// One node's term of the report: the 7 exact bins and used nodes / GPUs / GPU milli / CPU milli.
+// One node's term of the report: the 7 exact bins, the power terms (when pw is given) and used
+// nodes / GPUs / GPU milli / CPU milli.
 __device__ __forceinline__ void node_term(const NodeV& n, int cap, const TypDev* tp, int ncpu, int nt,
-                                          __int128 (&f)[kFields]) {
+                                          const PowerDev* pw, int cm, __int128 (&f)[kFields]) {
   int gl[kMaxGpu];
   unpack_gl(n, gl);
   double b[7];
@@ -44,12 +51,22 @@ __device__ __forceinline__ void node_term(const NodeV& n, int cap, const TypDev*
     total += gl[g];
   }
   const bool used = ff < cnt || n.cpu_left < cap;  // analysis.go:89
-  f[7] = used ? 1 : 0;
-  f[8] = used ? cnt : 0;
-  f[9] = used ? (long long)cnt * kMilli - total : 0;
-  f[10] = used ? (long long)cap - n.cpu_left : 0;
-  f[11] = 0;
-  f[12] = 0;
+  f[9] = used ? 1 : 0;
+  f[10] = used ? cnt : 0;
+  f[11] = used ? (long long)cnt * kMilli - total : 0;
+  f[12] = used ? (long long)cap - n.cpu_left : 0;
+  f[13] = 0;
+  f[14] = 0;
+  f[7] = f[8] = f[15] = 0;
+  if (pw) {
+    double cw = 0, gw = 0;
+    if (node_power(n.cpu_left, cap, cm, gl, cnt, n.gpu_type(), *pw, &cw, &gw)) {
+      f[7] = fix80(cw);
+      f[8] = fix80(gw);
+    } else {
+      f[15] = 1;
+    }
+  }
 }
 
 __device__ __forceinline__ void stage_typical(const TypDev* __restrict__ tp, int nt, TypDev* s_tp) {
@@ -60,15 +77,10 @@ __device__ __forceinline__ void stage_typical(const TypDev* __restrict__ tp, int
 
 __device__ __forceinline__ void store_rep(RepAcc* o, const __int128 (&f)[kFields]) {
 #pragma unroll
-  for (int k = 0; k < 7; ++k) o->bins[k] = f[k];
+  for (int k = 0; k < kFx; ++k) o->fx[k] = f[k];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) o->cnt[k] = (long long)f[7 + k];
-}
-__device__ __forceinline__ void load_rep(const RepAcc* o, __int128 (&f)[kFields]) {
-#pragma unroll
-  for (int k = 0; k < 7; ++k) f[k] = o->bins[k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) f[7 + k] = o->cnt[k];
+  for (int k = kFx; k < kFields; ++k) o->cnt[k - kFx] = (long long)f[k];
+  o->cnt[kFields - kFx] = 0;
 }
 
 // grid (ceil(E_max / kDeltaBlock), R): the report delta of every event.
@@ -86,19 +98,22 @@ __global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* 
   const PodDev p = rp.ev[e];
   const ResultDev res = rp.res[e];
   if (!(p.flags & kPodDelete)) {
-    d[11] = (long long)p.milli * (long long)p.num;  // PodResource.TotalMilliGpu (resource.go:129-131)
-    d[12] = p.cpu_nz;                               // PodResource.MilliCpu
+    d[13] = (long long)p.milli * (long long)p.num;  // PodResource.TotalMilliGpu (resource.go:129-131)
+    d[14] = p.cpu_nz;                               // PodResource.MilliCpu
   }
   if (res.node >= 0 && (res.status == ST_OK || res.status == ST_DELETED)) {
     const int pv = rp.prev[e];
     const NodeV after = load_node(rp.snap + e);
     const NodeV before = load_node(pv >= 0 ? rp.snap + pv : rp.init + res.node);
     const int cap = rp.cap[res.node];
+    const PowerDev* pw = rp.has_pw ? rp.pw : nullptr;
+    const int cm = rp.cpum[res.node];
     __int128 a[kFields], b[kFields];
-    node_term(after, cap, s_tp, rp.ncpu, rp.nt, a);
-    node_term(before, cap, s_tp, rp.ncpu, rp.nt, b);
+    node_term(after, cap, s_tp, rp.ncpu, rp.nt, pw, cm, a);
+    node_term(before, cap, s_tp, rp.ncpu, rp.nt, pw, cm, b);
 #pragma unroll
-    for (int k = 0; k < 11; ++k) d[k] = a[k] - b[k];
+    for (int k = 0; k < 13; ++k) d[k] = a[k] - b[k];
+    d[15] = a[15] - b[15];
   }
   store_rep(rp.rep + e, d);
 }
@@ -133,14 +148,15 @@ __device__ __forceinline__ __int128 block_excl_scan128(__int128 v, __int128* s_w
   return base + incl - v;
 }
 
-// Field k of a RepAcc (bins 0-6 are 128-bit, counters 7-12 are 64-bit).
+// Field k of a RepAcc (0-8 are 128-bit fixed point, 9-15 64-bit counters).
 __device__ __forceinline__ __int128 rep_get(const RepAcc* o, int k) {
-  return k < 7 ? o->bins[k] : (__int128)o->cnt[k - 7];
+  return k < kFx ? o->fx[k] : (__int128)o->cnt[k - kFx];
 }
 __device__ __forceinline__ void rep_set(RepAcc* o, int k, __int128 v) {
-  if (k < 7) o->bins[k] = v;
-  else o->cnt[k - 7] = (long long)v;
+  if (k < kFx) o->fx[k] = v;
+  else o->cnt[k - kFx] = (long long)v;
 }
+__device__ __forceinline__ bool power_field(int k) { return k == 7 || k == 8 || k == 15; }
 
 // grid R: the initial cluster's report, then the inclusive prefix over the events (in place),
 // one field at a time (keeps the 128-bit running sums in a few registers).
@@ -159,9 +175,10 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
     __int128 acc[kFields];
 #pragma unroll
     for (int k = 0; k < kFields; ++k) acc[k] = 0;
+    const PowerDev* pw = rp.has_pw ? rp.pw : nullptr;
     for (int i = tid; i < N; i += kScanBlock) {
       __int128 f[kFields];
-      node_term(load_node(rp.init + i), rp.cap[i], s_tp, rp.ncpu, rp.nt, f);
+      node_term(load_node(rp.init + i), rp.cap[i], s_tp, rp.ncpu, rp.nt, pw, rp.cpum[i], f);
 #pragma unroll
       for (int k = 0; k < kFields; ++k) acc[k] += f[k];
     }
@@ -179,6 +196,7 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
   const int lo = min(E, tid * per), hi = min(E, lo + per);
 #pragma unroll 1
   for (int k = 0; k < kFields; ++k) {
+    if (!rp.has_pw && power_field(k)) continue;  // stays 0 (k_report_delta wrote 0)
     __int128 loc = 0;
     for (int e = lo; e < hi; ++e) loc += rep_get(rp.rep + e, k);
     __int128 tot;

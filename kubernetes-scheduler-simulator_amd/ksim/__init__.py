@@ -97,6 +97,11 @@ class Report(C.Structure):
                 ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64)]
 
 
+class PowerReport(C.Structure):
+    _fields_ = [("cluster_w", C.c_double), ("cpu_w", C.c_double), ("gpu_w", C.c_double),
+                ("invalid_nodes", C.c_int64)]
+
+
 class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("nodes_per_block", C.c_int32), ("steps_per_graph", C.c_int32),
                 ("wgs_per_replica", C.c_int32), ("run_mode", C.c_int32), ("reserved", C.c_int32 * 3)]
@@ -123,7 +128,7 @@ class ReplayCfg(C.Structure):
 
 
 assert C.sizeof(Node) == 128 and C.sizeof(Pod) == 48 and C.sizeof(Typical) == 32 and C.sizeof(Result) == 24
-assert C.sizeof(Report) == 112
+assert C.sizeof(Report) == 112 and C.sizeof(PowerReport) == 32
 
 _LIB = None
 
@@ -159,6 +164,7 @@ SIGNATURES = {
     "ksim_engine_last_run_path": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
     "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
+    "ksim_engine_get_power_reports": (C.c_int, [_VP, C.c_int, _P(PowerReport), C.c_int]),
     "ksim_engine_last_report_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_shard_comm_id": (C.c_int, [_P(C.c_uint8)]),
     "ksim_engine_set_shard": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _P(C.c_uint8)]),
@@ -513,6 +519,15 @@ class Engine:
         d = {k: np.array(a[k]) for k in keys}
         d["frag_bins"] = np.array(a["frag_bins"])
         return d
+
+    def power_reports(self, r):
+        """The [Power] report after every event of replica r (analysis.go:24-56; needs set_power_model):
+        list of dicts cluster_w / cpu_w / gpu_w / invalid_nodes."""
+        n = self.n_events[r]
+        out = (PowerReport * max(1, n))()
+        check(lib().ksim_engine_get_power_reports(self.h, r, out, n), "get_power_reports")
+        return [dict(cluster_w=out[i].cluster_w, cpu_w=out[i].cpu_w, gpu_w=out[i].gpu_w,
+                     invalid_nodes=out[i].invalid_nodes) for i in range(n)]
 
     def last_report_ms(self):
         ms = C.c_double(0)

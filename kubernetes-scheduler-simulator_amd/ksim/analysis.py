@@ -61,25 +61,152 @@ def report_messages(rep):
     return [m + "\n" for m in msgs]
 
 
+_LOGRUS_SAFE = set("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-._/@^+")
+
+
 def logrus_line(msg, ts="2024-08-07T00:00:00Z"):
-    """The logrus TextFormatter line of log.Infof(msg): the message is %q-quoted, so the
-    trailing newline of the reference's report formats appears as the two characters \\n."""
+    """The logrus TextFormatter line of log.Info*(msg) (vendor/github.com/sirupsen/logrus/
+    text_formatter.go:151-153,298-337): no msg key for an empty message (log.Infoln()), the bare
+    message when every character is in logrus' safe set, else %q-quoted -- so the trailing newline
+    of the reference's Infof formats appears as the two characters \\n."""
+    if msg == "":
+        return 'time="%s" level=info\n' % ts
+    if all(ch in _LOGRUS_SAFE for ch in msg):
+        return 'time="%s" level=info msg=%s\n' % (ts, msg)
     q = msg.replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n")
     return 'time="%s" level=info msg="%s"\n' % (ts, q)
 
 
-def write_log(path, reports, pod_names=None, events=None):
-    """A log file with, per event, the "attempt to create/delete pod" line (when pod names are
-    given, simulator.go:410,420) and the report lines, as `simon apply` writes them."""
+NAMESPACE = "paib-gpu"  # the openb pod YAMLs' namespace (data/pod_csv_to_yaml.py:27,55)
+
+
+def pod_repr(cpu_milli, gpu_milli, gpu_count, gpu_spec=""):
+    """PodResource.Repr (pkg/type/resource.go:104-127); cpu_milli is PodResource.MilliCpu (the
+    non-zero request), gpu_spec the gpu-card-model pipe list ("" = none given)."""
+    gputype = gpu_spec if gpu_spec else ("ANY" if gpu_milli > 0 else "NONE")
+    return "<CPU: %6.2f, GPU: %d x {%-4d}m (CPUREQ: %s) (GPUREQ: %s)>" % (
+        cpu_milli / 1000, gpu_count, gpu_milli, "ANY", gputype)
+
+
+def power_message(pw):
+    """analysis.go:54-55: the [Power] line of ClusterPowerConsumptionReport (watts)."""
+    return "[Power]; cluster: %.1f; ClusterCPU: %.1f; ClusterGPU: %.1f\n" % (pw["cpu_w"] + pw["gpu_w"], pw["cpu_w"],
+                                                                           pw["gpu_w"])
+
+
+QUAD_NAMES = ["q1_lack_both", "q2_lack_gpu", "q3_satisfied", "q4_lack_cpu", "xl_satisfied", "xr_lack_cpu",
+              "no_access"]  # frag.go:18-35 FragRatioDataMap, in bin order
+MIB = 1024 * 1024
+
+
+def allocation_messages(nodes):
+    """alloc.go:65-88 ReportNodeAllocationRate over GetNodeAllocMap (alloc.go:90-126): requested /
+    allocatable per resource, summed over the nodes.  nodes: dicts cpu_alloc, cpu_used (milli),
+    mem_alloc_mib, mem_used_mib, gpu_count, gpu_used (per-GPU used milli)."""
+    req = {"MilliCpuLeft": 0, "Memory": 0, "Gpu": 0, "MilliGpu": 0}
+    alloc = dict(req)
+    for n in nodes:
+        req["MilliCpuLeft"] += n["cpu_used"]
+        alloc["MilliCpuLeft"] += n["cpu_alloc"]
+        req["Memory"] += n["mem_used_mib"] * MIB          # Quantity.Value() of "<n>Mi" requests
+        alloc["Memory"] += n["mem_alloc_mib"] * MIB
+        used = [u for u in n["gpu_used"][:n["gpu_count"]]]
+        req["Gpu"] += sum(1 for u in used if u > 0)        # DevsBrief with GpuUsedMilli > 0
+        alloc["Gpu"] += n["gpu_count"]
+        req["MilliGpu"] += sum(used)
+        alloc["MilliGpu"] += n["gpu_count"] * 1000
+    msgs = ["Allocation Ratio:\n"]
+    for k in ("MilliCpuLeft", "Memory", "Gpu", "MilliGpu"):  # alloc.go:21 resourceList
+        ratio = 0.0 if alloc[k] == 0 else 100.0 * float(req[k]) / float(alloc[k])
+        msgs.append("    %-8s: %4.1f%% (%d/%d)\n" % (k, ratio, req[k], alloc[k]))
+    return msgs
+
+
+def cluster_analysis_messages(nodes, frag_bins, tag="InitSchedule"):
+    """analysis.go:138-202 ClusterAnalysis(tag) on the final cluster: the block scripts/analysis.py
+    reads into analysis.csv (its 16 lines after the header, analysis.py:178-199).  frag_bins: the
+    cluster's 7 NodeGpuShareFragAmount sums (the last event's report).  gpuFragSum is summed in bin
+    order (the reference's Go-map order is random)."""
+    msgs = ["", "========== Cluster Analysis Results (%s) ==========" % tag]
+    msgs += allocation_messages(nodes)
+    total = 0.0
+    for v in frag_bins:
+        total += v
+    for k, v in enumerate(frag_bins):
+        msgs.append("%-13s: %6.2f x 10^3 (%s%%)\n" % (QUAD_NAMES[k], v / 1000, _go_f("%5.2f", _pct(v, total))))
+    msgs.append("--------------------")
+    msgs.append("%-13s: %6.2f x 10^3 (100.0%%)\n" % ("idle_gpu_milli", total / 1000))
+    frag = 0.0
+    for k in range(7):
+        if k != Q3:
+            frag += frag_bins[k]
+    msgs.append("%-13s: %6.2f x 10^3 (%s%%)\n" % ("frag_gpu_milli", frag / 1000, _go_f("%5.2f", _pct(frag, total))))
+    msgs.append("==============================================")
+    msgs.append("")
+    return msgs
+
+
+def _pct(v, total):
+    """100*v/total as Go evaluates it for %f (0/0 = NaN, x/0 = +-Inf: Go prints NaN / +Inf)."""
+    if total == 0:
+        return math.nan if v == 0 else math.copysign(math.inf, v)
+    return 100 * v / total
+
+
+def _go_f(fmt, x):
+    """Go's fmt of a float verb: Python's for finite values; NaN / +Inf / -Inf padded to the width."""
+    if math.isfinite(x):
+        return fmt % x
+    word = "NaN" if math.isnan(x) else ("+Inf" if x > 0 else "-Inf")
+    width = int(fmt[1:].split(".")[0] or 0)
+    return word.rjust(width)
+
+
+def failed_pods_messages(failed):
+    """utils.go:1344-1354 ReportFailedPods: failed = [(pod key, Repr)]."""
+    if not failed:
+        return []
+    return ["Failed Pods in detail:\n"] + ["  %s: %s\n" % (k, r) for k, r in failed] + [""]
+
+
+def write_log(path, reports, pod_names=None, events=None, power=None, pods=None, results=None, final_nodes=None,
+              n_original=None, tag="InitSchedule"):
+    """A log file as `simon apply` writes it, with the lines the reference's harness reads:
+      "Number of original workload pods" (core.go:108);
+      per event (simulator.go:405-428): "[i] attempt to create/delete pod(key)" and "Characteristics of
+        pod(key): Repr" (when pod names are given; pods = per-event (cpu_milli, gpu_milli, gpu_count,
+        gpu_spec) for the Repr), "[i] failed to schedule pod(key): Repr" (results[i] status
+        unschedulable / error), the [Report] / [Alloc] / [AllocCPU] lines, and [Power] when power
+        reports are given;
+      after the run (final_nodes given): ReportFailedPods (core.go:156), ClusterAnalysis(tag) (core.go:157)
+        and "there are N unscheduled pods" (apply.go:228-229)."""
+    n0 = n_original if n_original is not None else (len(reports) if pod_names is None else len(set(pod_names)))
+    failed = []
     with open(path, "w") as f:
-        f.write(logrus_line("Number of original workload pods: %d" % (len(reports) if pod_names is None
-                                                                      else len(set(pod_names)))))
+        f.write(logrus_line("Number of original workload pods: %d" % n0))
         for i, rep in enumerate(reports):
+            is_del = events is not None and bool(events[i]["is_delete"] if isinstance(events[i], dict) or
+                                                  hasattr(events[i], "dtype") else events[i].is_delete)
             if pod_names is not None:
-                kind = "delete" if events is not None and events[i].is_delete else "create"
-                f.write(logrus_line("[%d] attempt to %s pod(%s)\n" % (i, kind, pod_names[i])))
+                key = pod_names[i]
+                f.write(logrus_line("[%d] attempt to %s pod(%s)\n" % (i, "delete" if is_del else "create", key)))
+                if not is_del and pods is not None:
+                    f.write(logrus_line("Characteristics of pod(%s): %s\n" % (key, pod_repr(*pods[i]))))
+                if not is_del and results is not None and results[i] in (1, 2):
+                    rp = pod_repr(*pods[i]) if pods is not None else ""
+                    f.write(logrus_line("[%d] failed to schedule pod(%s): %s\n" % (i, key, rp)))
+                    failed.append((key, rp))
             for m in report_messages(rep):
                 f.write(logrus_line(m))
+            if power is not None:
+                f.write(logrus_line(power_message(power[i])))
+        if final_nodes is not None:
+            for m in failed_pods_messages(failed):
+                f.write(logrus_line(m))
+            for m in cluster_analysis_messages(final_nodes, reports[-1]["frag_bins"] if reports else [0.0] * 7, tag):
+                f.write(logrus_line(m))
+            if failed:
+                f.write(logrus_line("there are %d unscheduled pods\n" % len(failed)))
 
 
 def parse_log_lines(lines):
@@ -110,6 +237,57 @@ def parse_log_lines(lines):
                 for k, v in zip(["used_nodes", "used_gpus", "used_gpu_milli", "total_gpus", "arrived_gpu_milli"], vals):
                     allo.setdefault(k, []).append(v)
     return frag, allo
+
+
+ALLO_KEYS = ("MilliCpu", "Memory", "Gpu", "MilliGpu")  # scripts/analysis.py:7 (MilliCpuLeft is not one of them)
+
+
+def _snake(name):
+    """scripts/analysis.py:10-12 camel_to_snake."""
+    import re
+    name = re.sub("(.)([A-Z][a-z]+)", r"\1_\2", name)
+    return re.sub("([a-z0-9])([A-Z])", r"\1_\2", name).lower()
+
+
+def parse_log_full(lines):
+    """Everything scripts/analysis.py:120-330 (log_to_csv) takes from one log: the per-experiment
+    analysis.csv row (origin / unscheduled pods, the ClusterAnalysis allocation ratios, amounts, totals and
+    quadrant shares; no meta keys: the log name carries none here) and the per-event [Report] / [Alloc] /
+    [Power] columns.  Returns dict(row=..., frag=..., allo=..., power=...)."""
+    frag, allo = parse_log_lines(lines)
+    row = {"unscheduled": 0}
+    power = {}
+    counter, tag = 0, ""
+    for line in lines:
+        if INFOMSG not in line:
+            continue
+        line = line.split(INFOMSG)[1][1:-2]
+        if "Number of original workload pods" in line:
+            row["origin_pods"] = int(line.split(":")[1].strip())
+        if "there are" in line:
+            row["unscheduled"] = int(line.split("unscheduled pods")[0].split("there are")[1].strip())
+            break
+        if "Cluster Analysis" in line:
+            tag = line.split(")")[0].split("(")[1]
+            counter += 1
+        if 0 < counter <= 16:
+            counter = 0 if counter == 16 else counter + 1
+            item = line.strip().split(":")
+            if len(item) > 1:
+                key, value = item[0].strip(), item[1].strip()
+                if key in ALLO_KEYS:
+                    row[_snake(key + tag)] = float(value.split("%")[0])
+                    row[_snake(key + "Amount" + tag)] = float(value.split("(")[1].split("/")[0])
+                    row[_snake(key + "Total")] = float(value.split(")")[0].split("/")[1])
+                elif key in QUAD_NAMES or key == "frag_gpu_milli":
+                    row[_snake(key + tag)] = float(value.split("(")[1].split("%")[0].strip())
+        if line.startswith("[Power]"):
+            _, c, cpu, gpu = line.split(";")
+            for k, v in (("power_cluster", float(c.split(":")[1].strip())),
+                         ("power_cluster_CPU", float(cpu.split(":")[1].strip())),
+                         ("power_cluster_GPU", float(gpu.split(":")[1].strip()[:-2]))):
+                power.setdefault(k, []).append(v)
+    return dict(row=row, frag=frag, allo=allo, power=power)
 
 
 def parse_log(path):

@@ -85,8 +85,9 @@ class Sweep:
                 arr, n = typ[t]
                 eng.set_typical(r, arr, n)
                 eng.set_policy(r, ALL_POLICY_DIRS[p], seed=s)
-                if p in PWR_POLICY_DIRS:
-                    eng.set_power_model(r, traces[t].power_model())
+                # every experiment: PWR's energy model, and the per-event [Power] report the reference
+                # logs after every event whatever the policy (simulator.go:427)
+                eng.set_power_model(r, traces[t].power_model())
                 if p == "01-Random" and random_stream == "go":
                     eng.set_go_stream(r, traces[t].go_state(seed=s, tune_ratio=tune, shuffle=True))
                 eng.load_events(r, rp.events, rp.n)
@@ -149,6 +150,14 @@ def row_mismatches(curves, kind, expected):
         ours = c[kind]
         out[key] = sorted(k for k in set(ours) | set(ref) if ours.get(k) != ref.get(k))
     return out
+
+
+def max_rel_dev(ours, ref):
+    """Largest relative deviation |ours - ref| / |ref| over the points both curves have (absolute where
+    ref is 0); +inf when the point sets differ."""
+    if set(ours) != set(ref):
+        return float("inf")
+    return max((abs(ours[k] - ref[k]) / abs(ref[k]) if ref[k] else abs(ours[k])) for k in ref) if ref else 0.0
 
 
 def expected_mean_curve(csv_path, trace, policy, seeds=SEEDS):

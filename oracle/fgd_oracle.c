@@ -1394,6 +1394,13 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                     P->frag_bins[k] += 1.0 * b[k];
                     ex[k] += orc_fix80(b[k]);
                 }
+                double pc = 0, pg = 0;
+                if (orc_energy_node(&nr, &pc, &pg) == 0) {
+                    P->power_cpu += pc;  /* analysis.go:48-49 */
+                    P->power_gpu += pg;
+                } else {
+                    P->power_invalid += 1;
+                }
                 P->total_gpus += nr.gpu_number;
                 int ff = 0;
                 for (int g = 0; g < nr.n_gpu_left; g++)

@@ -202,6 +202,10 @@ typedef struct {
     int64_t used_cpu_milli, arrived_cpu_milli;
     double  frag_bins_exact[ORC_NBINS]; /* the same sums, exact, rounded once to nearest (see
                                            orc_fix80 in fgd_oracle.c; the product's contract) */
+    /* analysis.go:24-56 ClusterPowerConsumptionReport: Σ over nodes (input order) of
+     * orc_energy_node's CPU and GPU terms; nodes where it fails are counted, not summed */
+    double  power_cpu, power_gpu;
+    int64_t power_invalid;
 } orc_report;
 
 /* Go math/rand's global source (rng.go rngSource), for the Random draw structure */

@@ -65,7 +65,8 @@ class Result(C.Structure):
 class Report(C.Structure):
     _fields_ = [("frag_bins", C.c_double * 7), ("used_nodes", C.c_int64), ("used_gpus", C.c_int64),
                 ("used_gpu_milli", C.c_int64), ("total_gpus", C.c_int64), ("arrived_gpu_milli", C.c_int64),
-                ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64), ("frag_bins_exact", C.c_double * 7)]
+                ("used_cpu_milli", C.c_int64), ("arrived_cpu_milli", C.c_int64), ("frag_bins_exact", C.c_double * 7),
+                ("power_cpu", C.c_double), ("power_gpu", C.c_double), ("power_invalid", C.c_int64)]
 
 
 class GoRng(C.Structure):
@@ -335,7 +336,8 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
                         used_gpus=rep[i].used_gpus, used_gpu_milli=rep[i].used_gpu_milli,
                         total_gpus=rep[i].total_gpus, arrived_gpu_milli=rep[i].arrived_gpu_milli,
                         used_cpu_milli=rep[i].used_cpu_milli, arrived_cpu_milli=rep[i].arrived_cpu_milli,
-                        frag_bins_exact=list(rep[i].frag_bins_exact))
+                        frag_bins_exact=list(rep[i].frag_bins_exact), power_cpu=rep[i].power_cpu,
+                        power_gpu=rep[i].power_gpu, power_invalid=rep[i].power_invalid)
                    for i in range(ne)]
     return results, state, reports
 

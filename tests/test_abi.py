@@ -41,7 +41,8 @@ def test_struct_layouts_match_c():
     subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), src, "-o", exe], check=True)
     got = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
     want = [C.sizeof(t) for t in (ksim.Node, ksim.Pod, ksim.Typical, ksim.Result, ksim.Config, ksim.TraceNode,
-                                  ksim.TracePod, ksim.TypicalCfg, ksim.ReplayCfg)]
+                                  ksim.TracePod, ksim.TypicalCfg, ksim.ReplayCfg, ksim.Report, ksim.PowerReport,
+                                  ksim.PowerModel)]
     assert got == want
 
 

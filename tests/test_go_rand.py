@@ -33,6 +33,7 @@ ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "kubernetes-scheduler-simulator_amd")
 ALLO = os.path.join(HERE, "golden", "expected_results", "analysis_allo_discrete.csv")
 FRAG = os.path.join(HERE, "golden", "expected_results", "analysis_frag_discrete.csv")
+FRAG_RATIO = os.path.join(HERE, "golden", "expected_results", "analysis_frag_ratio_discrete.csv")
 
 # Go's documented outputs for the default seed 1 (math/rand before Go 1.20)
 SEED1_INT63 = [5577006791947779410, 8674665223082153551, 6129484611666145821, 4037200794235010051,
@@ -121,6 +122,11 @@ def test_whole_experiment_row_identical_via_oracle(trace, policy, seed):
         ref = SW.expected_rows(csv)[key]
         assert len(ref) == 131
         assert cv[kind] == ref, (kind, [a for a in ref if cv[kind].get(a) != ref[a]][:5])
+    # the full-precision fragmentation-ratio row (merge_frag_ratio_discrete.py:77-88: the mean of every
+    # event's 2-decimal "Frag ratio" in an arrived-% bin): north_star's 1e-9 relative curve contract
+    ref = SW.expected_rows(FRAG_RATIO)[key]
+    assert len(ref) == 131 and set(cv["frag_ratio"]) == set(ref)
+    assert SW.max_rel_dev(cv["frag_ratio"], ref) <= 1e-9
 
 
 def test_informer_draws_are_what_pins_the_node_names():

@@ -3,7 +3,9 @@
 Bar: for every event, the device report equals the oracle's exact-sum report bit for bit (7
 cluster bins, used nodes / GPUs / GPU milli / CPU milli, arrived GPU / CPU milli), and its bins
 are within 1e-9 relative of the oracle's literal fp64 sum in node order (the reference's sum
-order is a Go map's; north_star's curve tolerance).  Every test needs a gfx950 device.
+order is a Go map's; north_star's curve tolerance).  The [Power] report that follows it
+(analysis.go:24-56, with the trace's energy model set on every replica) equals the oracle's per-node
+GetEnergyConsumptionNode sums exactly on every event.  Every test needs a gfx950 device.
 """
 import pytest
 
@@ -32,11 +34,14 @@ def engine_reports(trace, nodes, events, n_ev, policy, seed=0, run_mode=0, wgs=0
     eng.set_nodes(0, nodes)
     eng.set_typical(0, arr, n)
     eng.set_policy(0, policy, seed=seed)
+    eng.set_power_model(0, trace.power_model())
     eng.set_report(True)
     eng.load_events(0, events, n_ev)
     eng.run()
-    res, reps = eng.results(0), eng.reports(0)
+    res, reps, pw = eng.results(0), eng.reports(0), eng.power_reports(0)
     eng.close()
+    for r, p in zip(reps, pw):
+        r["power"] = p
     return res, reps
 
 
@@ -48,6 +53,10 @@ def assert_reports(got, want):
             assert g[k] == w[k], (i, k, g[k], w[k])
         for a, b in zip(g["frag_bins"], w["frag_bins"]):
             assert abs(a - b) <= 1e-9 * max(abs(b), 1.0), (i, a, b)
+        if "power" in g:
+            p = g["power"]
+            assert (p["cpu_w"], p["gpu_w"], p["invalid_nodes"]) == (w["power_cpu"], w["power_gpu"], w["power_invalid"]), \
+                (i, p, w["power_cpu"], w["power_gpu"])
 
 
 def subset(trace, rp, step, off=0):
