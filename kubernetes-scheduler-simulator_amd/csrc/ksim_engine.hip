@@ -2475,6 +2475,11 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
 void ksim_engine_destroy(ksim_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  // drain every stream the engine launched on before anything they use is freed or destroyed: no
+  // dispatch (or a profiler's completion callback on it) may outlive its buffers, streams or graph
+  for (int i = 0; i < ksim_engine::kSide; ++i)
+    if (e->side[i]) (void)hipStreamSynchronize(e->side[i]);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->graph) (void)hipGraphExecDestroy(e->graph);
   for (auto p : e->d_ev) (void)hipFree(p);
   for (auto p : e->d_res) (void)hipFree(p);

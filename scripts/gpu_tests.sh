@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 1080 python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu "$@" \
+timeout -k 10 1080 python -u -m pytest -v --durations=40 --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu "$@" \
   > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3

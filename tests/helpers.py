@@ -27,6 +27,12 @@ def oracle_nodes(trace, replay):
                  model=types[tn[i]["type"]] if tn[i]["gpu"] > 0 else "") for i in range(len(tn))]
 
 
+def oracle_subset(trace, replay, keep):
+    """oracle_nodes restricted to the node indices `keep` (built once, not once per index)."""
+    full = oracle_nodes(trace, replay)
+    return [full[i] for i in keep]
+
+
 def oracle_events(trace, replay, limit=None):
     pods = trace.pods()
     n = replay.n if limit is None else min(limit, replay.n)

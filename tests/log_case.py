@@ -44,7 +44,7 @@ def oracle_log(path, policy):
     """The log of the oracle's run (string-typed restatement, oracle/fgd_oracle.c)."""
     import pyoracle as O
     t, rp, keep = inputs()
-    nodes = [helpers.oracle_nodes(t, rp)[i] for i in keep]
+    nodes = helpers.oracle_subset(t, rp, keep)
     pol, sel = POLICIES[policy]
     ev = helpers.oracle_events(t, rp, N_EVENTS)
     res, state, reps = O.run_events(nodes, helpers.oracle_typical(t), ev, policy=getattr(O, pol),

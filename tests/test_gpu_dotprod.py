@@ -56,21 +56,22 @@ def run_engine(nodes, nn, typical, events, n_ev, dim, norm, gpusel=None, report=
         eng.close()
 
 
-@pytest.mark.parametrize("run", sorted(PATHS))
 @pytest.mark.parametrize("norm", NORMS)
 @pytest.mark.parametrize("dim", DIMS)
-def test_subset_replay(default_trace, dim, norm, run):
+def test_subset_replay(default_trace, dim, norm):
+    # one oracle replay per configuration, every execution path against it
     rp = default_trace.replay(seed=42)
     keep = list(range(3, default_trace.num_nodes, 7))  # 173 nodes, every GPU model
     n_ev = 1500
-    res, state, path = run_engine(helpers.subset_nodes(rp, keep), len(keep), default_trace.typical(), rp.events,
-                                  n_ev, dim, norm, **PATHS[run])
-    assert path == run.split("-")[0]
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                                        helpers.oracle_events(default_trace, rp, n_ev), policy=O.POL_DOTPROD,
                                        gpu_sel=oracle_sel(dim, None), threads=16, dim_ext=ODIM[dim], norm=ONORM[norm])
-    assert_same(res, want, state, want_state, keep)
+    for run in sorted(PATHS):
+        res, state, path = run_engine(helpers.subset_nodes(rp, keep), len(keep), default_trace.typical(), rp.events,
+                                      n_ev, dim, norm, **PATHS[run])
+        assert path == run.split("-")[0]
+        assert_same(res, want, state, want_state, keep)
 
 
 @pytest.mark.parametrize("dim", ["share", "extend"])
@@ -80,7 +81,7 @@ def test_best_fit_selector_with_split_dims(default_trace, dim):
     keep = list(range(0, default_trace.num_nodes, 5))
     res, state, _ = run_engine(helpers.subset_nodes(rp, keep), len(keep), default_trace.typical(), rp.events, 2000,
                                dim, "node", gpusel="best")
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                                        helpers.oracle_events(default_trace, rp, 2000), policy=O.POL_DOTPROD,
                                        gpu_sel=O.SEL_BEST, threads=16, dim_ext=ODIM[dim], norm=O.NORM_NODE)

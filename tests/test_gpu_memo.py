@@ -120,7 +120,7 @@ def test_memo_deletions(default_trace, mode):
     eng.load_events(0, evs, len(evs))
     eng.run()
     got = eng.results(0)
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev, policy=O.POL_FGD,
                                        gpu_sel=O.SEL_FGD, threads=16)
     assert_same(got, want, eng.nodes(0), want_state, keep)

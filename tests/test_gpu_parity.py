@@ -158,7 +158,7 @@ def test_deletion_events(default_trace):
     eng.load_events(0, arr_ev, len(evs))
     eng.run()
     got = eng.results(0)
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev, policy=O.POL_FGD,
                                        gpu_sel=O.SEL_FGD, threads=16)
     assert got == want

@@ -109,7 +109,7 @@ def test_deletes_and_report(default_trace, policy, run):
     finally:
         eng.close()
     name, w = ksim.parse_policy(policy)
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     w_pwr, w_fgd = w if w else (0, 0)
     want, want_state, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev,
                                        policy=O.POL_PWR if name == "PWR" else O.POL_PWR_FGD,
@@ -128,7 +128,7 @@ def test_plugin_level_score_and_reserve(default_trace):
     eng.set_nodes(0, helpers.subset_nodes(rp, keep))
     eng.set_policy(0, "PWR")
     eng.set_power_model(0, default_trace.power_model())
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     evs = helpers.oracle_events(default_trace, rp, 200)
     for k in range(0, 200, 17):
         feas, score, gpu = eng.filter_score(0, rp.events[k], step=k)

@@ -53,7 +53,7 @@ def run_engine(trace, nodes, events, n_ev, states, gpusel="random", report=False
 
 
 def oracle(trace, rp, keep, n_ev, state, gpusel="random", report=False, events=None):
-    onodes = [helpers.oracle_nodes(trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(trace, rp, keep)
     oev = events if events is not None else helpers.oracle_events(trace, rp, n_ev)
     return O.run_events(onodes, helpers.oracle_typical(trace), oev, policy=O.POL_RANDOM, gpu_sel=SEL[gpusel],
                         seed=5, threads=8, with_report=report, go_stream=state[:3])
@@ -84,7 +84,7 @@ def test_selectors_and_mixed_engine(default_trace, gpusel):
     for r, st in enumerate(states):
         want, _, _ = oracle(default_trace, rp, keep, n_ev, st, gpusel=gpusel)
         assert got[r] == want, r
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     hashed, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                                 helpers.oracle_events(default_trace, rp, n_ev), policy=O.POL_RANDOM,
                                 gpu_sel=SEL[gpusel], seed=5, threads=8)

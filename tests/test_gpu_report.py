@@ -61,7 +61,7 @@ def assert_reports(got, want):
 
 def subset(trace, rp, step, off=0):
     keep = list(range(off, trace.num_nodes, step))
-    onodes = [helpers.oracle_nodes(trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(trace, rp, keep)
     return keep, helpers.subset_nodes(rp, keep), onodes
 
 
@@ -123,7 +123,7 @@ def test_report_multi_replica_ragged(default_trace):
     eng.run()
     assert eng.last_report_ms() > 0
     for r, (seed, name, pol, sel, n_ev) in enumerate(cfgs):
-        onodes = [helpers.oracle_nodes(default_trace, rps[r])[i] for i in keep]
+        onodes = helpers.oracle_subset(default_trace, rps[r], keep)
         _, _, want = O.run_events(onodes, helpers.oracle_typical(default_trace),
                                   helpers.oracle_events(default_trace, rps[r], n_ev), policy=pol, gpu_sel=sel,
                                   threads=16, with_report=True)

@@ -61,7 +61,7 @@ def test_group_all_policies_vs_oracle(default_trace, name, pol, sel):
     g.run()
     got = g.results()
     g.close()
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                               helpers.oracle_events(default_trace, rp, n_ev), policy=pol, gpu_sel=sel, seed=3,
                               threads=16)
@@ -78,7 +78,7 @@ def test_group_with_deletions(default_trace):
     g.run()
     got = g.results()
     g.close()
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace), oev, policy=O.POL_FGD,
                               gpu_sel=O.SEL_FGD, threads=16)
     assert got == want
@@ -192,7 +192,7 @@ def test_host_exchange_two_processes(default_trace, name, pol, sel):
         assert p.exitcode == 0
     rp = default_trace.replay(seed=7)
     keep = list(range(1, default_trace.num_nodes, 5))
-    onodes = [helpers.oracle_nodes(default_trace, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                               helpers.oracle_events(default_trace, rp, n_ev), policy=pol, gpu_sel=sel, seed=3,
                               threads=16)

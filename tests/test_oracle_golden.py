@@ -131,7 +131,7 @@ def test_report_exact_sum_is_fsum():
     t = ksim.Trace.openb("default")
     rp = t.replay(seed=42)
     keep = list(range(0, t.num_nodes, 5))
-    onodes = [helpers.oracle_nodes(t, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(t, rp, keep)
     tl = helpers.oracle_typical(t)
     tp = O.typical(tl)
     for n_ev in (1, 200, 900):

@@ -121,7 +121,7 @@ def _rank_main(rank, world, port, q):
     rp = t.replay(seed=42)
     keep = list(range(0, t.num_nodes, 10))
     nodes = helpers.subset_nodes(rp, keep)
-    onodes = [helpers.oracle_nodes(t, rp)[i] for i in keep]
+    onodes = helpers.oracle_subset(t, rp, keep)
     full, _, _ = O.run_events(onodes, helpers.oracle_typical(t), helpers.oracle_events(t, rp, 300), threads=1)
     OracleShard.full, OracleShard.all_nodes = full, nodes
     merged, _ = SH.run_distributed(nodes, t.typical(), rp.events, 300, dist, engine_cls=OracleShard)
