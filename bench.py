@@ -33,8 +33,14 @@ BYTES_PER_NODE_EVAL = 32
 BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # Counter passes of each bench configuration (scripts/profile_config.sh NAME ...): HBM bytes per
 # dispatch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section) and its
-# VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/r02/prof/<profile_key(args)>/pmc.json.
-PROF_DIR = os.path.join(ROOT, "profiles", "r02", "prof")
+# VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/<round>/prof/<profile_key(args)>/pmc.json, the
+# newest round that profiled the configuration first.
+PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r03", "r02")]
+PROF_DIR = PROF_DIRS[0]
+# MI355X_MICROARCH.md, persistent-kernel price list: handoff-1to1 = one producer -> one consumer
+# granule hand-off between CUs, idle chip, 8 B: 0.8 us.  A pod step whose decision crosses CUs
+# (k_memo, wide k_hmemo, k_replay at K > 1) pays at least one.
+HANDOFF_FLOOR_US = 0.8
 
 
 def profile_key(args):
@@ -56,8 +62,9 @@ def profile_key(args):
 def profile_rooflines(args, kernel):
     """(traffic, traffic_source, valu) from this configuration's counter passes, if it was profiled and
     the profiled dominant kernel is the one this run launched."""
-    pf = os.path.join(PROF_DIR, profile_key(args), "pmc.json")
-    if not os.path.exists(pf):
+    pf = next((f for f in (os.path.join(d, profile_key(args), "pmc.json") for d in PROF_DIRS) if os.path.exists(f)),
+              None)
+    if pf is None:
         return None, None, None
     with open(pf) as f:
         pmc = json.load(f)
@@ -165,6 +172,18 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def latency_block(kern_us, steps, wgs):
+    """Per pod step of one replica: the dominant launch's duration over the steps it replays (replicas run
+    concurrently, so this is the dependent-chain latency of one step), beside the measured floor of a
+    cross-CU hand-off when a step's decision crosses CUs (wgs > 1)."""
+    us = kern_us / steps if steps else None
+    out = {"bound": "latency", "us_per_pod_step": us, "steps_per_launch": steps}
+    if wgs and wgs > 1 and us:
+        out.update(floor_us=HANDOFF_FLOOR_US, frac=HANDOFF_FLOOR_US / us,
+                   floor="MI355X_MICROARCH.md handoff-1to1 (idle, 8 B): one cross-CU granule hand-off per pod step")
+    return out
 
 
 def seeds_for_rank(rank, replicas, base=42):
@@ -319,8 +338,12 @@ def main():
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     # what the counters saw the kernel move, as a fraction of peak over the same time
+                     "traffic_frac": (traffic / (kern_us * 1e-6) / (HBM_PEAK_GBS * 1e9)) if traffic else None,
                      "kernel": kernel, "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
                      "wgs_per_replica": eng.last_run_wgs()},
+        # the bound that binds: every replica is a chain of dependent pod steps
+        "latency": latency_block(kern_us, steps_per_run, eng.last_run_wgs()),
         "valu_roofline": valu,
     }
     if args.config == "c4":

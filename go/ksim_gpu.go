@@ -58,9 +58,14 @@ import (
 
 const (
 	KsimGpuPluginName                    = "KsimGpu"
+	KsimGpuCompanionName                 = "KsimGpuCompanion"
 	ksimStateKey      framework.StateKey = "PreFilter-" + KsimGpuPluginName
 	mib                                  = int64(1) << 20
 )
+
+// The primary plugin of each scheduler framework, for its companion score plugin (same profile, same
+// handle; the framework builds the two independently and in any order).
+var ksimPrimaries sync.Map // framework.Handle -> *KsimGpuPlugin
 
 // KsimGpuPluginCfg is the plugin's args in the scheduler configuration (pluginConfig), next to the
 // reference's OpenGpuSharePluginCfg (pkg/type/config.go:50-61).
@@ -80,6 +85,13 @@ type KsimGpuPluginCfg struct {
 	WriteGpuIndex bool `json:"writeGpuIndex,omitempty"`
 	// Device: the HIP device ordinal.
 	Device int `json:"device,omitempty"`
+	// Companion: a second score plugin computed on the same device state, by its reference name (e.g.
+	// "PWRScore" beside "FGDScore" for the fork's weighted "PWR 500 FGD 500" runs,
+	// experiments/run_scripts/generate_run_scripts.py:31-42).  Its scores reach the framework through
+	// the KsimGpuCompanion score plugin, which the scheduler configuration enables with the companion's
+	// weight next to KsimGpu's; the framework then sums weight x normalized score per plugin as it does
+	// for the reference's two plugins (framework.go:686-704).
+	Companion string `json:"companion,omitempty"`
 }
 
 var ksimPolicies = map[string]C.int{
@@ -124,6 +136,7 @@ type ksimCycle struct {
 	feasible []C.uint8_t
 	score    []C.int32_t
 	gpuMask  []C.int32_t
+	score2   []C.int32_t // the companion policy's scores (replica 1), when configured
 	step     int32
 }
 
@@ -143,6 +156,7 @@ type KsimGpuPlugin struct {
 	typicalPods *simontype.TargetPodList
 	policy      C.int
 	gpuSel      C.int
+	companion   C.int // the companion policy (replica 1 of the engine), -1 none
 
 	eng   *C.ksim_engine
 	names []string       // engine node index -> node name
@@ -189,8 +203,17 @@ func NewKsimGpuPlugin(configuration runtime.Object, handle framework.Handle,
 	if C.ksim_device_count() <= C.int(cfg.Device) { // no CPU fallback: fail at construction
 		return nil, ksimError("device", C.KSIM_ENODEV)
 	}
+	companion := C.int(-1)
+	if cfg.Companion != "" {
+		c, ok := ksimPolicies[cfg.Companion]
+		if !ok {
+			return nil, fmt.Errorf("ksim: unknown companion policy %q", cfg.Companion)
+		}
+		companion = c
+	}
 	p := &KsimGpuPlugin{cfg: cfg, handle: handle, typicalPods: typicalPods, policy: policy, gpuSel: gpuSel,
-		index: map[string]int{}, vocab: map[string]int{}, bound: map[types.UID]ksimBinding{}}
+		companion: companion, index: map[string]int{}, vocab: map[string]int{}, bound: map[types.UID]ksimBinding{}}
+	ksimPrimaries.Store(handle, p)
 	// a deleted pod leaves its node (informer DeleteFunc, open_gpu_share.go:58-70; the scheduler cache
 	// releases its cpu / memory, simulator.go:416-422): the device state follows
 	handle.SharedInformerFactory().Core().V1().Pods().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
@@ -368,7 +391,11 @@ func (p *KsimGpuPlugin) ensureEngine() error {
 	}
 	var eng *C.ksim_engine
 	cfg := C.ksim_config{device: C.int32_t(p.cfg.Device)}
-	if rc := C.ksim_engine_create(&cfg, C.int(len(infos)), 1, &eng); rc != 0 {
+	replicas := 1
+	if p.companion >= 0 {
+		replicas = 2
+	}
+	if rc := C.ksim_engine_create(&cfg, C.int(len(infos)), C.int(replicas), &eng); rc != 0 {
 		return ksimError("create", rc)
 	}
 	fail := func(what string, rc C.int) error {
@@ -379,8 +406,9 @@ func (p *KsimGpuPlugin) ensureEngine() error {
 		return fail("set_nodes", rc)
 	}
 	// the target workload (GetTypicalPods, frag.go:285-380; core.go:110 SetTypicalPods)
+	var ct []C.ksim_typical
 	if p.typicalPods != nil && len(*p.typicalPods) > 0 {
-		ct := make([]C.ksim_typical, len(*p.typicalPods))
+		ct = make([]C.ksim_typical, len(*p.typicalPods))
 		for i, t := range *p.typicalPods {
 			mask, err := p.typeMask(t.TargetPodResource.GpuType)
 			if err != nil {
@@ -398,36 +426,56 @@ func (p *KsimGpuPlugin) ensureEngine() error {
 	if rc := C.ksim_engine_set_policy(eng, 0, p.policy, p.gpuSel, C.uint64_t(p.cfg.Seed)); rc != 0 {
 		return fail("set_policy", rc)
 	}
-	if p.policy == C.KSIM_POLICY_DOTPROD {
-		// GenerateSchedulingMatchGroups' cfg (utils.go:1274-1342); empty = the paper's merge / max
-		dim, norm := C.int(C.KSIM_DIMEXT_MERGE), C.int(C.KSIM_NORM_MAX)
-		if p.cfg.DimExtMethod != "" {
-			d, ok := ksimDimExt[p.cfg.DimExtMethod]
-			if !ok {
-				return fmt.Errorf("ksim: undefined gpu dimension extension method: %v", p.cfg.DimExtMethod)
-			}
-			dim = d
-		}
-		if p.cfg.NormMethod != "" {
-			n, ok := ksimNorm[p.cfg.NormMethod]
-			if !ok {
-				return fmt.Errorf("ksim: undefined normalization for dot product: %v", p.cfg.NormMethod)
-			}
-			norm = n
-		}
-		if rc := C.ksim_engine_set_plugin_cfg(eng, 0, dim, norm); rc != 0 {
-			return fail("set_plugin_cfg", rc)
-		}
+	if err := p.setupPolicy(eng, 0, p.policy); err != nil {
+		C.ksim_engine_destroy(eng)
+		return err
 	}
-	if p.policy == C.KSIM_POLICY_PWR {
-		pm := p.powerModel()
-		if rc := C.ksim_engine_set_power_model(eng, 0, &pm); rc != 0 {
-			return fail("set_power_model", rc)
+	if p.companion >= 0 { // replica 1: the same cluster under the companion's score
+		if rc := C.ksim_engine_set_nodes(eng, 1, &cn[0]); rc != 0 {
+			return fail("set_nodes", rc)
+		}
+		if len(ct) > 0 {
+			if rc := C.ksim_engine_set_typical(eng, 1, &ct[0], C.int(len(ct))); rc != 0 {
+				return fail("set_typical", rc)
+			}
+		}
+		if rc := C.ksim_engine_set_policy(eng, 1, p.companion, C.KSIM_GPUSEL_BEST, C.uint64_t(p.cfg.Seed)); rc != 0 {
+			return fail("set_policy", rc)
+		}
+		if err := p.setupPolicy(eng, 1, p.companion); err != nil {
+			C.ksim_engine_destroy(eng)
+			return err
 		}
 	}
 	p.eng, p.names = eng, names
 	for i, n := range names {
 		p.index[n] = i
+	}
+	return nil
+}
+
+// setupPolicy: the per-policy configuration of one engine replica -- DotProduct's GpuPluginCfg
+// (GenerateSchedulingMatchGroups' cfg, utils.go:1274-1342; an empty or unknown method is an error, as
+// the reference panics on it, resource.go:290,377) and PWR's energy model.
+func (p *KsimGpuPlugin) setupPolicy(eng *C.ksim_engine, r C.int, policy C.int) error {
+	if policy == C.KSIM_POLICY_DOTPROD {
+		dim, ok := ksimDimExt[p.cfg.DimExtMethod]
+		if !ok {
+			return fmt.Errorf("ksim: undefined gpu dimension extension method: %q", p.cfg.DimExtMethod)
+		}
+		norm, ok := ksimNorm[p.cfg.NormMethod]
+		if !ok {
+			return fmt.Errorf("ksim: undefined normalization for dot product: %q", p.cfg.NormMethod)
+		}
+		if rc := C.ksim_engine_set_plugin_cfg(eng, r, dim, norm); rc != 0 {
+			return ksimError("set_plugin_cfg", rc)
+		}
+	}
+	if policy == C.KSIM_POLICY_PWR {
+		pm := p.powerModel()
+		if rc := C.ksim_engine_set_power_model(eng, r, &pm); rc != 0 {
+			return ksimError("set_power_model", rc)
+		}
 	}
 	return nil
 }
@@ -472,6 +520,13 @@ func (p *KsimGpuPlugin) PreFilter(ctx context.Context, state *framework.CycleSta
 	p.step++
 	if rc := C.ksim_engine_filter_score(p.eng, 0, &cp, C.int32_t(s.step), &s.feasible[0], &s.score[0], &s.gpuMask[0]); rc != 0 {
 		return framework.AsStatus(ksimError("filter_score", rc))
+	}
+	if p.companion >= 0 {
+		s.score2 = make([]C.int32_t, n)
+		feas2, gpu2 := make([]C.uint8_t, n), make([]C.int32_t, n)
+		if rc := C.ksim_engine_filter_score(p.eng, 1, &cp, C.int32_t(s.step), &feas2[0], &s.score2[0], &gpu2[0]); rc != 0 {
+			return framework.AsStatus(ksimError("filter_score", rc))
+		}
 	}
 	state.Write(ksimStateKey, s)
 	return framework.NewStatus(framework.Success)
@@ -519,6 +574,24 @@ func (p *KsimGpuPlugin) Score(ctx context.Context, state *framework.CycleState, 
 	if !ok {
 		return 0, framework.NewStatus(framework.Error, "ksim: unknown node "+nodeName)
 	}
+	if p.policy == C.KSIM_POLICY_RANDOM {
+		// the reference's draw: RandomScorePlugin.PreScore, which the simulator enables in every profile
+		// (pkg/simulator/utils.go:241-248), picked rand.Intn(len(nodes)) over the framework's feasible list
+		// on Go's global math/rand (random_score.go:42-51); Score gives that node 100
+		// (random_score.go:53-68) -- the same stream, the same draw, nothing drawn twice
+		c, err := state.Read(preScoreStateKey)
+		if err != nil {
+			return 0, framework.AsStatus(fmt.Errorf("reading %q from cycleState: %w", preScoreStateKey, err))
+		}
+		ps, ok := c.(*preScoreState)
+		if !ok {
+			return 0, framework.NewStatus(framework.Error, "ksim: bad RandomScore pre-score state")
+		}
+		if nodeName == ps.nodeName {
+			return framework.MaxNodeScore, framework.NewStatus(framework.Success)
+		}
+		return framework.MinNodeScore, framework.NewStatus(framework.Success)
+	}
 	return int64(s.score[i]), framework.NewStatus(framework.Success)
 }
 
@@ -565,10 +638,28 @@ func (p *KsimGpuPlugin) Reserve(ctx context.Context, state *framework.CycleState
 		if rc := C.ksim_engine_bind(p.eng, 0, &cp, C.int(i), mask); rc != 0 {
 			return framework.AsStatus(ksimError("bind", rc))
 		}
+	} else if p.gpuSel == C.KSIM_GPUSEL_RANDOM && cp.gpu_milli > 0 {
+		// allocateGpuIdBasedOnRandomFit itself (open_gpu_share.go:325-343): its rand.Intn per fitting GPU
+		// on Go's global math/rand, over the node's devices as the engine holds them.  With this selector
+		// Open-Gpu-Share's reserve must be disabled (writeGpuIndex: true) or the stream is drawn twice.
+		m, err := p.randomFitMask(i, pod)
+		if err != nil {
+			return framework.AsStatus(err)
+		}
+		mask = C.int32_t(m)
+		if rc := C.ksim_engine_bind(p.eng, 0, &cp, C.int(i), mask); rc != 0 {
+			return framework.AsStatus(ksimError("bind", rc))
+		}
 	} else if rc := C.ksim_engine_reserve(p.eng, 0, &cp, C.int(i), C.int32_t(step), &mask); rc != 0 {
 		// allocateGpuId returned "": updatePodGpuAnno's error (open_gpu_share.go:242-247)
 		return framework.NewStatus(framework.Error, fmt.Sprintf("failed to allocate gpu to pod(%s) to node(%s)",
 			utils.GeneratePodKey(pod), nodeName))
+	}
+	if p.companion >= 0 { // the companion's replica follows the same Bind
+		if rc := C.ksim_engine_bind(p.eng, 1, &cp, C.int(i), mask); rc != 0 {
+			_ = C.ksim_engine_unreserve(p.eng, 0, &cp, C.int(i), mask)
+			return framework.AsStatus(ksimError("bind", rc))
+		}
 	}
 	p.bound[pod.UID] = ksimBinding{node: i, mask: int32(mask), pod: cp}
 	if p.cfg.WriteGpuIndex && cp.gpu_milli > 0 {
@@ -600,5 +691,108 @@ func (p *KsimGpuPlugin) release(pod *v1.Pod) error {
 	if rc := C.ksim_engine_unreserve(p.eng, 0, &b.pod, C.int(b.node), C.int32_t(b.mask)); rc != 0 {
 		return ksimError("unreserve", rc)
 	}
+	if p.companion >= 0 {
+		if rc := C.ksim_engine_unreserve(p.eng, 1, &b.pod, C.int(b.node), C.int32_t(b.mask)); rc != 0 {
+			return ksimError("unreserve", rc)
+		}
+	}
 	return nil
+}
+
+// randomFitMask: the random GPU selector on node i (caller holds the lock): the reference's own
+// allocateGpuIdBasedOnRandomFit over the node's per-device milli left read back from the engine.
+func (p *KsimGpuPlugin) randomFitMask(i int, pod *v1.Pod) (int32, error) {
+	nodes := make([]C.ksim_node, len(p.names))
+	if rc := C.ksim_engine_get_nodes(p.eng, 0, &nodes[0]); rc != 0 {
+		return 0, ksimError("get_nodes", rc)
+	}
+	n := nodes[i]
+	left := make([]int64, int(n.gpu_count))
+	for g := range left {
+		left[g] = int64(gpushareutils.MILLI) - int64(n.gpu_used_milli[g])
+	}
+	nodeRes := simontype.NodeResource{NodeName: p.names[i], MilliCpuLeft: int64(n.cpu_alloc_milli - n.cpu_used_milli),
+		MilliCpuCapacity: int64(n.cpu_alloc_milli), MilliGpuLeftList: left, GpuNumber: int(n.gpu_count)}
+	id := allocateGpuIdBasedOnRandomFit(nodeRes, utils.GetPodResource(pod), p.cfg.GpuPluginCfg, p.typicalPods)
+	if id == "" {
+		return 0, fmt.Errorf("failed to allocate gpu to pod(%s) to node(%s)", utils.GeneratePodKey(pod), p.names[i])
+	}
+	idl, err := gpushareutils.GpuIdStrToIntList(id)
+	if err != nil {
+		return 0, err
+	}
+	var mask int32
+	for _, g := range idl {
+		mask |= 1 << uint(g)
+	}
+	return mask, nil
+}
+
+// KsimGpuCompanion: the companion score plugin -- the second score of a weighted pair (KsimGpuPluginCfg.
+// Companion), computed by the primary KsimGpu plugin in the same PreFilter batch on the same device
+// state.  Registry entry (simulator.go:153-181):
+//
+//	KsimGpuCompanionName: func(cfg runtime.Object, h framework.Handle) (framework.Plugin, error) {
+//		return simonplugin.NewKsimGpuCompanion(cfg, h)
+//	},
+type KsimGpuCompanion struct {
+	handle framework.Handle
+}
+
+var _ framework.ScorePlugin = &KsimGpuCompanion{}
+var _ framework.ScoreExtensions = &KsimGpuCompanion{}
+
+func NewKsimGpuCompanion(_ runtime.Object, handle framework.Handle) (framework.Plugin, error) {
+	return &KsimGpuCompanion{handle: handle}, nil
+}
+
+func (c *KsimGpuCompanion) Name() string { return KsimGpuCompanionName }
+
+func (c *KsimGpuCompanion) primary() (*KsimGpuPlugin, *framework.Status) {
+	v, ok := ksimPrimaries.Load(c.handle)
+	if !ok {
+		return nil, framework.NewStatus(framework.Error, "ksim: KsimGpuCompanion without a KsimGpu plugin in the profile")
+	}
+	p := v.(*KsimGpuPlugin)
+	if p.companion < 0 {
+		return nil, framework.NewStatus(framework.Error, "ksim: KsimGpu has no companion policy configured")
+	}
+	return p, nil
+}
+
+// Score: the companion policy's score of this node (before its NormalizeScore).
+func (c *KsimGpuCompanion) Score(ctx context.Context, state *framework.CycleState, pod *v1.Pod,
+	nodeName string) (int64, *framework.Status) {
+	p, st := c.primary()
+	if st != nil {
+		return 0, st
+	}
+	s, st := cycleOf(state)
+	if st != nil {
+		return 0, st
+	}
+	i, ok := p.index[nodeName]
+	if !ok || s.score2 == nil {
+		return 0, framework.NewStatus(framework.Error, "ksim: no companion score for node "+nodeName)
+	}
+	return int64(s.score2[i]), framework.NewStatus(framework.Success)
+}
+
+func (c *KsimGpuCompanion) ScoreExtensions() framework.ScoreExtensions { return c }
+
+// NormalizeScore: the companion policy's own (PWR: pwr_score.go:100-141; BestFit: plugin_utils.go:48-74;
+// the others keep their raw scores).
+func (c *KsimGpuCompanion) NormalizeScore(ctx context.Context, state *framework.CycleState, pod *v1.Pod,
+	scores framework.NodeScoreList) *framework.Status {
+	p, st := c.primary()
+	if st != nil {
+		return st
+	}
+	switch p.companion {
+	case C.KSIM_POLICY_PWR:
+		return (&PWRScorePlugin{}).NormalizeScore(ctx, state, pod, scores)
+	case C.KSIM_POLICY_BESTFIT:
+		return NormalizeScore(scores)
+	}
+	return framework.NewStatus(framework.Success)
 }

@@ -255,7 +255,9 @@ int  ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, 
                               uint8_t* feasible, int32_t* score, int32_t* gpu_mask);
 
 /* Reserve + Bind `pod` on `node` (GPU selection by the replica's gpusel) and
- * Unreserve/delete.  *gpu_mask_out receives the devices assigned. */
+ * Unreserve/delete.  *gpu_mask_out receives the devices assigned.  Unreserve returns KSIM_ESTATE,
+ * and changes nothing, when the node does not hold what the pod would release (a device would exceed
+ * 1000 milli or the CPU its allocatable: e.g. the same pod unreserved twice). */
 int  ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t step,
                          int32_t* gpu_mask_out);
 int  ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask);

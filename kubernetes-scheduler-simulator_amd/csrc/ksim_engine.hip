@@ -1412,10 +1412,11 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
   uint16_t* tg = rp.tags + (size_t)node * kTagStride;
   if (sign < 0) {
     // removePod (cache.go:96-111): every released device gets its milli back without exceeding the
-    // device (left + milli <= 1000, the invariant of the packed u16 lanes); else nothing changes
+    // device (left + milli <= 1000, the invariant of the packed u16 lanes) and the CPU stays within
+    // the node's allocatable; else nothing changes (e.g. a second Unreserve of the same pod)
     if (tid == 0) {
       const NodeV n = load_node(nr);
-      bool ok = n.pods_left() < 32767;
+      bool ok = n.pods_left() < 32767 && (long long)n.cpu_left + p.cpu_req <= (long long)rp.cap[node];
       for (int g = 0; g < kMaxGpu; ++g)
         if ((mask_in >> g) & 1) ok = ok && g < n.gpu_cnt() && n.gl(g) + (int)p.milli <= kMilli;
       if (ok) apply_bind(nr, tg, p, mask_in, -1);

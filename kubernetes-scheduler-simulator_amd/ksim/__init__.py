@@ -378,9 +378,12 @@ class Engine:
 
     def set_policy(self, r, policy="FGD", gpusel=None, seed=0, dim_ext=None, norm=None):
         """policy: a POLICY key or a generate_run_scripts.py string such as "PWR 500 FGD 500".
-        DotProd: dim_ext / norm as generate_config_and_run.py's -dimext / -norm (default merge / max,
-        the paper's); like that script, a dim_ext other than merge selects GPUs with the DotProduct
-        selector ("DotProd") unless gpusel says otherwise."""
+        DotProd: dim_ext / norm as generate_config_and_run.py's -dimext / -norm.  The default here is
+        merge / max, the paper sweep's configuration (expected_run_scripts_0511.sh passes -dimext merge);
+        NOTE the reference CLI's own default is -dimext share (generate_config_and_run.py:80), which also
+        switches gpuSelMethod to DotProductScore -- pass dim_ext="share" to get that.  Like that script, a
+        dim_ext other than merge selects GPUs with the DotProduct selector ("DotProd") unless gpusel says
+        otherwise."""
         policy, weights = parse_policy(policy)
         if policy == "DotProd" and dim_ext not in (None, "merge") and gpusel is None:
             gpusel = "DotProd"  # generate_config_and_run.py:271-275

@@ -242,6 +242,13 @@ def test_reserve_unreserve_roundtrip(default_trace):
     eng.unreserve(0, whole, b, m2)
     eng.unreserve(0, share, a, m1)
     assert bytes(eng.nodes(0)) == before
+    # a second Unreserve of the same pod would push the devices past 1000 milli: reported, not applied
+    # (the cgo plugin also forgets a binding once released, go/ksim_gpu.go release)
+    for pod, node, mask in ((whole, b, m2), (share, a, m1)):
+        with pytest.raises(ksim.KsimError) as ei:
+            eng.unreserve(0, pod, node, mask)
+        assert ei.value.code == ksim.KSIM_ESTATE
+    assert bytes(eng.nodes(0)) == before
     eng.close()
 
 
