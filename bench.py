@@ -370,6 +370,9 @@ def main():
         line["config"]["report"] = True
     if args.random_stream == "go":
         line["config"]["random_stream"] = "go"  # Random replicas on Go's math/rand draw structure
+        # the draws are the reference's; the feasible list they index is taken in node order (one filter
+        # worker), while the reference's 16 workers order it by timing: a contract, not reference-equal
+        line["config"]["parity"] = "unpinned (node-order contract, DESIGN.md §4)"
     if args.config == "c4" or args.report:
         line["report_ms_per_step"] = eng.last_report_ms()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":

@@ -1610,6 +1610,8 @@ struct ksim_engine {
   std::vector<int64_t> total_gpus;
   // node-sharded cluster (ksim_engine_set_shard)
   int shard_world = 0;        // 0: not sharded
+  unsigned long long* d_ggran = nullptr;  // a node-sharded group's exchange granules (engine 0 of the group)
+  void* d_hgargs = nullptr;               // its per-shard k_hmemo arguments
   int shard_rank = 0, node_off = 0, n_global = 0;
   ncclComm_t comm = nullptr;  // null: in-process shard group (ksim_shard_group_run) or world 1
   unsigned long long* d_send = nullptr;  // this shard's record {best, nfeas, err, lo|hi}
@@ -1858,7 +1860,8 @@ struct HPlan {
 // Classes of each replica grouped by score request (cpu_nz, milli, num: the candidate states of
 // fgd_score.go:99-149 depend on nothing else), and the distinct initial node states (the keys
 // before the first event depend on the state, the class and the rank only).
-static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int stride, HPlan& pl) {
+static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int stride, HPlan& pl, int forceK = 0,
+                       int forceS = 0) {
   using namespace ksim_hmemo;
   const int Rg = (int)reps.size();
   if (Rg == 0 || e->N > kHRankMax || !score_table()) return false;
@@ -1872,7 +1875,11 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
   pl.K = 1;
   pl.S = e->N;
   pl.nbw = pl.nb;
-  if (!small || (e->run_mode == 5 && e->wgs_req > 1)) {
+  if (forceK > 0) {  // a node-sharded group: every shard's slices alike (the caller checked S, K)
+    pl.S = forceS;
+    pl.K = forceK;
+    pl.nbw = forceS / kFan;
+  } else if (!small || (e->run_mode == 5 && e->wgs_req > 1)) {
     const int want = e->wgs_req > 1 ? e->wgs_req : 64;
     const int S = std::max(kFan, (e->N + want - 1) / want + kFan - 1) / kFan * kFan;
     const int K = (e->N + S - 1) / S;
@@ -1960,12 +1967,12 @@ static int upload_vec(T*& p, size_t& cap, const std::vector<T>& v, hipStream_t s
   return KSIM_OK;
 }
 
-static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev) {
+static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev, int forceK = 0, int forceS = 0) {
   e->hplan_ok = false;
   if (!e->hplan) e->hplan = new HPlan();
   HPlan& pl = *e->hplan;
   const int stride = std::max(max_ev, 1);
-  if (!hmemo_plan(e, reps, stride, pl)) return KSIM_OK;
+  if (!hmemo_plan(e, reps, stride, pl, forceK, forceS)) return KSIM_OK;
   const int Rg = (int)reps.size();
   hipStream_t st = e->stream;
   int rc;
@@ -2202,12 +2209,13 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   return KSIM_OK;
 }
 
-// k_hmemo launch: the initial keys (k_hinit_gk, k_hinit_keys), the replay, the result map.
-static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
+// The initial keys, L1 maxima and feasible counts of k_hmemo's plan (k_hinit_gk, k_hinit_keys); roff: a
+// node-sharded engine's first global rank.
+static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, int roff) {
   using namespace ksim_hmemo;
   const HPlan& pl = *e->hplan;
-  const int stride = std::max(max_ev, 1);
   HInitArgs ia;
+  ia.roff = roff;
   ia.reps = e->d_reps;
   ia.rep_list = e->d_replist + first;
   ia.N = e->N;
@@ -2235,6 +2243,13 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   hipLaunchKernelGGL(k_hinit_keys, dim3((unsigned)((pl.Npad + 255) / 256), (unsigned)pl.Cmax, (unsigned)Rg), dim3(256), 0,
                      st, ia);
   KSIM_HIP(hipGetLastError());
+  return KSIM_OK;
+}
+
+// k_hmemo's arguments for the planned launch (one group of Rg replicas from d_replist + first).
+static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
+  using namespace ksim_hmemo;
+  const HPlan& pl = *e->hplan;
   HMemoArgs ma;
   ma.reps = e->d_reps;
   ma.rep_list = e->d_replist + first;
@@ -2260,6 +2275,20 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   ma.gran = e->d_gran;
   ma.fail = e->d_fail;
   ma.hist = nullptr;
+  ma.roff = 0;
+  ma.wbase = 0;
+  ma.Ktot = pl.K;
+  ma.tp = e->d_tp;
+  return ma;
+}
+
+static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
+  using namespace ksim_hmemo;
+  const HPlan& pl = *e->hplan;
+  const int stride = std::max(max_ev, 1);
+  int irc = hmemo_init_keys(e, Rg, first, st, 0);
+  if (irc) return irc;
+  HMemoArgs ma = hmemo_args(e, first, stride);
   bool any_delete = false;
   for (const int r : e->mplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
   if (pl.K > 1) {
@@ -2493,7 +2522,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -3486,6 +3515,110 @@ int ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, vo
   return KSIM_OK;
 }
 
+// ---- a node-sharded FGD cluster on k_hmemo (one launch for the whole in-process group) ----
+// Every shard engine keeps its own plan, keys, L1 and node records; the launch's workgroups are the
+// shards' slices (K per shard, S ranks each), and each pod step's slice maxima go through ONE exchange of
+// world x K granule columns: selectHost over the union (generic_scheduler.go:187-212), the owner of the
+// winner binds.  Results carry global ranks as the k_step shards' do (ksim/shard.py merge_results).
+static bool hmemo_group_eligible(ksim_engine* const* engines, int world) {
+  const char* v = std::getenv("KSIM_SHARD_HMEMO");
+  if (v && v[0] == '0') return false;
+  if (!score_table()) return false;
+  for (int k = 0; k < world; ++k) {
+    const ksim_engine* e = engines[k];
+    if (e->R != 1 || e->reps[0].policy != POL_FGD || e->report || e->run_mode == 1 || e->run_mode == 2 ||
+        go_random(e, 0))
+      return false;
+  }
+  return true;
+}
+
+// KSIM_OK with *done = false: the group does not fit k_hmemo (the caller keeps the per-pod k_step path).
+static int run_hmemo_group(ksim_engine* const* engines, int world, int max_ev, bool* done) {
+  using namespace ksim_hmemo;
+  *done = false;
+  ksim_engine* e0 = engines[0];
+  const int stride = std::max(max_ev, 1);
+  int nmax = 1;
+  for (int k = 0; k < world; ++k) nmax = std::max(nmax, engines[k]->N);
+  const int want = std::max(1, std::min(64, e0->cus / world));
+  int S = std::max(kFan, (nmax + want - 1) / want + kFan - 1) / kFan * kFan;
+  S = std::min(S, kMaxNb * kFan);
+  const int K = (nmax + S - 1) / S;
+  const int Kt = world * K;
+  if (K < 1 || Kt > 256 || K * S < nmax) return KSIM_OK;
+  std::vector<HMemoArgs> args(world);
+  size_t lds = 0;
+  for (int k = 0; k < world; ++k) {
+    ksim_engine* e = engines[k];
+    const int zero = 0;
+    KSIM_HIP(hipMemcpyAsync(e->d_replist, &zero, sizeof(int), hipMemcpyHostToDevice, e->stream));
+    int rc = prepare_hmemo(e, std::vector<int>{0}, max_ev, K, S);
+    if (rc) return rc;
+    if (!e->hplan_ok) return KSIM_OK;
+    e->mplan_dirty = true;  // the unsharded plan is not this one
+    lds = std::max(lds, e->hplan->lds);
+  }
+  const void* f = Kt <= 64 ? (const void*)k_hmemo_group<1> : (const void*)k_hmemo_group<4>;
+  if (Kt > resident_cap(e0, f, lds)) return KSIM_OK;
+  hipStream_t st = e0->stream;
+  KSIM_HIP(hipSetDevice(e0->device));
+  if (!e0->d_ggran) KSIM_HIP(hipMalloc(&e0->d_ggran, sizeof(unsigned long long) * 2 * 256 * 2));
+  if (!e0->d_hgargs) KSIM_HIP(hipMalloc(&e0->d_hgargs, sizeof(HMemoArgs) * 16));
+  for (int k = 0; k < world; ++k) {
+    ksim_engine* e = engines[k];
+    KSIM_HIP(hipStreamSynchronize(e->stream));
+    KSIM_HIP(hipMemcpyAsync(e->d_nodes, e->d_nodes_init, sizeof(NodeRec) * (size_t)e->N, hipMemcpyDeviceToDevice, st));
+    KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride, hipMemcpyDeviceToDevice, st));
+    KSIM_HIP(hipMemsetAsync(e->d_res[0], 0xff, sizeof(ResultDev) * (size_t)std::max(e->n_events[0], 1), st));
+    int rc = hmemo_init_keys(e, 1, 0, st, e->node_off);
+    if (rc) return rc;
+    HMemoArgs a = hmemo_args(e, 0, stride);
+    a.roff = e->node_off;
+    a.wbase = k * K;
+    a.Ktot = Kt;
+    a.gran = e0->d_ggran;
+    a.fail = e0->d_fail;
+    if (e->has_delete[0]) {
+      rc = ensure_buf(e->d_h_hist, e->h_cap[13], (size_t)K * stride);
+      if (rc) return rc;
+      a.hist = e->d_h_hist;
+    }
+    args[k] = a;
+  }
+  KSIM_HIP(hipMemcpyAsync(e0->d_hgargs, args.data(), sizeof(HMemoArgs) * world, hipMemcpyHostToDevice, st));
+  KSIM_HIP(hipMemsetAsync(e0->d_ggran, 0, sizeof(unsigned long long) * 2 * (size_t)Kt * 2, st));
+  KSIM_HIP(hipMemsetAsync(e0->d_fail, 0, sizeof(int), st));
+  KSIM_HIP(hipStreamSynchronize(st));  // `args` is pageable
+  KSIM_HIP(hipEventRecord(e0->ev0, st));
+  KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const HMemoArgs* ap = reinterpret_cast<const HMemoArgs*>(e0->d_hgargs);
+  int Kk = K;
+  void* params[] = {(void*)&ap, (void*)&Kk};
+  const hipError_t lr = e0->coop ? hipLaunchCooperativeKernel(f, dim3(Kt), dim3(kHBlock), params, (unsigned)lds, st)
+                                 : hipLaunchKernel(f, dim3(Kt), dim3(kHBlock), params, lds, st);
+  if (lr == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    return KSIM_OK;
+  }
+  KSIM_HIP(lr);
+  KSIM_HIP(hipEventRecord(e0->ev1, st));
+  KSIM_HIP(hipStreamSynchronize(st));
+  int fail = 0;
+  KSIM_HIP(hipMemcpy(&fail, e0->d_fail, sizeof(int), hipMemcpyDeviceToHost));
+  if (fail) return KSIM_ESTATE;
+  float ms = 0;
+  KSIM_HIP(hipEventElapsedTime(&ms, e0->ev0, e0->ev1));
+  for (int k = 0; k < world; ++k) {
+    engines[k]->last_ms = ms;
+    engines[k]->last_steps = max_ev;
+    engines[k]->last_K = K;
+    engines[k]->last_hmemo = 1;
+  }
+  *done = true;
+  return KSIM_OK;
+}
+
 int ksim_shard_group_run(ksim_engine* const* engines, int world) {
   if (!engines || world < 1 || world > 16) return KSIM_EINVAL;
   ksim_engine* e0 = engines[0];
@@ -3499,6 +3632,11 @@ int ksim_shard_group_run(ksim_engine* const* engines, int world) {
     max_ev = std::max(max_ev, e->n_events[0]);
   }
   KSIM_HIP(hipSetDevice(e0->device));
+  if (hmemo_group_eligible(engines, world)) {
+    bool done = false;
+    const int rc = run_hmemo_group(engines, world, max_ev, &done);
+    if (rc || done) return rc;
+  }
   if (!e0->d_ptrs) KSIM_HIP(hipMalloc(&e0->d_ptrs, sizeof(unsigned long long*) * 32));
   std::vector<unsigned long long*> ptrs(32, nullptr);
   for (int k = 0; k < world; ++k) {

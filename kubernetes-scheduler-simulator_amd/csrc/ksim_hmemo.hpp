@@ -89,8 +89,14 @@ struct HMemoArgs {
   unsigned long long* prof; // optional [Rg * K][kHProf] (KSIM_PROFILE=1)
   int K, S, nbw;            // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
   unsigned long long* gran; // K > 1: [Rg][2][K][2] exchange granules {tag, value}
-  uint8_t* hist;            // K > 1 with deletes: [Rg][K][stride] 1 bound here, 2 Reserve failed here, 3 no winner
+  uint8_t* hist;            // K > 1 with deletes: [Rg][K][stride] 1 bound here, 2 Reserve failed here, 3 no winner,
+                            // 4 bound in another shard
   int* fail;                // K > 1: a granule poll timed out
+  // Node-sharded cluster (several engines, one per shard, in one exchange): every launch workgroup is
+  // workgroup w of its shard, granule column wbase + w of Ktot; the shard's ranks are global rank - roff
+  // (keys carry the global rank, so selectHost's tie-break spans the shards).  Unsharded: 0, 0, K.
+  int roff, wbase, Ktot;
+  const TypDev* tp;         // the typical tables (k_hmemo_group: per shard; k_hmemo: the kernel argument)
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -209,7 +215,7 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
 // workgroup form (K = 1, the exchange compiled out).  kProf: the KSIM_PROFILE phase timers (compiled
 // out of the lean launches, as k_memo's: the step loop's scalar registers are what it runs short of).
 template <int kSub, bool kProf>
-__global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
+__device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __restrict__ tp_all, const int wg) {
   using namespace ksim_replay;
   using ksim_memo::gget;
   using ksim_memo::gput;
@@ -218,7 +224,10 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   HShared& sh = *reinterpret_cast<HShared*>(smem);
   constexpr int kS = kSub > 0 ? kSub : 1;
   const int K = kSub == 0 ? 1 : a.K;
-  const int gi = (int)blockIdx.x / K, w = (int)blockIdx.x % K;
+  const int Kt = kSub == 0 ? 1 : a.Ktot;  // granule columns of the exchange (every shard's workgroups)
+  const int roff = kSub == 0 ? 0 : a.roff;
+  const bool sharded = Kt > K;
+  const int gi = wg / K, w = wg % K;
   const int r = a.rep_list[gi];
   const ReplicaDev rp = a.reps[r];
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
@@ -245,8 +254,9 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
   const int* evc = a.evc + (size_t)gi * a.stride;
-  unsigned long long* gr = K > 1 ? a.gran + (size_t)gi * 2 * K * 2 : nullptr;
-  uint8_t* hist = (K > 1 && a.hist) ? a.hist + ((size_t)gi * K + w) * a.stride : nullptr;
+  unsigned long long* gr = Kt > 1 ? a.gran + (size_t)gi * 2 * Kt * 2 : nullptr;
+  const int col = (kSub == 0 ? 0 : a.wbase) + w;  // this workgroup's granule column
+  uint8_t* hist = (Kt > 1 && a.hist) ? a.hist + ((size_t)gi * K + w) * a.stride : nullptr;
 
   // ---- start-up: the slice (slot = rank - lo), classes, groups, typical table, score steps, L1, counts
   for (int i = tid; i < ns; i += kHBlock) {
@@ -351,7 +361,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           s_fnew[c] = filter_sum(sn, dn, q) ? 1 : 0;
           s_fold[c] = filter_sum(so, dold, q) ? 1 : 0;
           const unsigned old = s_l1[c * nb + b];
-          const bool fl = old != 0u && hkey_rank(old) == d;
+          const bool fl = old != 0u && hkey_rank(old) == roff + d;
           const unsigned long long fm = __ballot(fl);
           if (fm) {
             int o = 0;
@@ -421,13 +431,13 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           const int g = s_cgrp[c];
           const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
           if (is_share_pod(s_gpod[g])) {
-            k = hkey(0, d, 0);  // feasible with no fitting GPU
+            k = hkey(0, roff + d, 0);  // feasible with no fitting GPU
             for (int i = o + (i0 < 0 ? 0 : i0); i < oe; i += (i0 < 0 ? 1 : 64)) {  // i0 < 0: all, serially
-              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), d, 15 - (s_code[i] - 1));
+              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), roff + d, 15 - (s_code[i] - 1));
               k = x > k ? x : k;
             }
           } else if (i0 <= 0) {
-            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), d, 0);  // NodeResource.Sub state
+            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), roff + d, 0);  // NodeResource.Sub state
           }
         }
         return k;
@@ -439,7 +449,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         unsigned* l = &s_l1[c * nb + b];
         const unsigned old = *l;
         if (k > old) *l = k;
-        else if (old != 0u && hkey_rank(old) == d) *l = k > s_bx[c] ? k : s_bx[c];
+        else if (old != 0u && hkey_rank(old) == roff + d) *l = k > s_bx[c] ? k : s_bx[c];
       };
       if (wv != 0) {
         for (int c = tid - 64; c < C; c += kHBlock - 64) {
@@ -469,20 +479,20 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         const unsigned lv = lane < nb ? s_l1[cs * nb + lane] : 0u;
         unsigned W = (unsigned)wave_max_dpp((int)lv);
         int nfeas = __builtin_amdgcn_readfirstlane(s_cnt[cs]);
-        if (K > 1) {
+        if (Kt > 1) {
           // the slices' maxima and feasible counts: granules {tag, key}, {tag, count} (k_replay's exchange)
-          unsigned long long* slot = gr + (size_t)(seq & 1) * K * 2;
+          unsigned long long* slot = gr + (size_t)(seq & 1) * Kt * 2;
           const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
           if (lane == 0) {
-            ksim_replay::gstore(slot + (size_t)w * 2 + 0, tag | W);
-            ksim_replay::gstore(slot + (size_t)w * 2 + 1, tag | (unsigned)nfeas);
+            ksim_replay::gstore(slot + (size_t)col * 2 + 0, tag | W);
+            ksim_replay::gstore(slot + (size_t)col * 2 + 1, tag | (unsigned)nfeas);
           }
           unsigned long long x0[kS], x1[kS];
           auto load = [&]() {
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
               const int k = lane + 64 * j;
-              if (k < K) {
+              if (k < Kt) {
                 x0[j] = ksim_replay::gload(slot + (size_t)k * 2 + 0);
                 x1[j] = ksim_replay::gload(slot + (size_t)k * 2 + 1);
               }
@@ -492,7 +502,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
             bool ok = true;
 #pragma unroll
             for (int j = 0; j < kS; ++j)
-              ok = ok && (lane + 64 * j >= K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
+              ok = ok && (lane + 64 * j >= Kt || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
             return ok;
           };
           load();
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
           int c = 0;
 #pragma unroll
           for (int j = 0; j < kS; ++j) {
-            if (lane + 64 * j < K) {
+            if (lane + 64 * j < Kt) {
               const unsigned kj = (unsigned)(x0[j] & 0xffffffffull);
               m = kj > m ? kj : m;
               c += (int)(unsigned)(x1[j] & 0xffffffffull);
@@ -523,8 +533,17 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
         write = W == 0u && w == 0;  // nobody feasible: workgroup 0 reports
         uint8_t h = 3;
         if (W != 0u) {
-          const int wr = hkey_rank(W);
+          const int wr = hkey_rank(W) - roff;  // the winner's rank in this shard
           h = 0;
+          if (sharded && (wr < 0 || wr >= N)) {
+            // the winner is in another shard (history 4): this shard's first workgroup writes a provisional
+            // record naming it (the owner's record is authoritative; ksim/shard.py merge_results)
+            h = 4;
+            if (w == 0) {
+              out = ResultDev{wr + roff, 0, result_score(rp, nfeas, hkey_score(W), 0, 0), nfeas, ST_OK};
+              write = true;
+            }
+          }
           if (wr >= lo && wr < lo + ns) {  // the winner is in this slice
             const NodeV wn = uniform_node(&s_nodes[wr - lo]);
             mask = select_gpus(wn, p, rp.gpusel, hkey_gpu(W), rp.seed, step);
@@ -535,7 +554,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
             } else {
               out.status = ST_OK;
               out.score = result_score(rp, nfeas, hkey_score(W), 0, 0);
-              out.node = wr;  // name rank; k_memo_finish maps it to the node index
+              out.node = wr + roff;  // name rank (global); k_memo_finish maps it to the node index
               out.gpu_mask = mask;
               rk = wr;
               before = wn;
@@ -549,10 +568,12 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
       } else if (p.ref >= 0 && p.ref < step) {
         // simulator.go:416-422 deletePod: undo the creation's Bind (its result holds the rank and mask);
         // with K > 1 only the workgroup that bound it (its own history) reads that result
+        // (every value read here was written by this workgroup: a record another workgroup -- possibly on
+        // another XCD, another L2 -- wrote is never read back)
         const int hh = hist ? (int)hist[p.ref] : 1;
         if (hh == 1) {
           const ResultDev cr = gget(rp.res + p.ref);
-          const int crk = __builtin_amdgcn_readfirstlane(cr.node);
+          const int crk = __builtin_amdgcn_readfirstlane(cr.node) - roff;
           const int cst = __builtin_amdgcn_readfirstlane(cr.status);
           const int cmask = __builtin_amdgcn_readfirstlane(cr.gpu_mask);
           if (crk >= 0 && cst == ST_OK) {
@@ -561,11 +582,16 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
             before = uniform_node(&s_nodes[rk - lo]);
             after = before;
             bind_node(after, bp, cmask, -1);
-            out = ResultDev{rk, cmask, 0, 0, ST_DELETED};
+            out = ResultDev{rk + roff, cmask, 0, 0, ST_DELETED};
           }
           write = true;
         } else {
           write = hh == 2 || (hh == 3 && w == 0);
+          if (hh == 4 && w == 0) {  // bound in another shard: name it, from this workgroup's own record
+            const ResultDev cr = gget(rp.res + p.ref);
+            out = ResultDev{__builtin_amdgcn_readfirstlane(cr.node), 0, 0, 0, ST_DELETED};
+            write = true;
+          }
         }
         if (hist && lane == 0) hist[step] = 0;
       } else {
@@ -592,7 +618,7 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
     }
     __syncthreads();
     mark(5);
-    if (K > 1 && sh.stop) break;
+    if (Kt > 1 && sh.stop) break;
   }
   if (prof && tid == 0) {
     sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
@@ -602,6 +628,19 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
   if (prof && tid < kHProf) a.prof[(size_t)blockIdx.x * kHProf + tid] = sh.prof[tid];
   // final cluster state
   for (int i = tid; i < ns; i += kHBlock) store_node(rp.nodes + rank2idx[lo + i], load_node(&s_nodes[i]));
+}
+
+template <int kSub, bool kProf>
+__global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
+  hmemo_body<kSub, kProf>(a, tp_all, (int)blockIdx.x);
+}
+
+// One launch over the shards of a node-sharded cluster on one device (ksim_shard_group_run): workgroup
+// blockIdx.x is workgroup blockIdx.x % K of shard blockIdx.x / K, with that shard engine's arguments.
+template <int kSub>
+__global__ __launch_bounds__(kHBlock) void k_hmemo_group(const HMemoArgs* __restrict__ sa, int K) {
+  const HMemoArgs a = sa[blockIdx.x / K];
+  hmemo_body<kSub, false>(a, a.tp, (int)blockIdx.x % K);
 }
 
 // ---------------------------------------------------------------------------
@@ -618,6 +657,7 @@ struct HInitArgs {
   const PodDev* cls;       // [Rg][Cmax]
   const uint16_t* cgrp;    // [Rg][Cmax]
   const PodDev* gpod;      // [Rg][Gmax]
+  int roff;                // node-sharded: the shard's first global rank (keys carry global ranks)
   const NodeRec* st;       // [Rg][Smax] distinct initial node states
   const int* ns;           // [Rg] distinct states
   const int* nstate;       // [Rg][Npad] state of each rank (-1 padding)
@@ -665,7 +705,7 @@ __global__ __launch_bounds__(256) void k_hinit_keys(HInitArgs a) {
     const PodDev q = a.cls[(size_t)gi * a.Cmax + c];
     if (filter_node(n, q)) {
       const int g = a.cgrp[(size_t)gi * a.Cmax + c];
-      k = a.gsc[((size_t)gi * a.Gmax + g) * a.Smax + s] | hkey_rankbits(rank);
+      k = a.gsc[((size_t)gi * a.Gmax + g) * a.Smax + s] | hkey_rankbits(a.roff + rank);
     }
   }
   a.keys[((size_t)gi * a.Cmax + c) * a.Npad + rank] = k;

@@ -35,20 +35,29 @@ def main():
            "wgs": e.last_run_wgs(), "device_ms": ms1, "us_per_pod": ms1 * 1e3 / a.events}, "groups": []}
     e.close()
     for w in a.worlds:
-        g = SH.ShardGroup(rp.nodes, (arr, n), w)
-        g.load_events(rp.events, a.events)
-        g.run()
-        t0 = time.perf_counter()
-        ms = g.run()
-        wall = time.perf_counter() - t0
-        same = g.results() == want
-        g.close()
-        out["groups"].append({"world": w, "device_ms": ms, "us_per_pod": ms * 1e3 / a.events,
-                              "wall_us_per_pod": wall * 1e6 / a.events, "results_equal_unsharded": same})
-        print("world %d: %.2f us/pod, equal %s" % (w, ms * 1e3 / a.events, same), file=sys.stderr, flush=True)
-    out["note"] = ("in-process shard group: every shard's Filter+Score (k_step mode 2) and the record exchange "
-                   "as a gather kernel on one device; the RCCL all-gather across processes stays unmeasured on a "
-                   "1-GPU lease")
+        for mode in ("hmemo", "step"):
+            # hmemo: one k_hmemo launch over every shard's slices, one granule exchange per pod (the default);
+            # step: KSIM_SHARD_HMEMO=0, the per-pod k_step + gather + commit launches (round 2's path)
+            os.environ["KSIM_SHARD_HMEMO"] = "1" if mode == "hmemo" else "0"
+            g = SH.ShardGroup(rp.nodes, (arr, n), w)
+            g.load_events(rp.events, a.events)
+            g.run()
+            t0 = time.perf_counter()
+            ms = g.run()
+            wall = time.perf_counter() - t0
+            same = g.results() == want
+            wgs = g.engines[0].last_run_wgs()
+            g.close()
+            out["groups"].append({"world": w, "mode": mode, "wgs_per_shard": wgs, "device_ms": ms,
+                                  "us_per_pod": ms * 1e3 / a.events, "wall_us_per_pod": wall * 1e6 / a.events,
+                                  "results_equal_unsharded": same})
+            print("world %d %s: %.2f us/pod, equal %s" % (w, mode, ms * 1e3 / a.events, same), file=sys.stderr,
+                  flush=True)
+    os.environ.pop("KSIM_SHARD_HMEMO", None)
+    out["note"] = ("in-process shard group on one device. hmemo: every shard's k_hmemo slices in one launch, the "
+                   "pod step's slice maxima exchanged as world x K granules (no host, no collective per pod); "
+                   "step: per pod every shard's Filter+Score (k_step mode 2), a gather kernel and the commit. The "
+                   "cross-process exchange (one process per GPU) stays unmeasured on a 1-GPU lease")
     print(json.dumps(out))
 
 

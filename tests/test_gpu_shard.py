@@ -46,7 +46,25 @@ def test_group_fgd_equals_unsharded(default_trace, world):
     g.load_events(rp.events, n_ev)
     g.run()
     got = g.results()
+    wgs = g.engines[0].last_run_wgs()
     g.close()
+    assert wgs >= 1  # the FGD group ran on k_hmemo's sharded launch (K slices per shard)
+    assert got == unsharded(default_trace, rp.nodes, rp.events, n_ev, "FGD")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_fgd_step_path_still_equal(default_trace, world, monkeypatch):
+    # KSIM_SHARD_HMEMO=0 keeps round 2's per-pod k_step + gather + commit path for an FGD group
+    monkeypatch.setenv("KSIM_SHARD_HMEMO", "0")
+    rp = default_trace.replay(seed=43)
+    n_ev = 600
+    g = SH.ShardGroup(rp.nodes, default_trace.typical(), world)
+    g.load_events(rp.events, n_ev)
+    g.run()
+    got = g.results()
+    wgs = g.engines[0].last_run_wgs()
+    g.close()
+    assert wgs == 0
     assert got == unsharded(default_trace, rp.nodes, rp.events, n_ev, "FGD")
 
 
