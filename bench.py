@@ -59,11 +59,15 @@ def profile_key(args):
     return k
 
 
+def profile_file(key):
+    """The newest round's counter summary of a bench configuration (PROF_DIRS order), or None."""
+    return next((f for f in (os.path.join(d, key, "pmc.json") for d in PROF_DIRS) if os.path.exists(f)), None)
+
+
 def profile_rooflines(args, kernel):
     """(traffic, traffic_source, valu) from this configuration's counter passes, if it was profiled and
     the profiled dominant kernel is the one this run launched."""
-    pf = next((f for f in (os.path.join(d, profile_key(args), "pmc.json") for d in PROF_DIRS) if os.path.exists(f)),
-              None)
+    pf = profile_file(profile_key(args))
     if pf is None:
         return None, None, None
     with open(pf) as f:
@@ -240,8 +244,17 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        ndev = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
+        if args.sharded and ndev < world:
+            # shard processes sharing a device (a 1-GPU box rehearsing the multi-process sharded mode): the
+            # data path is the device exchange, the launcher's own barrier / reductions go over gloo (RCCL
+            # refuses two ranks on one device)
+            local = local % max(ndev, 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
     import torch
 
     if world == 1:
@@ -279,6 +292,7 @@ def main():
         eng.run()
 
     def barrier():
+        torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -290,7 +304,8 @@ def main():
         dev_ms += eng.run()
     barrier()
     dt = time.perf_counter() - t0
-    dt, job_events = reduce_job(dt, total_events * args.steps, dist, "cuda")
+    dt, job_events = reduce_job(dt, total_events * args.steps, dist,
+                                "cpu" if dist is not None and dist.get_backend() == "gloo" else "cuda")
     if args.sharded:
         job_events = total_events * args.steps  # one cluster: every rank processed the same events
 
@@ -356,7 +371,8 @@ def main():
     if args.config == "c5" and args.sharded:
         line["scaling"] = "strong"
         line["config"] = {"workload": "C5: synthetic 100000 nodes x 1000000 pods, FGD, ONE cluster node-sharded "
-                                      "over %d GPU(s), RCCL all-gather of a 32-B record per pod" % world,
+                                      "over %d shard process(es), k_hmemo slices with a device-to-device granule "
+                                      "exchange per pod (IPC-mapped buffers, no collective)" % world,
                           "replicas_per_gpu": 1, "events_per_gpu": total_events,
                           "parallelism": "nodeshard%d" % world}
         line["data"] = "synthetic (SURVEY §8(d) C5): nodes and pods drawn i.i.d. from the openb default trace"
@@ -387,17 +403,20 @@ def main():
 
 
 def _sharded_engine(device, rank, world, trace, dist):
-    """This rank's shard of the one C5 cluster (ksim.shard; RCCL id made on rank 0)."""
+    """This rank's shard of the one C5 cluster (ksim.shard): FGD shards exchange each pod step's slice maxima
+    device to device through IPC-mapped buffers (ksim_engine_set_shard_peers; the handles go over `dist`)."""
     import ksim.shard as SH
     rp = trace.replay(seed=1, tune_ratio=0.0, shuffle=False)
     parts = SH.partition(rp.nodes, world)
     off, local, idx = parts[rank]
-    box = [ksim.shard_comm_id() if rank == 0 else None]
-    if dist is not None:
-        dist.broadcast_object_list(box, src=0)
     arr, n = trace.typical()
     eng = ksim.Engine(len(idx), 1, device=device)
-    eng.set_shard(rank, world, off, trace.num_nodes, box[0])
+    eng.set_shard(rank, world, off, trace.num_nodes, None)
+    handles = [eng.shard_peer_handle()]
+    if dist is not None:
+        handles = [None] * world
+        dist.all_gather_object(handles, eng.shard_peer_handle())
+    eng.set_shard_peers(handles)
     eng.set_nodes(0, local)
     eng.set_typical(0, arr, n)
     eng.set_policy(0, "FGD")

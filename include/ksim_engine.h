@@ -314,6 +314,17 @@ int  ksim_engine_set_shard(ksim_engine* e, int rank, int world, int node_offset,
                            const uint8_t* comm_id);
 int  ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, void* user);
 int  ksim_shard_group_run(ksim_engine* const* engines, int world);
+/* Device-initiated exchange between shard processes (one process per GPU; FGD shards): no host step and no
+ * collective per pod.  ksim_shard_peer_handle allocates this shard's exchange buffer (after set_shard, without
+ * comm_id or a host exchange) and returns its IPC handle; every rank gathers the `world` handles in rank order
+ * (e.g. torch.distributed all_gather_object) and passes them to ksim_engine_set_shard_peers, which maps the
+ * peers' buffers (its own handle must sit at its rank: KSIM_EINVAL otherwise).  ksim_engine_run then replays
+ * the shard's slices on k_hmemo and, per pod step, stores its slice maxima straight into every peer's buffer
+ * (xGMI) and polls its own: selectHost over the union, the owner of the winner binds (results as above).
+ * Every rank must run the same runs.  Other policies, the report or a plan that does not fit: KSIM_ENOTSUP. */
+#define KSIM_SHARD_HANDLE_BYTES 64
+int  ksim_shard_peer_handle(ksim_engine* e, uint8_t* out /* KSIM_SHARD_HANDLE_BYTES */);
+int  ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles /* world * KSIM_SHARD_HANDLE_BYTES */);
 
 /* Measurement.  Restarts from the set_nodes state and runs the first `n_steps`
  * pod steps of every replica as eager launches with an event pair around every

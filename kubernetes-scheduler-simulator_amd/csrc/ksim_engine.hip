@@ -1612,6 +1612,13 @@ struct ksim_engine {
   int shard_world = 0;        // 0: not sharded
   unsigned long long* d_ggran = nullptr;  // a node-sharded group's exchange granules (engine 0 of the group)
   void* d_hgargs = nullptr;               // its per-shard k_hmemo arguments
+  // one shard per process (ksim_shard_peer_handle / ksim_engine_set_shard_peers): this shard's exchange
+  // buffer (uncached device memory, exported by IPC), the peers' buffers mapped here, the run epoch
+  unsigned long long* d_pgran = nullptr;
+  std::vector<uint8_t> pgran_handle;      // the handle ksim_shard_peer_handle returned (exports differ per call)
+  std::vector<unsigned long long*> peers;
+  std::vector<char> peer_opened;
+  int peer_epoch = 0;
   int shard_rank = 0, node_off = 0, n_global = 0;
   ncclComm_t comm = nullptr;  // null: in-process shard group (ksim_shard_group_run) or world 1
   unsigned long long* d_send = nullptr;  // this shard's record {best, nfeas, err, lo|hi}
@@ -1649,6 +1656,7 @@ static int upload_reps(ksim_engine* e) {
 // CUs the engine may use: the occupancy query times the CU count.  A persistent grid whose workgroups
 // exchange granules (K > 1) must not exceed it.
 static int resident_cap(const ksim_engine* e, const void* f, size_t lds);
+static int run_hmemo_peer(ksim_engine* e, int max_ev);
 
 // A persistent launch: K > 1 workgroups per replica poll each other's granules every step, so the
 // whole grid must be resident -- a cooperative launch, which the runtime refuses up front
@@ -2279,6 +2287,9 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   ma.wbase = 0;
   ma.Ktot = pl.K;
   ma.tp = e->d_tp;
+  ma.npeer = 0;
+  ma.epoch = 0;
+  for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }
 
@@ -2533,6 +2544,9 @@ void ksim_engine_destroy(ksim_engine* e) {
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
   if (e->comm) destroy_comm(e->comm);
+  for (size_t q = 0; q < e->peers.size(); ++q)
+    if (e->peer_opened[q]) (void)hipIpcCloseMemHandle(e->peers[q]);
+  if (e->d_pgran) (void)hipFree(e->d_pgran);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e->mplan;
   delete e->hplan;
@@ -3437,7 +3451,8 @@ int ksim_engine_run(ksim_engine* e) {
     if (go_random(e, r) && (step_path || e->shard_world > 0 ||
                             (e->reps[r].gpusel != SEL_BEST && e->reps[r].gpusel != SEL_WORST && e->reps[r].gpusel != SEL_RANDOM)))
       return KSIM_ENOTSUP;
-  if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
+  if (e->shard_world > 0 && !e->peers.empty()) rc = run_hmemo_peer(e, max_ev);
+  else if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
   else rc = step_path ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
@@ -3512,6 +3527,131 @@ int ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, vo
   e->xuser = user;
   e->h_send.assign(4, 0);
   e->h_recv.assign(4 * (size_t)e->shard_world, 0);
+  return KSIM_OK;
+}
+
+// ---- one shard per process: device-initiated exchange through IPC-mapped granule buffers ----
+constexpr size_t kPeerGranBytes = sizeof(unsigned long long) * 2 * 256 * 2;  // 2 slots x 256 columns x 2
+
+int ksim_shard_peer_handle(ksim_engine* e, uint8_t* out) {
+  if (!e || !out) return KSIM_EINVAL;
+  if (e->shard_world < 1 || e->comm || e->xfn) return KSIM_ESTATE;
+  KSIM_HIP(hipSetDevice(e->device));
+  if (!e->d_pgran) {
+    // uncached device memory: the peers' stores land in it over xGMI and the local polls read it there
+    KSIM_HIP(hipExtMallocWithFlags((void**)&e->d_pgran, kPeerGranBytes, hipDeviceMallocUncached));
+    KSIM_HIP(hipMemset(e->d_pgran, 0, kPeerGranBytes));
+  }
+  if (e->pgran_handle.empty()) {
+    hipIpcMemHandle_t h;
+    KSIM_HIP(hipIpcGetMemHandle(&h, e->d_pgran));
+    static_assert(sizeof(hipIpcMemHandle_t) <= KSIM_SHARD_HANDLE_BYTES, "IPC handle size");
+    e->pgran_handle.assign(KSIM_SHARD_HANDLE_BYTES, 0);
+    std::memcpy(e->pgran_handle.data(), &h, sizeof h);
+  }
+  std::memcpy(out, e->pgran_handle.data(), KSIM_SHARD_HANDLE_BYTES);
+  return KSIM_OK;
+}
+
+int ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles) {
+  if (!e || !handles) return KSIM_EINVAL;
+  if (e->shard_world < 1 || !e->d_pgran || e->pgran_handle.empty() || !e->peers.empty()) return KSIM_ESTATE;
+  KSIM_HIP(hipSetDevice(e->device));
+  const int world = e->shard_world;
+  e->peers.assign(world, nullptr);
+  e->peer_opened.assign(world, 0);
+  if (e->pgran_handle.empty() ||
+      std::memcmp(handles + (size_t)e->shard_rank * KSIM_SHARD_HANDLE_BYTES, e->pgran_handle.data(),
+                  KSIM_SHARD_HANDLE_BYTES) != 0) {
+    e->peers.clear();
+    return KSIM_EINVAL;  // this shard's own handle must sit at its rank
+  }
+  for (int q = 0; q < world; ++q) {
+    if (q == e->shard_rank) {
+      e->peers[q] = e->d_pgran;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles + (size_t)q * KSIM_SHARD_HANDLE_BYTES, sizeof h);
+    void* p = nullptr;
+    const hipError_t r = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (r != hipSuccess) {
+      std::fprintf(stderr, "ksim: hipIpcOpenMemHandle (shard %d): %s\n", q, hipGetErrorString(r));
+      (void)hipGetLastError();
+      for (int k = 0; k < q; ++k)
+        if (e->peer_opened[k]) (void)hipIpcCloseMemHandle(e->peers[k]);
+      e->peers.clear();
+      e->peer_opened.clear();
+      return KSIM_EHIP;
+    }
+    e->peers[q] = reinterpret_cast<unsigned long long*>(p);
+    e->peer_opened[q] = 1;
+  }
+  return KSIM_OK;
+}
+
+// ksim_engine_run of a shard with peers: k_hmemo over this shard's slices, the exchange spanning every
+// shard's workgroups (K per shard, the same K and S on every rank: from n_global and world only).
+static int run_hmemo_peer(ksim_engine* e, int max_ev) {
+  using namespace ksim_hmemo;
+  if (e->R != 1 || e->reps[0].policy != POL_FGD || e->report || go_random(e, 0) || !score_table())
+    return KSIM_ENOTSUP;
+  const int world = e->shard_world;
+  const int nmax = (e->n_global + world - 1) / world;
+  int K = std::max(1, 64 / world);
+  int S = std::max(kFan, (nmax + K - 1) / K + kFan - 1) / kFan * kFan;
+  if (S > kMaxNb * kFan) {
+    S = kMaxNb * kFan;
+    K = (nmax + S - 1) / S;
+  }
+  const int Kt = world * K;
+  if (Kt > 256 || e->N > K * S) return KSIM_ENOTSUP;
+  const int stride = std::max(max_ev, 1);
+  hipStream_t st = e->stream;
+  const int zero = 0;
+  KSIM_HIP(hipMemcpyAsync(e->d_replist, &zero, sizeof(int), hipMemcpyHostToDevice, st));
+  int rc = prepare_hmemo(e, std::vector<int>{0}, max_ev, K, S);
+  if (rc) return rc;
+  if (!e->hplan_ok) return KSIM_ENOTSUP;
+  e->mplan_dirty = true;
+  KSIM_HIP(hipMemcpyAsync(e->d_nodes, e->d_nodes_init, sizeof(NodeRec) * (size_t)e->N, hipMemcpyDeviceToDevice, st));
+  KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride, hipMemcpyDeviceToDevice, st));
+  KSIM_HIP(hipMemsetAsync(e->d_res[0], 0xff, sizeof(ResultDev) * (size_t)stride, st));
+  if ((rc = hmemo_init_keys(e, 1, 0, st, e->node_off))) return rc;
+  HMemoArgs a = hmemo_args(e, 0, stride);
+  a.roff = e->node_off;
+  a.wbase = e->shard_rank * K;
+  a.Ktot = Kt;
+  a.gran = e->d_pgran;
+  a.npeer = world;
+  e->peer_epoch = (e->peer_epoch + 1) & 0xff;  // every rank runs the same runs: the same epoch
+  if (e->peer_epoch == 0) e->peer_epoch = 1;
+  a.epoch = e->peer_epoch;
+  for (int q = 0; q < world; ++q) a.peer[q] = e->peers[q];
+  if (e->has_delete[0]) {
+    if ((rc = ensure_buf(e->d_h_hist, e->h_cap[13], (size_t)K * stride))) return rc;
+    a.hist = e->d_h_hist;
+  }
+  KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), st));
+  const void* f = Kt <= 64 ? (const void*)k_hmemo<1, false> : (const void*)k_hmemo<4, false>;
+  if (K > resident_cap(e, f, e->hplan->lds)) return KSIM_ERANGE;
+  KSIM_HIP(hipEventRecord(e->ev0, st));
+  const TypDev* tpp = e->d_tp;
+  // a plain launch: K <= 64 one-per-CU workgroups are resident (checked above), and a cooperative launch
+  // takes the device's one global-wave-sync resource, which a second shard process on the same device
+  // would wait for behind the first's persistent kernel
+  if ((rc = launch_persistent(f, K, kHBlock, e->hplan->lds, st, false, a, tpp))) return rc;
+  KSIM_HIP(hipEventRecord(e->ev1, st));
+  KSIM_HIP(hipStreamSynchronize(st));
+  int fail = 0;
+  KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
+  if (fail) return KSIM_ESTATE;
+  float ms = 0;
+  KSIM_HIP(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+  e->last_ms = ms;
+  e->last_steps = max_ev;
+  e->last_K = K;
+  e->last_hmemo = 1;
   return KSIM_OK;
 }
 

@@ -52,6 +52,7 @@ constexpr int kMaxGroups = 128;
 constexpr int kMaxItems = 1 + 8 * kMaxGroups;
 constexpr int kEvBuf = 128;
 constexpr int kQuarters = kHBlock / 16;
+constexpr int kMaxPeers = 16;  // shard processes of a device exchange (ksim_engine_set_shard: world <= 16)
 
 // Packed key of (class, node): [30:24] score + 1 | [23:4] kHRankMax - rank | [3:0] gpu field
 // (15 - g for a share pod placed on GPU g, 0 otherwise).  0 = infeasible.  Max key = max score,
@@ -97,6 +98,13 @@ struct HMemoArgs {
   // (keys carry the global rank, so selectHost's tie-break spans the shards).  Unsharded: 0, 0, K.
   int roff, wbase, Ktot;
   const TypDev* tp;         // the typical tables (k_hmemo_group: per shard; k_hmemo: the kernel argument)
+  // One shard per process / GPU (ksim_engine_set_shard_peers): `gran` is this shard's own exchange buffer
+  // (uncached device memory), peer[q] shard q's buffer mapped here (IPC; own included); each step's
+  // granules are stored into every peer's buffer (system scope, over xGMI) and polled in the own one.
+  // epoch tags a run's granules (no reset between runs, so no rank can clear a granule a peer already
+  // wrote).  npeer = 0: the exchange buffer is shared in place (one launch).
+  int npeer, epoch;
+  unsigned long long* peer[kMaxPeers];
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -481,9 +489,18 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         int nfeas = __builtin_amdgcn_readfirstlane(s_cnt[cs]);
         if (Kt > 1) {
           // the slices' maxima and feasible counts: granules {tag, key}, {tag, count} (k_replay's exchange)
-          unsigned long long* slot = gr + (size_t)(seq & 1) * Kt * 2;
-          const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-          if (lane == 0) {
+          const size_t so = (size_t)(seq & 1) * Kt * 2;
+          unsigned long long* slot = gr + so;
+          const unsigned long long tag =
+              (unsigned long long)(((unsigned)a.epoch << 24) | ((unsigned)(seq + 1) & 0xffffffu)) << 32;
+          const int np = a.npeer;
+          if (np > 0) {  // lane q -> shard q's buffer
+            if (lane < np) {
+              unsigned long long* ps = a.peer[lane] + so + (size_t)col * 2;
+              __hip_atomic_store(ps, tag | W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(ps + 1, tag | (unsigned)nfeas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          } else if (lane == 0) {
             ksim_replay::gstore(slot + (size_t)col * 2 + 0, tag | W);
             ksim_replay::gstore(slot + (size_t)col * 2 + 1, tag | (unsigned)nfeas);
           }
@@ -493,8 +510,13 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
             for (int j = 0; j < kS; ++j) {
               const int k = lane + 64 * j;
               if (k < Kt) {
-                x0[j] = ksim_replay::gload(slot + (size_t)k * 2 + 0);
-                x1[j] = ksim_replay::gload(slot + (size_t)k * 2 + 1);
+                if (np > 0) {
+                  x0[j] = __hip_atomic_load(slot + (size_t)k * 2 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  x1[j] = __hip_atomic_load(slot + (size_t)k * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                } else {
+                  x0[j] = ksim_replay::gload(slot + (size_t)k * 2 + 0);
+                  x1[j] = ksim_replay::gload(slot + (size_t)k * 2 + 1);
+                }
               }
             }
           };

@@ -169,6 +169,8 @@ SIGNATURES = {
     "ksim_shard_comm_id": (C.c_int, [_P(C.c_uint8)]),
     "ksim_engine_set_shard": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_int, _P(C.c_uint8)]),
     "ksim_shard_group_run": (C.c_int, [_P(_VP), C.c_int]),
+    "ksim_shard_peer_handle": (C.c_int, [_VP, _P(C.c_uint8)]),
+    "ksim_engine_set_shard_peers": (C.c_int, [_VP, _P(C.c_uint8)]),
     "ksim_engine_set_shard_exchange": (C.c_int, [_VP, C.c_void_p, C.c_void_p]),
     "ksim_engine_set_plugin_cfg": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int]),
     "ksim_trace_load_openb": (C.c_int, [C.c_char_p, C.c_char_p, _P(_VP)]),
@@ -475,6 +477,18 @@ class Engine:
         check(lib().ksim_engine_set_shard(self.h, rank, world, node_offset, n_global, cid), "set_shard")
         self._shard = (rank, world)
 
+    def shard_peer_handle(self):
+        """This shard's exchange buffer as an IPC handle (bytes; ksim_shard_peer_handle)."""
+        buf = (C.c_uint8 * SHARD_HANDLE_BYTES)()
+        check(lib().ksim_shard_peer_handle(self.h, buf), "shard_peer_handle")
+        return bytes(buf)
+
+    def set_shard_peers(self, handles):
+        """Map every shard's exchange buffer (handles: the ranks' shard_peer_handle() in rank order)."""
+        blob = b"".join(handles)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(lib().ksim_engine_set_shard_peers(self.h, buf), "set_shard_peers")
+
     def set_go_stream(self, r, state):
         """Random on Go's math/rand stream (ksim_engine_set_go_stream) from state = (vec[607], tap,
         feed[, ...]) as Trace.go_state returns it; None restores the hash contract."""
@@ -579,6 +593,7 @@ class Engine:
 
 
 SHARD_ID_BYTES = 128
+SHARD_HANDLE_BYTES = 64
 # ksim_shard_exchange_fn
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p)
 

@@ -102,6 +102,8 @@ def run_distributed(nodes, typical, events, n, dist, policy="FGD", seed=0, devic
     `device`, replays the events, and the per-shard results are gathered and merged on every rank.
     exchange="host": no RCCL communicator; every pod step's record goes through `dist` (host_gather),
     e.g. shards sharing one GPU, or hosts without a common RCCL fabric.
+    exchange="device" (FGD): each shard's persistent k_hmemo stores its per-step slice maxima straight into
+    every peer's IPC-mapped exchange buffer (ksim_engine_set_shard_peers); `dist` only carries the handles.
     Returns (merged results, device ms of this rank's run)."""
     engine_cls = engine_cls or ksim.Engine
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -110,14 +112,18 @@ def run_distributed(nodes, typical, events, n, dist, policy="FGD", seed=0, devic
     if exchange == "rccl":
         box = [shard_comm_id_for(engine_cls) if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-    elif exchange == "host":
+    elif exchange in ("host", "device"):
         box = [None]
     else:
-        raise ValueError("exchange must be 'rccl' or 'host'")
+        raise ValueError("exchange must be 'rccl', 'host' or 'device'")
     e = engine_cls(len(idx), 1, device=device)
     e.set_shard(rank, world, off, len(nodes), box[0])
     if exchange == "host":
         e.set_shard_exchange(host_gather(dist))
+    if exchange == "device":  # FGD: the shards' k_hmemo slices exchange granules through IPC-mapped buffers
+        handles = [None] * world
+        dist.all_gather_object(handles, e.shard_peer_handle())
+        e.set_shard_peers(handles)
     e.set_nodes(0, local)
     arr, nt = typical
     e.set_typical(0, arr, nt)

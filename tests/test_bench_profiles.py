@@ -1,6 +1,6 @@
 """bench.py's counter-backed rooflines: every bench configuration's profile is
-committed under profiles/r02/prof/<profile_key>, and bench.py picks it up only for the kernel the run
-launched.  CPU only (reads the committed summaries)."""
+committed under profiles/<round>/prof/<profile_key> (the newest round first), and bench.py picks it up
+only for the kernel the run launched.  CPU only (reads the committed summaries)."""
 import argparse
 import json
 import os
@@ -33,7 +33,7 @@ def test_profile_keys():
                                       ("c2-PWR", "k_replay"), ("c2-PWR_500_FGD_500", "k_replay")])
 def test_committed_profiles_feed_the_bench_line(key, path):
     import bench
-    pf = os.path.join(bench.PROF_DIR, key, "pmc.json")
+    pf = bench.profile_file(key)
     with open(pf) as f:
         dom = json.load(f)["dominant"]
     assert dom["hbm_bytes_per_dispatch"] > 0 and dom["mean_duration_ns"] > 0

@@ -169,6 +169,68 @@ def test_host_exchange_bad_gather_fails(default_trace, bad):
     assert ei.value.code == ksim.KSIM_ESTATE
 
 
+def _device_rank_main(rank, world, port, n_ev, deletes, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = ksim.Trace.openb("default")
+    rp = t.replay(seed=7)
+    nodes = helpers.subset_nodes(rp, list(range(1, t.num_nodes, 5)))
+    events, n = rp.events, n_ev
+    if deletes:
+        events, _ = helpers.delete_stream(t, rp, n_ev, p_delete=0.2, seed=4)
+        n = len(events)
+    runs = []
+    for _ in range(2):  # two runs: the second's granules carry the next epoch over the first's
+        runs.append(SH.run_distributed(nodes, t.typical(), events, n, dist, policy="FGD", seed=3, exchange="device"))
+    q.put((rank, runs[0][0], runs[1][0], runs[0][1]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(150)
+@pytest.mark.parametrize("deletes", [False, True], ids=["create", "delete"])
+def test_device_exchange_two_processes(default_trace, deletes):
+    # two shard processes on the one GPU, each a persistent k_hmemo over its slices, exchanging per-pod
+    # granules through each other's IPC-mapped buffers (the one-process-per-GPU mode's exchange; on a
+    # node the peers' buffers sit on other GPUs, over xGMI)
+    import multiprocessing as mp
+    import socket
+    n_ev = 600
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_device_rank_main, args=(r, 2, port, n_ev, deletes, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=100) for _ in procs), key=lambda x: x[0])
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.join(20)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    rp = default_trace.replay(seed=7)
+    keep = list(range(1, default_trace.num_nodes, 5))
+    if deletes:
+        events, oev = helpers.delete_stream(default_trace, rp, n_ev, p_delete=0.2, seed=4)
+    else:
+        oev = helpers.oracle_events(default_trace, rp, n_ev)
+    want, _, _ = O.run_events(helpers.oracle_subset(default_trace, rp, keep), helpers.oracle_typical(default_trace),
+                              oev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, seed=3, threads=16)
+    for r in res:
+        assert r[1] == want and r[2] == want
+    print("device exchange world 2: %d events, rank times %.2f / %.2f ms" % (len(oev), res[0][3], res[1][3]))
+
+
 def _host_rank_main(rank, world, port, policy, n_ev, q):
     import os
     import torch.distributed as dist
