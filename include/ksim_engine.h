@@ -212,7 +212,10 @@ typedef struct {
                                       for FGD (KSIM_ENOTSUP otherwise), 4 = k_memo in decider mode (workgroup 0
                                       decides every event from the class owners' top lists; KSIM_ENOTSUP if it
                                       does not fit), 5 = k_hmemo required for FGD (one workgroup per replica,
-                                      keys in HBM; KSIM_ENOTSUP if it does not fit) */
+                                      keys in HBM; KSIM_ENOTSUP if it does not fit), 6 = k_pmemo required for FGD
+                                      (node slices of <= 64 ranks on co-resident workgroups, the previous
+                                      step's exchange overlapping the next step's key refresh; KSIM_ENOTSUP
+                                      if it does not apply) */
     int32_t reserved[3];
 } ksim_config;
 
@@ -342,7 +345,8 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
  * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica), KSIM_PATH_RANDOM_GO
  * (k_random_go: every replica Random on Go's stream, ksim_engine_set_go_stream), KSIM_PATH_SCAN1
  * (k_scan1: every replica a cheap policy on one 256-thread workgroup, every node scanned per pod;
- * a mix of k_scan1 and k_replay groups reports KSIM_PATH_REPLAY). */
+ * a mix of k_scan1 and k_replay groups reports KSIM_PATH_REPLAY), KSIM_PATH_PMEMO (k_pmemo: pipelined
+ * memoised FGD, node slices). */
 #define KSIM_PATH_REPLAY  0
 #define KSIM_PATH_MEMO    1
 #define KSIM_PATH_MIXED   2
@@ -351,6 +355,7 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 #define KSIM_PATH_HMEMO   5
 #define KSIM_PATH_RANDOM_GO 6
 #define KSIM_PATH_SCAN1   7
+#define KSIM_PATH_PMEMO   8
 int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus

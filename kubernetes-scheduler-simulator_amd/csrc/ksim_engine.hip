@@ -656,6 +656,7 @@ __global__ void k_shard_gather(unsigned long long* const* sends, unsigned long l
 #include "ksim_report.hpp"
 #include "ksim_memo.hpp"
 #include "ksim_hmemo.hpp"
+#include "ksim_pmemo.hpp"
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
@@ -1579,6 +1580,13 @@ struct ksim_engine {
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
   size_t h_cap[14] = {};
   int last_hmemo = 0;
+  // k_pmemo (pipelined memoised FGD replay, ksim_pmemo.hpp): uses the k_hmemo plan's tables
+  bool pplan_ok = false;
+  int p_K = 0, p_S = 0;
+  size_t p_lds = 0;
+  int* d_p_evg = nullptr;
+  size_t p_cap = 0;
+  int last_pmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
   int scan1 = 2;       // single-workgroup cheap-policy groups on k_scan1, node records in VGPRs where they fit
@@ -2005,6 +2013,8 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   return KSIM_OK;
 }
 
+static int prepare_pmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev);
+
 // Plan and upload the k_memo launch of the FGD replicas (before the timed region of a run; cached
 // until events or policies change).
 static int prepare_memo(ksim_engine* e, int max_ev) {
@@ -2018,8 +2028,17 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   e->mplan_max_ev = max_ev;
   e->mplan_ok = false;
   e->hplan_ok = false;
+  e->pplan_ok = false;
   if (reps.empty()) return KSIM_OK;
   if (e->run_mode == 5) return prepare_hmemo(e, reps, max_ev);  // k_hmemo required
+  if (e->run_mode == 6) return prepare_pmemo(e, reps, max_ev);  // k_pmemo required
+  {  // auto: k_pmemo where it applies (KSIM_PMEMO=0: not)
+    const char* pm = std::getenv("KSIM_PMEMO");
+    if (e->run_mode == 0 && pm && pm[0] == '1') {
+      int rc = prepare_pmemo(e, reps, max_ev);
+      if (rc || e->pplan_ok) return rc;
+    }
+  }
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
   // run_mode 4 (or KSIM_MEMO_DECIDER=1 with run_mode 0): the decider variant of k_memo
@@ -2369,6 +2388,107 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   return KSIM_OK;
 }
 
+// ---- k_pmemo (pipelined memoised FGD replay, ksim_pmemo.hpp): the k_hmemo plan's tables (score
+// groups, their requests, the distinct initial states) plus the group of every event; K co-resident
+// workgroups per replica with <= 64 slots each.  Not eligible (pplan_ok stays false): deletes, the
+// cluster report, a GPU selector other than FGD / best / worst / random, more than 128 score groups,
+// clusters wider than 64 slots x the workgroups the CUs give each replica.
+static int prepare_pmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev) {
+  using namespace ksim_pmemo;
+  e->pplan_ok = false;
+  if (e->report) return KSIM_OK;
+  for (int r : reps) {
+    if (e->has_delete[r]) return KSIM_OK;
+    const int sel = e->reps[r].gpusel;
+    if (sel != SEL_FGD && sel != SEL_BEST && sel != SEL_WORST && sel != SEL_RANDOM) return KSIM_OK;
+  }
+  const int Rg = (int)reps.size();
+  const int Kmax = std::min(kSlots, e->cus / std::max(Rg, 1));
+  int K = e->wgs_req > 0 ? e->wgs_req : Kmax;
+  if (K < 1 || K > Kmax) return KSIM_OK;
+  const int S = (e->N + K - 1) / K;
+  if (S > kSlots) return KSIM_OK;
+  K = (e->N + S - 1) / S;  // no empty workgroup
+  int rc = prepare_hmemo(e, reps, max_ev, K, S);  // (K, S only size its unused LDS estimate)
+  if (rc || !e->hplan_ok) return rc;
+  e->hplan_ok = false;  // the tables serve k_pmemo
+  const HPlan& pl = *e->hplan;
+  if (pl.Gmax > kMaxGroups) return KSIM_OK;
+  const size_t lds = pmemo_lds(pl.Gmax);
+  if (lds > 160 * 1024) return KSIM_OK;
+  if (K > 1 && Rg * K > resident_cap(e, (const void*)k_pmemo, lds)) return KSIM_OK;
+  const int stride = std::max(max_ev, 1);
+  std::vector<int> evg((size_t)Rg * stride, -1);
+  for (int i = 0; i < Rg; ++i)
+    for (int k = 0; k < stride; ++k) {
+      const int c = pl.evc[(size_t)i * stride + k];
+      evg[(size_t)i * stride + k] = c < 0 ? -1 : (int)pl.cgrp[(size_t)i * pl.Cmax + c];
+    }
+  if ((rc = upload_vec(e->d_p_evg, e->p_cap, evg, e->stream))) return rc;
+  KSIM_HIP(hipStreamSynchronize(e->stream));
+  e->p_K = K;
+  e->p_S = S;
+  e->p_lds = lds;
+  e->pplan_ok = true;
+  return KSIM_OK;
+}
+
+static int launch_pmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
+  using namespace ksim_pmemo;
+  const HPlan& pl = *e->hplan;
+  const int stride = std::max(max_ev, 1);
+  // the group keys of the distinct initial states (k_hmemo's first init kernel)
+  ksim_hmemo::HInitArgs ia{};
+  ia.reps = e->d_reps;
+  ia.rep_list = e->d_replist + first;
+  ia.N = e->N;
+  ia.Npad = pl.Npad;
+  ia.nb = pl.nb;
+  ia.Cmax = pl.Cmax;
+  ia.Gmax = pl.Gmax;
+  ia.Smax = pl.Smax;
+  ia.cg = e->d_h_cg;
+  ia.cls = e->d_h_cls;
+  ia.cgrp = e->d_h_cgrp;
+  ia.gpod = e->d_h_gpod;
+  ia.roff = 0;
+  ia.st = e->d_h_st;
+  ia.ns = e->d_h_ns;
+  ia.nstate = e->d_h_nstate;
+  ia.gsc = e->d_h_gsc;
+  ia.th = e->d_th;
+  hipLaunchKernelGGL(ksim_hmemo::k_hinit_gk, dim3((unsigned)((pl.Smax + 255) / 256), (unsigned)pl.Gmax, (unsigned)Rg),
+                     dim3(256), 0, st, ia, (const TypDev*)e->d_tp);
+  KSIM_HIP(hipGetLastError());
+  const int K = e->p_K;
+  if (K > 1) KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)Rg * 2 * K, st));
+  PMemoArgs pa;
+  pa.reps = e->d_reps;
+  pa.rep_list = e->d_replist + first;
+  pa.N = e->N;
+  pa.K = K;
+  pa.S = e->p_S;
+  pa.Gmax = pl.Gmax;
+  pa.Smax = pl.Smax;
+  pa.Npad = pl.Npad;
+  pa.cg = e->d_h_cg;
+  pa.gpod = e->d_h_gpod;
+  pa.evg = e->d_p_evg;
+  pa.stride = stride;
+  pa.gsc = e->d_h_gsc;
+  pa.nstate = e->d_h_nstate;
+  pa.th = e->d_th;
+  pa.gran = e->d_gran;
+  pa.fail = e->d_fail;
+  const TypDev* tpp = e->d_tp;
+  const int lrc = launch_persistent((const void*)k_pmemo, Rg * K, kPBlock, e->p_lds, st, e->coop && K > 1, pa, tpp);
+  if (lrc) return lrc;
+  hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
+                     e->d_reps, (const int*)(e->d_replist + first), e->N);
+  KSIM_HIP(hipGetLastError());
+  return KSIM_OK;
+}
+
 extern "C" {
 
 const char* ksim_strerror(int code) {
@@ -2533,7 +2653,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_p_evg};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -3245,6 +3365,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   int first = 0;
   e->last_memo = 0;
   e->last_hmemo = 0;
+  e->last_pmemo = 0;
   e->last_rgo = 0;
   e->last_scan1 = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
@@ -3257,6 +3378,10 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     if (!concurrent) break;
     if (gp.first == kPolRandomGo) continue;  // one workgroup per replica
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
+    if (gp.first == POL_FGD && e->run_mode != 2 && e->pplan_ok) {
+      if (e->p_K > 1) { concurrent = false; break; }
+      continue;
+    }
     if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) {
       if (e->hplan->K > 1) { concurrent = false; break; }  // a co-resident wide launch
       continue;  // one workgroup per replica
@@ -3318,6 +3443,15 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                                   pl.decider ? " (decider)" : "", Rg, pl.K, pl.Cw, pl.nfw, pl.lds);
         continue;
       }
+      if (e->pplan_ok) {  // k_pmemo: node slices, pipelined exchange, keys in LDS
+        const int rc = launch_pmemo(e, Rg, first, max_ev, gs);
+        if (rc) return rc;
+        e->last_K = e->p_K;
+        e->last_groups = (int)groups.size();
+        e->last_pmemo += Rg;
+        first += Rg;
+        continue;
+      }
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
         const int rc = launch_hmemo(e, Rg, first, max_ev, gs);
         if (rc) return rc;
@@ -3327,7 +3461,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         first += Rg;
         continue;
       }
-      if (e->run_mode == 3 || e->run_mode == 4 || e->run_mode == 5) return KSIM_ENOTSUP;
+      if (e->run_mode >= 3 && e->run_mode <= 6) return KSIM_ENOTSUP;
     }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
@@ -3890,9 +4024,10 @@ int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
   else if (e->last_rgo == e->R) *path = KSIM_PATH_RANDOM_GO;
   else if (e->last_scan1 == e->R) *path = KSIM_PATH_SCAN1;
-  else if (e->last_memo == 0 && e->last_hmemo == 0) *path = KSIM_PATH_REPLAY;
+  else if (e->last_memo == 0 && e->last_hmemo == 0 && e->last_pmemo == 0) *path = KSIM_PATH_REPLAY;
   else if (e->last_memo == e->R) *path = KSIM_PATH_MEMO;
   else if (e->last_hmemo == e->R) *path = KSIM_PATH_HMEMO;
+  else if (e->last_pmemo == e->R) *path = KSIM_PATH_PMEMO;
   else *path = KSIM_PATH_MIXED;
   return KSIM_OK;
 }

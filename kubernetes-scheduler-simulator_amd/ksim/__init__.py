@@ -357,7 +357,8 @@ class Engine:
     def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0, wgs_per_replica=0,
                  run_mode=0):
         """run_mode (ksim_config.run_mode): 0 auto (FGD: k_memo, else k_hmemo, else k_replay), 1 k_step per
-        pod (hipGraph), 2 k_replay only, 3 k_memo required, 4 k_memo decider mode, 5 k_hmemo required."""
+        pod (hipGraph), 2 k_replay only, 3 k_memo required, 4 k_memo decider mode, 5 k_hmemo required,
+        6 k_pmemo required (pipelined memoised FGD on node slices of <= 64 ranks)."""
         self.N, self.R = n_nodes, n_replicas
         cfg = Config(device, nodes_per_block, steps_per_graph, wgs_per_replica, run_mode)
         h = _VP()
@@ -557,11 +558,13 @@ class Engine:
         return s.value
 
     def last_run_path(self):
-        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go': the kernels the last run()
+        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go' | 'k_scan1' |
+        'k_pmemo': the kernels the last run()
         used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
-        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1"][k.value]
+        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1",
+                "k_pmemo"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)
