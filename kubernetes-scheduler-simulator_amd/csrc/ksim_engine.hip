@@ -2416,7 +2416,7 @@ static int prepare_pmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   if (pl.Gmax > kMaxGroups) return KSIM_OK;
   const size_t lds = pmemo_lds(pl.Gmax);
   if (lds > 160 * 1024) return KSIM_OK;
-  if (K > 1 && Rg * K > resident_cap(e, (const void*)k_pmemo, lds)) return KSIM_OK;
+  if (K > 1 && Rg * K > resident_cap(e, (const void*)k_pmemo<false>, lds)) return KSIM_OK;
   const int stride = std::max(max_ev, 1);
   std::vector<int> evg((size_t)Rg * stride, -1);
   for (int i = 0; i < Rg; ++i)
@@ -2480,9 +2480,109 @@ static int launch_pmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   pa.th = e->d_th;
   pa.gran = e->d_gran;
   pa.fail = e->d_fail;
+  pa.prof = nullptr;
+  pa.trace = nullptr;
+  pa.trace_steps = 0;
+  const char* pe = std::getenv("KSIM_PROFILE");
+  const bool profile = pe && (pe[0] == '1' || pe[0] == '2');
+  const bool tracing = pe && pe[0] == '2';
+  const int TS = std::min(max_ev, 4000);
+  unsigned long long* d_trace = nullptr;
+  if (tracing) {
+    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * kTr * (size_t)Rg * K * TS));
+    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * kTr * (size_t)Rg * K * TS, st));
+    pa.trace = d_trace;
+    pa.trace_steps = TS;
+  }
+  if (profile) {
+    int rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)Rg * K * kPProf);
+    if (rc) return rc;
+    KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * K * kPProf, st));
+    pa.prof = e->d_prof;
+  }
   const TypDev* tpp = e->d_tp;
-  const int lrc = launch_persistent((const void*)k_pmemo, Rg * K, kPBlock, e->p_lds, st, e->coop && K > 1, pa, tpp);
+  const void* f = profile ? (const void*)k_pmemo<true> : (const void*)k_pmemo<false>;
+  const int lrc = launch_persistent(f, Rg * K, kPBlock, e->p_lds, st, e->coop && K > 1, pa, tpp);
   if (lrc) return lrc;
+  if (profile) {
+    KSIM_HIP(hipStreamSynchronize(st));
+    const int nwg = Rg * K;
+    std::vector<unsigned long long> h((size_t)nwg * kPProf);
+    KSIM_HIP(hipMemcpy(h.data(), e->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    static const char* names[] = {"F round", "D: job keys", "D: slice max", "D: exchange wait",
+                                  "D: publish+commit+virtual", "D: next list", "end barrier"};
+    const double steps = std::max(max_ev, 1);
+    std::fprintf(stderr, "ksim pmemo profile: %d replicas x K=%d (S %d), LDS %zu B; us/step mean [max]:", Rg, K, e->p_S,
+                 e->p_lds);
+    for (int ph = 0; ph < 7; ++ph) {
+      double sum = 0, mx = 0;
+      for (int b = 0; b < nwg; ++b) {
+        const double us = (double)h[(size_t)b * kPProf + ph] / 100.0 / steps;
+        sum += us;
+        mx = std::max(mx, us);
+      }
+      std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / nwg, mx);
+    }
+    double it = 0, jb = 0, cr = 0, cyc = 0, tick = 0;
+    for (int b = 0; b < nwg; ++b) {
+      it += (double)h[(size_t)b * kPProf + 7];
+      jb += (double)h[(size_t)b * kPProf + 8];
+      cr += (double)h[(size_t)b * kPProf + 9];
+      cyc += (double)h[(size_t)b * kPProf + 10];
+      tick += (double)h[(size_t)b * kPProf + 11];
+    }
+    std::fprintf(stderr, " per workgroup and step: critical items %.2f, critical jobs %.2f, bulk items %.2f;",
+                 it / nwg / steps, jb / nwg / steps, cr / nwg / steps);
+    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nwg / 1e5);
+    std::fprintf(stderr, "\n");
+  }
+  if (tracing) {
+    // replica 0: per step, the first and the last workgroup to publish, and where their time went
+    std::vector<unsigned long long> h((size_t)kTr * Rg * K * TS);
+    KSIM_HIP(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+    KSIM_HIP(hipFree(d_trace));
+    auto at = [&](int wg, int s, int k) { return (double)h[((size_t)wg * TS + s) * kTr + k] / 100.0; };  // us
+    // phases of step s at one workgroup: prev lists done -> F start (barrier), F round, D start -> wait,
+    // wait, done -> publish, publish -> lists done
+    double ph_last[6] = {}, ph_first[6] = {}, spread = 0, vis = 0, period = 0;
+    int n = 0;
+    for (int s = 2; s + 2 < TS; ++s) {
+      int lastk = 0, firstk = 0;
+      bool okk = true;
+      for (int k = 0; k < K && okk; ++k)
+        for (int x = 0; x < kTr; ++x) okk = okk && at(k, s, x) > 0 && at(k, s - 1, x) > 0 && at(k, s + 1, x) > 0;
+      if (!okk) continue;
+      for (int k = 1; k < K; ++k) {
+        if (at(k, s, 4) > at(lastk, s, 4)) lastk = k;
+        if (at(k, s, 4) < at(firstk, s, 4)) firstk = k;
+      }
+      auto phases = [&](int k, double* ph) {
+        ph[0] += at(k, s, 0) - at(k, s - 1, 5);
+        ph[1] += at(k, s, 1) - at(k, s, 0);
+        ph[2] += at(k, s, 2) - at(k, s, 1);
+        ph[3] += at(k, s, 3) - at(k, s, 2);
+        ph[4] += at(k, s, 4) - at(k, s, 3);
+        ph[5] += at(k, s, 5) - at(k, s, 4);
+      };
+      phases(lastk, ph_last);
+      phases(firstk, ph_first);
+      spread += at(lastk, s, 4) - at(firstk, s, 4);
+      double vmin = 1e300;
+      for (int k = 0; k < K; ++k) vmin = std::min(vmin, at(k, s + 1, 3) - at(lastk, s, 4));
+      vis += vmin;
+      period += at(lastk, s + 1, 4) - at(lastk, s, 4);
+      ++n;
+    }
+    if (n) {
+      std::fprintf(stderr, "ksim pmemo trace (replica 0, %d steps, us): publish spread %.3f; last publish -> first exchange done %.3f; "
+                   "period %.3f; phases [barrier, F, D to wait, wait, to publish, lists] last publisher:", n, spread / n, vis / n,
+                   period / n);
+      for (int x = 0; x < 6; ++x) std::fprintf(stderr, " %.3f", ph_last[x] / n);
+      std::fprintf(stderr, "; first publisher:");
+      for (int x = 0; x < 6; ++x) std::fprintf(stderr, " %.3f", ph_first[x] / n);
+      std::fprintf(stderr, "\n");
+    }
+  }
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
   KSIM_HIP(hipGetLastError());

@@ -6,39 +6,42 @@
 // k_replay's pipelining (ksim_replay.hpp) on memoised keys, so the hand-off overlaps the step's work:
 //
 //   - node slices: replica r is run by K co-resident workgroups, workgroup w owning the name ranks
-//     [w S, w S + S) with S <= 64 (one wave-0 lane per slot).  LDS holds the slice's records, the F
-//     of every slot's current state and the packed key of every (score group, slot) pair:
+//     [w S, w S + S) with S <= 64: wave-0 lane n holds slot n's record, its stale bits and (LDS) the
+//     F of its current state.  LDS holds the packed key of every (score group, slot) pair:
 //     gk[g][slot] = the group's best (score, GPU) on that node with the rank (hkey), the Filter NOT
 //     applied -- groups share the candidate states (same cpu_nz, milli, num: fgd_score.go:99-149),
 //     and the per-class Filter is evaluated when a step reads the key (one lane per slot);
 //   - the only slot of a slice that step s can change is the slice's own candidate b (its best key
 //     for step s).  Right after publishing step s a workgroup works on step s+1 with b excluded,
 //     and evaluates b twice: as it is (pre) and in a VIRTUAL slot holding b with step s's Reserve +
-//     Bind applied (post).  When step s's exchange completes it commits (it owned the winner: the
-//     virtual slot becomes b) and publishes step s+1 with post or pre (selectHost over the union,
-//     generic_scheduler.go:187-212);
-//   - staleness: a committed slot's keys are stale in every group but the step's (bit per (slot,
-//     group)).  Each step's work list holds the critical items -- the virtual slot's F0 and the
-//     step group's candidates on it, the step group's candidates on every slot still stale in it --
-//     and fills the rest of the round's 16 wave slots with stale (slot, group) pairs of one focus
-//     slot (bulk), so a changed node's keys become fresh within a few steps while no step waits on
-//     a key it does not read.
+//     Bind applied (post).  When step s's exchange completes it publishes step s+1 with post (it
+//     owned the winner) or pre -- selectHost over the union (generic_scheduler.go:187-212) -- and
+//     commits (the virtual slot becomes b);
+//   - staleness: a committed slot's keys are stale in every group but the step's (one bit per (slot,
+//     group), in wave 0's registers).  Each step's critical list holds the virtual slot's F0 and the
+//     step group's candidates on it, and the step group's candidates on every slot still stale in
+//     it; a bulk batch of other stale (slot, group) pairs of one focus slot is evaluated by waves
+//     1-15 while wave 0 runs the next step's decision (their keys land one step later), so a changed
+//     node's keys become fresh within a few steps, no step waits on a key it does not read, and the
+//     refresh stays off the chain.  A batch listed at step t leaves out step t+1's group and the
+//     slot pending after step t (the only one step t+1 can commit).
 //
 // Per pod step s (every workgroup of the replica):
-//   F   one wave per listed item: fgd_candidate + wave_F (frag.go's sequential fp64 bins, the same
+//   F   one wave per critical item: fgd_candidate + wave_F (frag.go's sequential fp64 bins, the same
 //       bits as frag_F);                                                                  | barrier
-//   K   one wave per job (slot, group): the candidates' score steps (score_lookup_dev), the group key
-//       = max (ties: lowest GPU, fgd_score.go:128), the stale bit cleared;               | barrier
-//   D   wave 0: the slice's best key for step s over the fresh keys with b excluded (Filter per
-//       lane), the exchange of step s-1 (granules polled since the F round), the commit and the
-//       result of step s-1, b's version, the granule of step s, Reserve + Bind of the new candidate
-//       into the virtual slot, and the work list of step s+1.                           | barrier
+//   D   wave 0: the group keys of the critical jobs and of the bulk batch listed at step s-2 (one
+//       lane per item: the score steps; one lane per job: the max, ties to the lowest GPU,
+//       fgd_score.go:128), the slice's best key for step s with b excluded (Filter per lane), b's
+//       versions, the exchange of step s-1 (granules polled since the F round), the granule of step
+//       s, the result and commit of step s-1, Reserve + Bind of the new candidate into the virtual
+//       slot, the critical list of step s+1 and the next bulk batch;
+//       waves 1-15: the bulk batch listed at step s-1.                                     | barrier
 // Every key read in D is fresh, and b's versions are the same keys k_hmemo / k_replay / the oracle
 // compute (the same device functions), so the decisions are theirs.
 //
-// Scope: FGD replicas on create-only streams (no report, no profile), N <= 64 K, K <= 64 co-resident
-// workgroups, <= 128 score groups, the FGD / best / worst / random GPU selectors.  The host takes
-// k_memo / k_hmemo / k_replay otherwise.
+// Scope: FGD replicas on create-only streams (no report), N <= 64 K, K <= 64 co-resident workgroups,
+// <= 128 score groups, the FGD / best / worst / random GPU selectors.  The host takes k_memo /
+// k_hmemo / k_replay otherwise.
 #pragma once
 
 namespace ksim_pmemo {
@@ -53,11 +56,11 @@ using ksim_hmemo::hkey_score;
 constexpr int kPBlock = 1024;
 constexpr int kPWaves = kPBlock / 64;
 constexpr int kSlots = 64;                       // slots per workgroup (one wave-0 lane each)
-constexpr int kVirt = kSlots;                    // slot index of the virtual node
+constexpr int kVirt = kSlots;                    // job slot code of the virtual node
 constexpr int kMaxGroups = 128;                  // two u64 stale words per slot
-constexpr int kBulkJobs = kPWaves;               // bulk jobs per step (one K round)
-constexpr int kMaxJobs = 1 + kSlots + kBulkJobs;
-constexpr int kMaxItems = 9 + 8 * kSlots + kPWaves + 15;
+constexpr int kBulk = kPWaves - 1;               // bulk items (and jobs) per step: waves 1-15, one each
+constexpr int kMaxJobs = 1 + kSlots;             // critical jobs: the virtual slot + every slot
+constexpr int kMaxItems = 9 + 8 * kSlots;        // critical items
 constexpr int kEvBuf = 128;
 constexpr int kTagBits = 19;                     // granule: key << 32 | count << 19 | (step + 1) tag
 constexpr unsigned kTagMask = (1u << kTagBits) - 1u;
@@ -78,28 +81,47 @@ struct PMemoArgs {
   const double* th;         // [102] FGD score steps
   unsigned long long* gran; // [Rg][2][K] exchange granules
   int* fail;                // a granule poll timed out
+  unsigned long long* prof; // k_pmemo<true>: [Rg * K][kPProf] phase sums (KSIM_PROFILE=1)
+  unsigned long long* trace; // k_pmemo<true>: [Rg * K][trace_steps][kTr] times of step s (see kTr)
+  int trace_steps;
 };
+// 0 F round, 1 D: job keys, 2 D: slice max + b's versions, 3 exchange wait, 4 publish + result +
+// commit + virtual, 5 next lists, 6 end barrier; 7 critical items, 8 critical jobs, 9 bulk items,
+// 10 shader clock, 11 wall ticks
+constexpr int kPProf = 12;
+// trace of step s: 0 F round start, 1 D start, 2 wait start, 3 exchange(s-1) done, 4 publish(s), 5 lists done
+constexpr int kTr = 6;
+
+// Item descriptor: slot (kVirt: the virtual slot) | fgd_candidate code << 8 | group << 16.
+__device__ __forceinline__ unsigned pdesc(int slot, int code, int g) {
+  return (unsigned)slot | ((unsigned)code << 8) | ((unsigned)g << 16);
+}
 
 struct __align__(16) PShared {
   PodDev ev[kEvBuf];
   int evg[kEvBuf];
   TypDev tp[kMaxTypical];
   double th[104];
-  NodeRec nodes[kSlots + 1];                    // slot kVirt: the pending candidate after its Bind
-  double F0[kSlots + 2];                        // F of every slot's current state (kVirt: the virtual's)
-  unsigned long long stale[kSlots + 1][2];      // bit g: gk[g][slot] is stale
-  double F[kMaxItems];
-  uint8_t item_job[kMaxItems];
-  uint8_t item_code[kMaxItems];                 // fgd_candidate: 0 current, 1..8 GPU, 9 Sub
+  NodeRec nodes[kSlots + 1];                    // wave 0's records (slot kVirt: the virtual slot) for the F waves
+  double F0[kSlots];                            // F of every slot's current state
+  double F[kMaxItems];                          // critical items
+  unsigned desc[kMaxItems];
+  unsigned kbuf[kMaxItems];                     // the items' keys (D)
+  double bF[2][kBulk + 1];                      // bulk batches (by listing step parity)
+  unsigned bdesc[2][kBulk + 1];
+  unsigned bkbuf[kBulk + 1];
   uint8_t job_slot[kMaxJobs];
   uint8_t job_grp[kMaxJobs];
   uint8_t job_n[kMaxJobs];
-  uint8_t pad_[(16 - (2 * kMaxItems + 3 * kMaxJobs) % 16) % 16];
+  uint8_t bjob_n[2][kBulk + 1];
+  uint8_t bjob_grp[2][kBulk + 1];
+  uint8_t bjob_o[2][kBulk + 1];
+  uint8_t pad_[(16 - (3 * kMaxJobs + 6 * (kBulk + 1)) % 16) % 16];
   uint16_t job_o[kMaxJobs];
   uint16_t pad2_[(8 - kMaxJobs % 8) % 8];
-  int nitems, njobs, vslot, stop;
-  unsigned vgk;                                 // the virtual slot's key in the step's group
-  int pad3_[3];
+  int nitems, njobs, ncrit, stop;
+  int nbitems[2], nbjobs[2], bslot[2], pad3_[2];
+  unsigned long long prof[kPProf];
 };
 static_assert(sizeof(PShared) % 16 == 0, "keep the dynamic regions 16-B aligned");
 
@@ -107,11 +129,6 @@ static_assert(sizeof(PShared) % 16 == 0, "keep the dynamic regions 16-B aligned"
 inline size_t pmemo_lds(int Gmax) {
   return sizeof(PShared) + (size_t)Gmax * sizeof(PodDev) + (size_t)Gmax * kSlots * 4 +
          (size_t)kPWaves * ksim_memo::kFoldBuf * 8;
-}
-
-// Wave-uniform 64-bit readlane.
-__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
-  return ksim_replay::readlane_u64(v, l);
 }
 
 // Exclusive prefix and total of a per-lane count 0..15 over the wave (four ballot bit planes).
@@ -129,7 +146,37 @@ __device__ __forceinline__ int lane_prefix(int v, int* tot) {
 __device__ __forceinline__ int lanes_before(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
+// Workgroup barrier for LDS hand-offs only: __syncthreads() is a release fence as well, which makes
+// every wave wait for its outstanding global stores (here: the granule and result stores, whose
+// acknowledgement takes about a hand-off latency) before the barrier.  Nothing in the step loop
+// hands global memory between waves of one workgroup, so the wave's LDS queue is all it drains.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// A lane's record as wave-uniform values (v_readlane).
+__device__ __forceinline__ NodeV readlane_node(const NodeV& n, int l) {
+  NodeV u;
+  u.cpu_left = __builtin_amdgcn_readlane(n.cpu_left, l);
+  u.mem_left = __builtin_amdgcn_readlane(n.mem_left, l);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u.g[i] = (uint32_t)__builtin_amdgcn_readlane((int)n.g[i], l);
+  u.meta = (uint32_t)__builtin_amdgcn_readlane((int)n.meta, l);
+  u.name_rank = (uint32_t)__builtin_amdgcn_readlane((int)n.name_rank, l);
+  return u;
+}
+
+// F of one listed item (one wave): the candidate state of its slot's LDS record for its group's request.
+__device__ __forceinline__ double item_F(unsigned d, const NodeRec* nodes, const PodDev* gpod, bool typed, const TypDev* ltp,
+                                        int ncpu, int nt, int lane, double* fold) {
+  const int slot = (int)(d & 0xffu), code = (int)((d >> 8) & 0xfu), g = (int)(d >> 16);
+  const NodeV m = ksim_replay::uniform_node(&nodes[slot]);
+  const PodDev gp = ksim_replay::uniform_pod(&gpod[g]);
+  int cpuL, total;
+  uint32_t gs[4];
+  ksim_replay::fgd_candidate(m, code, gp, &cpuL, gs, &total);
+  return ksim_memo::wave_F(cpuL, gs, total, 1u << m.gpu_type(), typed, ltp, ncpu, nt, lane, fold);
+}
+
+template <bool kProf>
 __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __restrict__ tp_all) {
   using namespace ksim_replay;
   using ksim_memo::gget;
@@ -147,14 +194,14 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + sizeof(PShared));
   unsigned* s_gk = reinterpret_cast<unsigned*>(s_gpod + a.Gmax);
   double* s_fold = reinterpret_cast<double*>(s_gk + (size_t)a.Gmax * kSlots);
+  double* fold = s_fold + (size_t)wv * ksim_memo::kFoldBuf;
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   const int* evg = a.evg + (size_t)gi * a.stride;
   unsigned long long* gr = a.gran + (size_t)gi * 2 * K;
   const int E = rp.n_events;
   const bool typed = rp.typed != 0;
 
-  // ---- start-up: the slice (slot = rank - lo), the groups, the initial keys, the tables
-  for (int i = tid; i < ns; i += kPBlock) store_node(&sh.nodes[i], load_node(rp.nodes + rank2idx[lo + i]));
+  // ---- start-up: the groups, the initial keys, the tables; wave 0 lane n: slot n's record
   for (int g = tid; g < G; g += kPBlock) s_gpod[g] = a.gpod[(size_t)gi * a.Gmax + g];
   for (int x = tid; x < G * ns; x += kPBlock) {
     const int g = x / ns, i = x - g * ns;
@@ -163,119 +210,152 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
   }
   for (int i = tid; i < rp.nt * 2; i += kPBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kPBlock) sh.th[i] = a.th[i];
-  for (int i = tid; i < 2 * (kSlots + 1); i += kPBlock) (&sh.stale[0][0])[i] = 0ull;
-  if (tid == 0) { sh.stop = 0; sh.nitems = 0; sh.njobs = 0; sh.vslot = -1; sh.vgk = 0u; }
+  for (int i = tid; i < ns; i += kPBlock) {
+    const NodeV n = load_node(rp.nodes + rank2idx[lo + i]);
+    store_node(&sh.nodes[i], n);
+    sh.F0[i] = eval_fgd_item(n, 0, PodDev{}, rp, tp);
+  }
+  if (tid == 0) {
+    sh.stop = 0; sh.nitems = 0; sh.njobs = 0; sh.ncrit = 0;
+    sh.nbitems[0] = sh.nbitems[1] = 0; sh.nbjobs[0] = sh.nbjobs[1] = 0; sh.bslot[0] = sh.bslot[1] = 0;
+  }
+  if (kProf && tid < kPProf) sh.prof[tid] = 0ull;
+  NodeV rec{};                                 // wave 0, lane n < ns: slot n's record
+  unsigned long long st0 = 0ull, st1 = 0ull;   // wave 0, lane n: slot n's stale groups
+  if (wv == 0 && lane < ns) rec = load_node(rp.nodes + rank2idx[lo + lane]);
   __syncthreads();
-  for (int i = tid; i < ns; i += kPBlock) sh.F0[i] = eval_fgd_item(load_node(&sh.nodes[i]), 0, PodDev{}, rp, tp);
+  const bool prof = kProf && a.prof != nullptr;
+  unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long t_start = t_last, c_start = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto tr = [&](int s, int k) {  // KSIM_PROFILE=2: thread 0's timestamps of step s
+    if (kProf && a.trace && tid == 0 && s < a.trace_steps)
+      a.trace[((size_t)blockIdx.x * a.trace_steps + s) * kTr + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto mark = [&](int ph) {  // thread 0 (wave 0 lane 0)
+    if (prof && tid == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - t_last;
+      t_last = t;
+    }
+  };
 
-  // ---- wave 0: the work list of step s1 (event window slot eb1): virtual slot vb (or -1), then the
-  // slots stale in the step's group, then bulk pairs of one focus slot while the round has room.
-  auto build_list = [&](int eb1, int vb) {
+  // wave 0's pending step (published, not committed): candidate slot, key, Reserve mask, count, and
+  // the candidate with the pending Bind applied (the virtual slot; uniform)
+  int pb = -1, pmask = -1, pcnt = 0;
+  unsigned pkey = 0u;
+  bool pend = false;
+  NodeV vrec{};
+  const unsigned long long all0 = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+  const unsigned long long all1 = G > 64 ? (G >= 128 ? ~0ull : ((1ull << (G - 64)) - 1ull)) : 0ull;
+
+  // ---- wave 0: the critical list of the step in event-window slot eb1 (the virtual slot if `virt`,
+  // then every slot stale in the step's group) and the bulk batch `bb` (other stale groups of one
+  // focus slot other than `excl`, the step's group left out); listed pairs leave the stale set now
+  auto build_lists = [&](int eb1, bool virt, int excl, int bb) {
     const int g1 = __builtin_amdgcn_readfirstlane(sh.evg[eb1]);
     const PodDev gp = uniform_pod(&s_gpod[g1]);
     const bool share = is_share_pod(gp);
     int o = 0, nj = 0;
-    if (vb >= 0) {  // item 0: F0 of the virtual slot, then its candidates in the step's group
-      const NodeV vn = uniform_node(&sh.nodes[kVirt]);
-      const unsigned f0 = ksim_memo::first_mask_lanes(vn, lane);
-      const unsigned cm = share ? (f0 & ksim_memo::ge_mask(vn, gp.milli)) : 0x100u;
+    if (virt) {  // item 0: the virtual slot's current state (its F0), then its candidates
+      const unsigned f0 = ksim_memo::first_mask_lanes(vrec, lane);
+      const unsigned cm = share ? (f0 & ksim_memo::ge_mask(vrec, gp.milli)) : 0x100u;
       const int nc = __popc(cm);
+      if (lane <= nc) {
+        unsigned m = cm;
+        for (int q = 1; q < lane; ++q) m &= m - 1u;
+        sh.desc[lane] = pdesc(kVirt, lane == 0 ? 0 : (share ? 1 + __builtin_ctz(m) : 9), g1);
+      }
       if (lane == 0) {
         sh.job_slot[0] = (uint8_t)kVirt;
         sh.job_grp[0] = (uint8_t)g1;
         sh.job_o[0] = 0;
         sh.job_n[0] = (uint8_t)(1 + nc);
-        sh.item_job[0] = 0;
-        sh.item_code[0] = 0;
-        sh.vslot = vb;
-      }
-      if (lane < nc) {
-        unsigned m = cm;
-        for (int q = 0; q < lane; ++q) m &= m - 1u;
-        sh.item_job[1 + lane] = 0;
-        sh.item_code[1 + lane] = (uint8_t)(share ? 1 + __builtin_ctz(m) : 9);
       }
       o = 1 + nc;
       nj = 1;
     }
     // critical: every slot stale in the step's group
-    const unsigned long long st0 = lane < ns ? sh.stale[lane][0] : 0ull, st1 = lane < ns ? sh.stale[lane][1] : 0ull;
     const unsigned long long gbit = 1ull << (g1 & 63);
-    const bool crit = ((g1 < 64 ? st0 : st1) & gbit) != 0ull;
-    unsigned cm = 0u;
-    if (crit) {
-      const NodeV nd = load_node(&sh.nodes[lane]);
-      cm = share ? first_of_class(nd, gp.milli) : 0x100u;
-    }
+    const bool crit = lane < ns && ((g1 < 64 ? st0 : st1) & gbit) != 0ull;
+    const unsigned cm = crit ? (share ? first_of_class(rec, gp.milli) : 0x100u) : 0u;
     int tot = 0;
     const int nc = __popc(cm);
-    const int excl = lane_prefix(nc, &tot);
+    const int ex = lane_prefix(nc, &tot);
     const unsigned long long cb = __ballot(crit);
     if (crit) {
-      const int j = nj + lanes_before(cb), io = o + excl;
+      const int j = nj + lanes_before(cb), io = o + ex;
       sh.job_slot[j] = (uint8_t)lane;
       sh.job_grp[j] = (uint8_t)g1;
       sh.job_o[j] = (uint16_t)io;
       sh.job_n[j] = (uint8_t)nc;
       unsigned m = cm;
       for (int k = 0; k < nc; ++k) {
-        sh.item_job[io + k] = (uint8_t)j;
-        sh.item_code[io + k] = (uint8_t)(share ? 1 + __builtin_ctz(m) : 9);
+        sh.desc[io + k] = pdesc(lane, share ? 1 + __builtin_ctz(m) : 9, g1);
         m &= m - 1u;
       }
+      if (g1 < 64) st0 &= ~gbit;
+      else st1 &= ~gbit;
     }
     nj += __popcll(cb);
     o += tot;
-    // bulk: the lowest slot with other stale groups, its groups in order while the round has room
-    const bool other = lane < ns && ((st0 & (g1 < 64 ? ~gbit : ~0ull)) | (st1 & (g1 < 64 ? ~0ull : ~gbit))) != 0ull;
-    const unsigned long long ob = __ballot(other);
-    int cap = kPWaves - o, jcap = kBulkJobs - nj;
-    if (ob != 0ull && cap > 0 && jcap > 0) {
-      const int fs = __builtin_ctzll(ob);
-      const NodeV fn = uniform_node(&sh.nodes[fs]);
+    if (lane == 0) {
+      sh.nitems = o;
+      sh.njobs = nj;
+      if (kProf) sh.ncrit = nj;
+    }
+    // bulk batch: the lowest slot (not `excl`) with stale groups, its groups in order, one item per wave
+    int bo = 0, bj = 0, fs = -1;
+    const unsigned long long ob = __ballot(lane < ns && lane != excl && (st0 | st1) != 0ull);
+    if (ob != 0ull) {
+      fs = __builtin_ctzll(ob);
+      const NodeV fn = readlane_node(rec, fs);
       const unsigned f0 = ksim_memo::first_mask_lanes(fn, lane);
-      const unsigned long long fw0 = readlane64(st0, fs), fw1 = readlane64(st1, fs);
+      const unsigned long long fw0 = readlane_u64(st0, fs), fw1 = readlane_u64(st1, fs);
+      unsigned long long took0 = 0ull, took1 = 0ull;
       for (int half = 0; half < 2; ++half) {
         const int gg = half * 64 + lane;
         const unsigned long long fw = half ? fw1 : fw0;
-        const bool want = gg < G && gg != g1 && ((fw >> lane) & 1ull) != 0ull;
+        const bool want = ((fw >> lane) & 1ull) != 0ull && gg != g1;
         int bc = 0;
+        unsigned bm = 0u;
         bool bshare = false;
         if (want) {
           const PodDev q = s_gpod[gg];
           bshare = is_share_pod(q);
-          bc = bshare ? __popc(f0 & ksim_memo::ge_mask(fn, q.milli)) : 1;
+          bm = bshare ? (f0 & ksim_memo::ge_mask(fn, q.milli)) : 0x100u;
+          bc = __popc(bm);
         }
         int btot = 0;
         const int bex = lane_prefix(bc, &btot);
         const unsigned long long wb = __ballot(want);
-        const bool take = want && bex + bc <= cap && lanes_before(wb) < jcap;
+        const bool take = want && bo + bex + bc <= kBulk && bj + lanes_before(wb) < kBulk;
         const unsigned long long tb = __ballot(take);
         if (take) {
-          const int j = nj + lanes_before(tb), io = o + bex;
-          sh.job_slot[j] = (uint8_t)fs;
-          sh.job_grp[j] = (uint8_t)gg;
-          sh.job_o[j] = (uint16_t)io;
-          sh.job_n[j] = (uint8_t)bc;
-          unsigned m = bshare ? (f0 & ksim_memo::ge_mask(fn, s_gpod[gg].milli)) : 0x100u;
+          const int j = bj + lanes_before(tb), io = bo + bex;
+          sh.bjob_grp[bb][j] = (uint8_t)gg;
+          sh.bjob_o[bb][j] = (uint8_t)io;
+          sh.bjob_n[bb][j] = (uint8_t)bc;
+          unsigned m = bm;
           for (int k = 0; k < bc; ++k) {
-            sh.item_job[io + k] = (uint8_t)j;
-            sh.item_code[io + k] = (uint8_t)(bshare ? 1 + __builtin_ctz(m) : 9);
+            sh.bdesc[bb][io + k] = pdesc(fs, bshare ? 1 + __builtin_ctz(m) : 9, gg);
             m &= m - 1u;
           }
         }
-        const int used = wave_sum_dpp(take ? bc : 0);
-        nj += __popcll(tb);
-        o += used;
-        cap -= used;
-        jcap -= __popcll(tb);
-        if ((wb & ~tb) != 0ull || cap <= 0 || jcap <= 0) break;  // the round is full
+        if (half == 0) took0 = tb;
+        else took1 = tb;
+        bo += wave_sum_dpp(take ? bc : 0);
+        bj += __popcll(tb);
+        if ((wb & ~tb) != 0ull) break;  // the batch is full
+      }
+      if (lane == fs) {
+        st0 &= ~took0;
+        st1 &= ~took1;
       }
     }
     if (lane == 0) {
-      sh.nitems = o;
-      sh.njobs = nj;
-      if (vb < 0) sh.vslot = -1;
+      sh.nbitems[bb] = bo;
+      sh.nbjobs[bb] = bj;
+      sh.bslot[bb] = fs;
     }
   };
   // wave 0: stage the event window starting at step s0
@@ -287,20 +367,6 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   };
-
-  // wave 0's pending step (published, not committed): candidate slot, key, Reserve mask, count
-  int pb = -1, pmask = -1, pcnt = 0;
-  unsigned pkey = 0u;
-  bool pend = false;
-  const unsigned long long all0 = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
-  const unsigned long long all1 = G > 64 ? (G >= 128 ? ~0ull : ((1ull << (G - 64)) - 1ull)) : 0ull;
-  __syncthreads();
-  if (wv == 0 && E > 0) {
-    refill(0);
-    build_list(0, -1);
-  }
-  __syncthreads();
-
   // wave 0, lane k < K: step ps's granule of workgroup k
   auto poll = [&](int ps) -> unsigned long long {
     return lane < K ? gload(gr + (size_t)(ps & 1) * K + lane) : 0ull;
@@ -326,9 +392,9 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
     *cnt = wave_sum_dpp(cc);
     return ok;
   };
-  // wave 0: the pending step's result and, if this workgroup owned the winner, its commit (the virtual
-  // slot becomes the slot; kg >= 0: the virtual's key in group kg is fresh, every other group stale)
-  auto commit = [&](int ps, unsigned W, int wcnt, int kg) {
+  // wave 0: the pending step's result and, if this workgroup owned the winner and it bound, the commit
+  // (the virtual slot becomes the slot; kg >= 0: its key in group kg is vgk, every other group stale)
+  auto commit = [&](int ps, unsigned W, int wcnt, int kg, unsigned vgk, double F0v) {
     const bool owner = pb >= 0 && W != 0u && W == pkey;
     if (lane == 0) {
       ResultDev out{-1, 0, 0, wcnt, ST_UNSCHED};
@@ -346,144 +412,188 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
       }
       if (write) gput(rp.res + ps, out);
     }
-    if (owner && pmask >= 0) {
-      if (lane < 2) reinterpret_cast<uint4*>(&sh.nodes[pb])[lane] = reinterpret_cast<const uint4*>(&sh.nodes[kVirt])[lane];
-      else if (lane == 2) sh.F0[pb] = sh.F0[kVirt];
-      else if (lane == 3 && kg >= 0) s_gk[kg * kSlots + pb] = sh.vgk;
-      else if (lane == 4) sh.stale[pb][0] = all0 & ((kg >= 0 && kg < 64) ? ~(1ull << kg) : ~0ull);
-      else if (lane == 5) sh.stale[pb][1] = all1 & ((kg >= 64) ? ~(1ull << (kg - 64)) : ~0ull);
+    if (owner && pmask >= 0 && lane == pb) {
+      rec = vrec;
+      store_node(&sh.nodes[pb], vrec);
+      sh.F0[pb] = F0v;
+      if (kg >= 0) s_gk[kg * kSlots + pb] = vgk;
+      st0 = all0 & ((kg >= 0 && kg < 64) ? ~(1ull << kg) : ~0ull);
+      st1 = all1 & ((kg >= 64) ? ~(1ull << (kg - 64)) : ~0ull);
     }
-    return owner && pmask >= 0;
   };
+  // wave 0: the group keys of a job list -- lane i scores item i (F0 - F through the score steps,
+  // keyed with the rank and the item's GPU field), lane j takes job j's max.  fvirt: the virtual
+  // slot's F0 (item 0).
+  auto item_keys = [&](const unsigned* desc, const double* F, unsigned* kb, int nit, int vrank, double fvirt) {
+    for (int i0 = 0; i0 < nit; i0 += 64) {
+      const int i = i0 + lane;
+      if (i < nit) {
+        const unsigned d = desc[i];
+        const int slot = (int)(d & 0xffu), code = (int)((d >> 8) & 0xfu);
+        const bool virt = slot == kVirt;
+        const double F0 = virt ? fvirt : sh.F0[slot];
+        const int rank = virt ? vrank : lo + slot;
+        kb[i] = code == 0 ? 0u
+                          : hkey(ksim_memo::score_lookup_dev(F0 - F[i], sh.th), rank, code <= 8 ? 15 - (code - 1) : 0);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto job_key = [&](const unsigned* kb, int o, int n, int rank, bool share) -> unsigned {
+    unsigned k = share ? hkey(0, rank, 0) : 0u;  // share: feasible with no fitting GPU
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < n) k = kb[o + c] > k ? kb[o + c] : k;
+    return k;
+  };
+
+  __syncthreads();
+  if (wv == 0 && E > 0) {
+    refill(0);
+    build_lists(0, false, -1, 1);  // (an empty-step-parity batch: nothing in flight yet)
+    if (lane == 0) { sh.nbitems[1] = 0; sh.nbjobs[1] = 0; }
+  }
+  __syncthreads();
 
   for (int s = 0; s < E; ++s) {
     const int eb = s & (kEvBuf - 1);
-    // ---- F: one wave per item (wave 0 first issues the pending exchange's loads)
+    // ---- F: one wave per critical item (wave 0 first issues the pending exchange's loads)
     unsigned long long pv = 0ull;
+    tr(s, 0);
     if (wv == 0 && pend && K > 1) pv = poll(s - 1);
     {
       const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
       for (int it = wv; it < nit; it += kPWaves) {
-        const int j = __builtin_amdgcn_readfirstlane((int)sh.item_job[it]);
-        const int code = __builtin_amdgcn_readfirstlane((int)sh.item_code[it]);
-        const int slot = __builtin_amdgcn_readfirstlane((int)sh.job_slot[j]);
-        const int g = __builtin_amdgcn_readfirstlane((int)sh.job_grp[j]);
-        const NodeV m = uniform_node(&sh.nodes[slot]);
-        const PodDev gp = uniform_pod(&s_gpod[g]);
-        int cpuL, total;
-        uint32_t gs[4];
-        fgd_candidate(m, code, gp, &cpuL, gs, &total);
-        const double F = ksim_memo::wave_F(cpuL, gs, total, 1u << m.gpu_type(), typed, sh.tp, rp.ncpu, rp.nt, lane,
-                                           s_fold + (size_t)wv * ksim_memo::kFoldBuf);
+        const double F = item_F(sh.desc[it], sh.nodes, s_gpod, typed, sh.tp, rp.ncpu, rp.nt, lane, fold);
         if (lane == 0) sh.F[it] = F;
       }
     }
-    __syncthreads();
-    // ---- K: one wave per job, the group key from its candidates' score steps
-    {
-      const int nj = __builtin_amdgcn_readfirstlane(sh.njobs);
-      for (int j = wv; j < nj; j += kPWaves) {
-        const int slot = __builtin_amdgcn_readfirstlane((int)sh.job_slot[j]);
-        const int g = __builtin_amdgcn_readfirstlane((int)sh.job_grp[j]);
-        const int o = __builtin_amdgcn_readfirstlane((int)sh.job_o[j]);
-        const int m = __builtin_amdgcn_readfirstlane((int)sh.job_n[j]);
-        const bool virt = slot == kVirt;
-        const int vs = virt ? __builtin_amdgcn_readfirstlane(sh.vslot) : slot;
-        const double F0 = virt ? sh.F[o] : sh.F0[slot];
-        const int c0 = virt ? o + 1 : o, nc = virt ? m - 1 : m;
-        const int rank = lo + vs;
-        const bool share = is_share_pod(uniform_pod(&s_gpod[g]));
-        int k = 0;
-        if (lane < nc) {
-          const int code = sh.item_code[c0 + lane];
-          k = (int)hkey(ksim_memo::score_lookup_dev(F0 - sh.F[c0 + lane], sh.th), rank, share ? 15 - (code - 1) : 0);
+    lds_barrier();
+    mark(0);
+    if (wv != 0) {
+      // ---- waves 1-15: the bulk batch listed at step s-1 (its slot is not the one D commits now)
+      const int bb = (s - 1) & 1;
+      const int nb = __builtin_amdgcn_readfirstlane(sh.nbitems[bb]);
+      if (s >= 1 && wv - 1 < nb) {
+        const double F = item_F(sh.bdesc[bb][wv - 1], sh.nodes, s_gpod, typed, sh.tp, rp.ncpu, rp.nt, lane, fold);
+        if (lane == 0) sh.bF[bb][wv - 1] = F;
+      }
+    } else {
+      // ---- D: wave 0
+      tr(s, 1);
+      const PodDev p = uniform_pod(&sh.ev[eb]);
+      const int g = __builtin_amdgcn_readfirstlane(sh.evg[eb]);
+      // 1. keys: the critical jobs (the virtual job, job 0, kept in registers) and the bulk batch of step s-2
+      const bool vjob = pend && pb >= 0 && pmask >= 0;
+      const double F0v = vjob ? sh.F[0] : 0.0;
+      unsigned vgk = 0u;
+      {
+        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems), nj = __builtin_amdgcn_readfirstlane(sh.njobs);
+        item_keys(sh.desc, sh.F, sh.kbuf, nit, lo + pb, F0v);
+        for (int j0 = 0; j0 < nj; j0 += 64) {
+          const int j = j0 + lane;
+          unsigned k = 0u;
+          if (j < nj) {
+            const int slot = sh.job_slot[j], jg = sh.job_grp[j], o = sh.job_o[j], n = sh.job_n[j];
+            const bool virt = slot == kVirt;
+            k = job_key(sh.kbuf, virt ? o + 1 : o, virt ? n - 1 : n, virt ? lo + pb : lo + slot,
+                        is_share_pod(s_gpod[jg]));
+            if (!virt) s_gk[jg * kSlots + slot] = k;
+          }
+          if (j0 == 0 && vjob) vgk = (unsigned)__builtin_amdgcn_readlane((int)k, 0);
         }
-        unsigned gkey = (unsigned)wave_max_dpp(k);
-        if (share) {
-          const unsigned z = hkey(0, rank, 0);  // feasible with no fitting GPU
-          gkey = gkey > z ? gkey : z;
-        }
-        if (lane == 0) {
-          if (virt) {
-            sh.vgk = gkey;
-            sh.F0[kVirt] = F0;
-          } else {
-            s_gk[g * kSlots + slot] = gkey;
-            __hip_atomic_fetch_and(&sh.stale[slot][g >> 6], ~(1ull << (g & 63)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int bb = s & 1;
+        const int nbi = __builtin_amdgcn_readfirstlane(sh.nbitems[bb]), nbj = __builtin_amdgcn_readfirstlane(sh.nbjobs[bb]);
+        if (s >= 2 && nbj > 0) {
+          const int fs = __builtin_amdgcn_readfirstlane(sh.bslot[bb]);
+          item_keys(sh.bdesc[bb], sh.bF[bb], sh.bkbuf, nbi, 0, 0.0);
+          if (lane < nbj) {
+            const int jg = sh.bjob_grp[bb][lane];
+            const unsigned k = job_key(sh.bkbuf, sh.bjob_o[bb][lane], sh.bjob_n[bb][lane], lo + fs, is_share_pod(s_gpod[jg]));
+            s_gk[jg * kSlots + fs] = k;
           }
         }
       }
-    }
-    __syncthreads();
-    // ---- D: wave 0
-    if (wv == 0) {
-      const PodDev p = uniform_pod(&sh.ev[eb]);
-      const int g = __builtin_amdgcn_readfirstlane(sh.evg[eb]);
-      // the slice's best key over the fresh keys, the pending slot excluded (Filter per lane)
-      bool f = false;
-      if (lane < ns && lane != pb) f = filter_node(load_node(&sh.nodes[lane]), p);
-      int A = (int)(f ? s_gk[g * kSlots + lane] : 0u);
-      A = wave_max_dpp(A);
-      int cnt = (int)__popcll(__ballot(f));
-      // the pending slot as it is (pre) and with the pending Bind applied (post)
+      mark(1);
+      // 2. the slice's best key over the fresh keys, the pending slot excluded (Filter per lane), and the
+      //    pending slot as it is (pre) and with the pending Bind applied (post)
+      const bool fa = lane < ns && filter_node(rec, p);
+      const unsigned ka = fa ? s_gk[g * kSlots + lane] : 0u;
+      const bool fx = fa && lane != pb;
+      int A = wave_max_dpp((int)(fx ? ka : 0u));
+      int cnt = (int)__popcll(__ballot(fx));
       bool fpre = false, fpost = false;
       unsigned kpre = 0u, kpost = 0u;
       if (pb >= 0) {
-        fpre = filter_node(uniform_node(&sh.nodes[pb]), p);
-        kpre = fpre ? s_gk[g * kSlots + pb] : 0u;
+        fpre = ((__ballot(fa) >> pb) & 1ull) != 0ull;
+        kpre = (unsigned)__builtin_amdgcn_readlane((int)ka, pb);
         fpost = fpre;
         kpost = kpre;
         if (pmask >= 0) {
-          fpost = filter_node(uniform_node(&sh.nodes[kVirt]), p);
-          kpost = fpost ? sh.vgk : 0u;
+          fpost = filter_node(vrec, p);
+          kpost = fpost ? vgk : 0u;
         }
       }
-      bool ok = true, bound = false;
-      if (pend) {
-        unsigned W;
-        int wcnt;
-        ok = finish_exchange(s - 1, pv, &W, &wcnt);
-        if (ok) bound = commit(s - 1, W, wcnt, g);
-      }
+      mark(2);
+      tr(s, 2);
+      bool ok = true;
+      unsigned W = 0u;
+      int wcnt = 0;
+      if (pend) ok = finish_exchange(s - 1, pv, &W, &wcnt);
+      mark(3);
+      tr(s, 3);
       if (ok) {
+        const bool bound = pend && pb >= 0 && W != 0u && W == pkey && pmask >= 0;
         if (pb >= 0) {
           const unsigned kb = bound ? kpost : kpre;
           A = (int)((unsigned)A > kb ? (unsigned)A : kb);
           cnt += (bound ? fpost : fpre) ? 1 : 0;
         }
-        // publish step s
+        // publish step s first, then the pending step's result and commit
         if (K > 1 && lane == 0)
           gstore(gr + (size_t)(s & 1) * K + w, ((unsigned long long)(unsigned)A << 32) |
                                                    ((unsigned long long)(unsigned)(cnt & kCntMask) << kTagBits) |
                                                    (unsigned long long)((unsigned)(s + 1) & kTagMask));
+        tr(s, 4);
+        if (pend) commit(s - 1, W, wcnt, g, vgk, F0v);
         // Reserve + Bind of the new candidate into the virtual slot
         int nb = -1, nmask = -1;
         if (A != 0) {
           nb = hkey_rank((unsigned)A) - lo;
-          NodeV bn = uniform_node(&sh.nodes[nb]);
+          NodeV bn = readlane_node(rec, nb);
           nmask = select_gpus(bn, p, rp.gpusel, hkey_gpu((unsigned)A), rp.seed, s);
           if (nmask >= 0) {
             bind_node(bn, p, nmask, +1);
             if (lane == 0) store_node(&sh.nodes[kVirt], bn);
           }
+          vrec = bn;
         }
         pend = true;
         pb = nb;
         pkey = (unsigned)A;
         pmask = nmask;
         pcnt = cnt;
+        mark(4);
         if (s + 1 < E) {
           const int eb1 = (s + 1) & (kEvBuf - 1);
           if (eb1 == 0) refill(s + 1);
-          build_list(eb1, (nb >= 0 && nmask >= 0) ? nb : -1);
+          build_lists(eb1, nb >= 0 && nmask >= 0, nb, s & 1);
+          if (prof && lane == 0) {
+            sh.prof[7] += (unsigned long long)sh.nitems;
+            sh.prof[8] += (unsigned long long)sh.ncrit;
+            sh.prof[9] += (unsigned long long)sh.nbitems[s & 1];
+          }
         }
+        mark(5);
+        tr(s, 5);
       } else if (lane == 0) {
         sh.stop = 1;
         atomicOr(a.fail, 1);
       }
     }
-    __syncthreads();
+    lds_barrier();
+    mark(6);
     if (sh.stop) break;
   }
   // the last step's exchange and commit (no key is read any more)
@@ -491,13 +601,17 @@ __global__ __launch_bounds__(kPBlock) void k_pmemo(PMemoArgs a, const TypDev* __
     unsigned W;
     int wcnt;
     const unsigned long long pv = K > 1 ? poll(E - 1) : 0ull;
-    if (finish_exchange(E - 1, pv, &W, &wcnt)) (void)commit(E - 1, W, wcnt, -1);
+    if (finish_exchange(E - 1, pv, &W, &wcnt)) commit(E - 1, W, wcnt, -1, 0u, 0.0);
     else if (lane == 0) { sh.stop = 1; atomicOr(a.fail, 1); }
   }
+  if (prof && tid == 0) {
+    sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
+    sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;
+  }
   __syncthreads();
-  // final cluster state
-  if (!sh.stop)
-    for (int i = tid; i < ns; i += kPBlock) store_node(rp.nodes + rank2idx[lo + i], load_node(&sh.nodes[i]));
+  if (prof && tid < kPProf) a.prof[(size_t)blockIdx.x * kPProf + tid] = sh.prof[tid];
+  // final cluster state (wave 0's registers)
+  if (wv == 0 && !sh.stop && lane < ns) store_node(rp.nodes + rank2idx[lo + lane], rec);
 }
 
 }  // namespace ksim_pmemo
