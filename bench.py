@@ -118,6 +118,38 @@ def cpu_baseline(trace, seed, threads):
                                                                                os.cpu_count(), cpu_model()))
 
 
+def _c2_worker(seed):
+    """One C2 replica on the oracle, single-threaded, replayed to completion (cpu_baseline_replicas)."""
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import helpers
+    import pyoracle as O
+    t = ksim.Trace.openb("default")
+    rp = t.replay(seed=seed, tune_ratio=1.3, shuffle=True)
+    nodes, tp, ev = helpers.oracle_nodes(t, rp), helpers.oracle_typical(t), helpers.oracle_events(t, rp)
+    t0 = time.perf_counter()
+    O.run_events(nodes, tp, ev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=1)
+    return len(ev), time.perf_counter() - t0
+
+
+def cpu_baseline_replicas(seeds):
+    """SURVEY §8(d)(iii) for C2, like for like with the GPU line: the same seeds as independent
+    single-threaded oracle processes, one core each (the reference runs replicas as separate simon
+    processes), every replica replayed to completion."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    t0 = time.perf_counter()
+    with cf.ProcessPoolExecutor(max_workers=len(seeds), mp_context=mp.get_context("spawn")) as ex:
+        out = list(ex.map(_c2_worker, seeds))
+    wall = time.perf_counter() - t0
+    events = sum(o[0] for o in out)
+    slowest = max(o[1] for o in out)
+    return dict(value=events / slowest, unit="pods/s", cores=len(seeds), kind="port", wall_s=wall,
+                sample="the bench's %d seeds (openb default, FGD, tune 1.3) replayed to completion (%d events) as %d "
+                       "single-threaded oracle processes, one core each; value = events / the slowest replica's "
+                       "replay time (process start-up and trace loads excluded); host nproc=%d, cpu %s"
+                       % (len(seeds), events, len(seeds), os.cpu_count(), cpu_model()))
+
+
 # paper-sweep policy directories -> the oracle's (policy, gpu selection) (tests/test_gpu_parity.py)
 ORACLE_POLICY = {"01-Random": ("POL_RANDOM", "SEL_RANDOM"), "02-DotProd": ("POL_DOTPROD", "SEL_BEST"),
                  "03-GpuClustering": ("POL_CLUSTERING", "SEL_BEST"), "04-GpuPacking": ("POL_PACKING", "SEL_BEST"),
@@ -392,7 +424,12 @@ def main():
     if args.config == "c4" or args.report:
         line["report_ms_per_step"] = eng.last_report_ms()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        line["cpu_baseline"] = cpu_baseline(trace, seeds[0], args.cpu_threads)
+        # like for like: the GPU line's seeds as single-threaded replicas on as many cores; beside it one
+        # replica with `cpu_threads` workers per cycle (parallelize.Until) and one thread on a prefix
+        one = cpu_baseline(trace, seeds[0], args.cpu_threads)
+        line["cpu_baseline"] = cpu_baseline_replicas(seeds)
+        line["cpu_baseline"]["one_replica_threaded"] = {k: one[k] for k in ("value", "unit", "cores", "sample")}
+        line["cpu_baseline"]["single_thread"] = one["single_thread"]
     if sweep_cpu is not None:
         line["cpu_baseline"] = sweep_cpu
     if rank == 0:
