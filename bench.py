@@ -423,6 +423,7 @@ def main():
         line["config"]["parity"] = "unpinned (node-order contract, DESIGN.md §4)"
     if args.config == "c4" or args.report:
         line["report_ms_per_step"] = eng.last_report_ms()
+    line["build_id"] = ksim.build_id()  # sha256 prefix of the library's sources (ksim.source_hash())
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         # like for like: the GPU line's seeds as single-threaded replicas on as many cores; beside it one
         # replica with `cpu_threads` workers per cycle (parallelize.Until) and one thread on a prefix

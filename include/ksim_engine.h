@@ -221,6 +221,8 @@ typedef struct {
 
 const char* ksim_strerror(int code);
 int  ksim_abi_version(void);
+/* sha256 prefix (16 hex digits) of the sources this library was built from (Makefile HASH_SRCS). */
+const char* ksim_build_id(void);
 int  ksim_device_count(void);      /* gfx950 devices visible; 0 when none */
 
 /* Lifecycle.  n_replicas independent clusters of n_nodes each share one device. */

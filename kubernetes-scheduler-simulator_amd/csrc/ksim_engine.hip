@@ -2608,6 +2608,11 @@ const char* ksim_strerror(int code) {
 
 int ksim_abi_version(void) { return KSIM_ABI_VERSION; }
 
+#ifndef KSIM_SOURCE_HASH
+#define KSIM_SOURCE_HASH "unknown"
+#endif
+const char* ksim_build_id(void) { return KSIM_SOURCE_HASH; }
+
 int ksim_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

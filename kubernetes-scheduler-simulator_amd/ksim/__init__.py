@@ -138,6 +138,7 @@ _VP = C.c_void_p
 SIGNATURES = {
     "ksim_strerror": (C.c_char_p, [C.c_int]),
     "ksim_abi_version": (C.c_int, []),
+    "ksim_build_id": (C.c_char_p, []),
     "ksim_device_count": (C.c_int, []),
     "ksim_engine_create": (C.c_int, [_P(Config), C.c_int, C.c_int, _P(_VP)]),
     "ksim_engine_destroy": (None, [_VP]),
@@ -220,6 +221,31 @@ def check(rc, what):
 
 def device_count():
     return lib().ksim_device_count()
+
+
+def build_id():
+    """sha256 prefix of the sources the loaded library was built from (Makefile HASH_SRCS)."""
+    return lib().ksim_build_id().decode()
+
+
+def source_hash():
+    """The same prefix computed from the sources in this tree (equal to build_id() unless the library is stale)."""
+    import hashlib
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mk = open(os.path.join(pkg, "Makefile")).read()
+    var = {}
+    for line in mk.splitlines():
+        for name in ("DEV_HDRS", "HASH_SRCS"):
+            if line.startswith(name + " :="):
+                var[name] = line.split(":=", 1)[1].split()
+    files = []
+    for f in var["HASH_SRCS"]:
+        files += var["DEV_HDRS"] if f == "$(DEV_HDRS)" else [f]
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 GO_INT63, GO_INTN, GO_FLOAT64, GO_PERM, GO_SHUFFLE = range(5)

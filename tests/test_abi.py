@@ -111,3 +111,8 @@ def test_integration_points_to_go_shim():
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert "go/ksim_gpu.go" in doc
     assert "```go" not in doc  # the code lives in the file, not in the document
+
+
+def test_library_built_from_this_tree():
+    # the prebuilt libksim_hip.so travels to the GPU box untracked: it must be the build of these sources
+    assert ksim.build_id() == ksim.source_hash(), "libksim_hip.so is stale: rebuild (make -C kubernetes-scheduler-simulator_amd)"
