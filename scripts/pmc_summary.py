@@ -30,8 +30,8 @@ def rows(pattern):
 
 def kernel_of(name):
     """Kernel family from a (mangled or demangled) name: k_memo, k_hmemo, k_replay<policy>, ..."""
-    for k in ("k_hinit_gk", "k_hinit_keys", "k_hmemo", "k_memo_finish", "k_memo", "k_random_go", "k_report_delta", "k_report_scan",
-              "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance"):
+    for k in ("k_hinit_gk", "k_hinit_keys", "k_hmemo", "k_memo_finish", "k_pmemo", "k_memo", "k_random_go", "k_report_delta", "k_report_scan",
+              "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance", "k_scan1"):
         if k in name:
             return k
     if "k_replay" in name:

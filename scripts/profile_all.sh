@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter passes for the bench configurations named on the command line (profile_key() in bench.py):
 #   bash scripts/profile_all.sh c2 c2-rm5 c2-BestFit c4 c5
-# each -> gpurun_out/prof/<name>/{pmc.json,kernel_stats.csv,*.log}; copy them to profiles/r02/prof/.
+# each -> gpurun_out/prof/<name>/{pmc.json,kernel_stats.csv,*.log}; copy them to profiles/r03/prof/.
 set -u
 cd "$(dirname "$0")/.."
 for name in "$@"; do
@@ -9,6 +9,7 @@ for name in "$@"; do
     c2) a="";;
     c2-rm5) a="--run-mode 5";;
     c2-rm2) a="--run-mode 2";;
+    c2-rm6) a="--run-mode 6";;
     c2-BestFit) a="--policy BestFit";;
     c2-PWR) a="--policy PWR";;
     c2-PWR_500_FGD_500) a="--policy PWR_500_FGD_500";;
