@@ -2123,6 +2123,10 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ma.decider = pl.decider ? 1 : 0;
   ma.ev_cls = e->d_m_evcls;
   ma.topg = e->d_topg;
+  {
+    const char* sk = std::getenv("KSIM_SKIP");
+    ma.skip = !(sk && sk[0] == '0');
+  }
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   const bool tracing = pe && pe[0] == '2';

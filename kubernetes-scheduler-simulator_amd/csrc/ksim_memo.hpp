@@ -47,6 +47,7 @@ constexpr int kFoldStride = 66;
 constexpr int kFoldBuf = kFoldRows * kFoldStride;  // doubles per evaluating wave
 constexpr int kEvBuf = 128;
 constexpr unsigned kSpinLimit = 1u << 22;
+constexpr int kMaxDeadWords = 32;  // dead-class bitmask: class ids < 1024
 // Decider mode (MemoArgs::decider): class owners publish, for event s, the top kTopN keys of its
 // class and its feasible count as of kLag events earlier; the decider adds the <= kLag nodes
 // changed since.
@@ -78,6 +79,7 @@ struct MemoArgs {
   int decider;
   const int* ev_cls;         // [launch replica][win_stride] class of each event, -1 delete
   unsigned* topg;            // [launch replica][win_stride][kTopWords] top granules, zeroed before launch
+  int skip;                  // lean launches: the dead-class skip (KSIM_SKIP=0: off)
 };
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
                                  // 14 step-start loads, 15 owner's A, 16-20 owner's A split (wave 0)
@@ -86,6 +88,7 @@ struct __align__(16) MemoShared {
   PodDev ev[kEvBuf];
   int evo[kEvBuf + 8];  // owner code of each staged event (+ the next window's first): workgroup << 16 |
                         // first slot of its group << 8 | slot; -1 delete
+  unsigned dead[kMaxDeadWords];  // lean launches: classes with no feasible node (create-only: for good)
   PodDev cls[kMaxCw];
   TypDev tp[kMaxTypical];
   NodeRec dnode;      // the record of the node the previous event changed (d)
@@ -128,7 +131,8 @@ KSIM_HD int key32_gpu(unsigned k) {
   return gf ? 15 - gf : -1;
 }
 
-// Granule of step s: bit 0 written | [23:8] rank + 1 (0: nothing bound) | [31:24] GPU mask.
+// Granule of step s: bit 0 written | bit 1 no feasible node | [23:8] rank + 1 (0: nothing bound) |
+// [31:24] GPU mask.
 KSIM_HD unsigned pack_pay(int rank, int mask) {
   return 1u | ((unsigned)(rank + 1) << 8) | ((unsigned)(mask & 0xff) << 24);
 }
@@ -741,6 +745,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   unsigned* win = a.win + (size_t)gi * a.win_stride;
   const int* evo = a.ev_owner + (size_t)gi * a.win_stride;
   const bool is_w0 = w == 0;
+  constexpr bool kSkip = !kDecider && !kGeneral;  // the dead-class skip (create-only streams)
+  const bool skip_ok = kSkip && a.skip && a.Cmax <= kMaxDeadWords * 32;
 
   // ---- start-up: the cluster in rank order, the owned classes, the typical table
   for (int i = tid; i < N; i += kMBlock) {
@@ -759,6 +765,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   for (int i = tid; i < rp.nt * 2; i += kMBlock)
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; sh.crit_done = 0; }
+  for (int i = tid; i < kMaxDeadWords; i += kMBlock) sh.dead[i] = 0u;
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
   const bool prof = kGeneral && a.prof != nullptr;
   unsigned long long* const trace = kGeneral ? a.trace : nullptr;
@@ -891,6 +898,27 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       for (int i = tid; i <= ne + kLag; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
       __syncthreads();
     }
+    // Dead-class skip (lean launches, create-only streams): Filter is monotone in a node's resources and a
+    // creation only takes resources, so once an event found no feasible node (its granule says so), every
+    // later event of its class finds none either -- unscheduled, 0 feasible, nothing changes.  Every
+    // workgroup holds the same dead set (updated from the same granules), so all skip the same steps;
+    // the dirty node is carried to the next decided step, and the owner of the next event's class
+    // still precomputes its top-2 (with the dirty node excluded there, as on any step).
+    if constexpr (kSkip) {
+      const int cls = __builtin_amdgcn_readfirstlane(sh.ev[eb].pad);  // the event's class (load_events)
+      if (skip_ok && ((sh.dead[cls >> 5] >> (cls & 31)) & 1u)) {
+        if (is_w0 && tid == 0) gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
+        if (step + 1 < rp.n_events) {
+          const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + 1]);
+          if (ocn >= 0 && (ocn >> 16) == w) {
+            __syncthreads();
+            top2(ocn & 0xff);
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+    }
     if (trace && tid == 0 && step < a.trace_steps)
       trace[((size_t)blockIdx.x * a.trace_steps + step) * 4] = __builtin_amdgcn_s_memrealtime();
     // one LDS round trip: the event, its owner code, d and d's record
@@ -1022,7 +1050,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       // Reserve (open_gpu_share.go:178-205) on the winner: d's record is in registers
       const int gW = key32_gpu(W);
       const int mask = W == 0u ? -1 : (W == ex ? mask_ex : (d_gpu_from_key ? (gW < 0 ? -1 : 1 << gW) : mask_d_pre));
-      const unsigned pay = (W != 0u && mask >= 0) ? pack_pay(rk, mask) : 1u;
+      // bit 1: no feasible node at all (W == 0), as opposed to a Reserve failure on the winner
+      const unsigned pay = (W != 0u && mask >= 0) ? pack_pay(rk, mask) : (W == 0u ? 3u : 1u);
       if (lane == 0) {
         gstore32(win + step, pay);
         asm volatile("" ::: "memory");
@@ -1152,6 +1181,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
       }
       int nd = -1;
+      if (kSkip && skip_ok && ok && (pay & 2u))  // this event's class has no feasible node, for good
+        sh.dead[p.pad >> 5] |= 1u << (p.pad & 31);
       if (!ok) {
         sh.stop = 1;
         atomicOr(a.fail, 1);
