@@ -2277,6 +2277,8 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
   return KSIM_OK;
 }
 
+static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps);
+
 // k_hmemo's arguments for the planned launch (one group of Rg replicas from d_replist + first).
 static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   using namespace ksim_hmemo;
@@ -2312,6 +2314,11 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   ma.tp = e->d_tp;
   ma.npeer = 0;
   ma.epoch = 0;
+  {
+    std::vector<int> all(e->R);
+    std::iota(all.begin(), all.end(), 0);
+    ma.skip = dead_skip(e, all) ? 1 : 0;
+  }
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }
@@ -3432,6 +3439,18 @@ static size_t replay_lds(int S, int pol, bool general) {  // S real slots + the 
 }
 
 
+// The dead-class skip (k_memo, k_hmemo, k_scan1): on create-only streams a class that once found no
+// feasible node never finds one again (Filter is monotone in the resources a creation takes), so its
+// later events are decided without a scan.  Needs every replica create-only with class ids < 1024;
+// KSIM_SKIP=0 turns it off (A/B runs).
+static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps) {
+  const char* sk = std::getenv("KSIM_SKIP");
+  if (sk && sk[0] == '0') return false;
+  for (int r : reps)
+    if (e->has_delete[r] || e->h_cls[r].size() > 1024) return false;
+  return true;
+}
+
 // One k_replay launch per policy present (the kernel is specialised on the policy);
 // launches of different policies run back to back on the engine stream.
 constexpr int kPolRandomGo = 64;  // run_persistent's group id of the k_random_go replicas
@@ -3581,7 +3600,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg) <= 160 * 1024) {
       const void* f = scan1_fn(gp.first, e->report, reg);
       const size_t lds = ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg);
-      ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N};
+      ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N,
+                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0};
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       void* params[] = {(void*)&sa};
       KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));

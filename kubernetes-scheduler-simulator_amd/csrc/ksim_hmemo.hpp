@@ -105,6 +105,7 @@ struct HMemoArgs {
   // wrote).  npeer = 0: the exchange buffer is shared in place (one launch).
   int npeer, epoch;
   unsigned long long* peer[kMaxPeers];
+  int skip;                 // the dead-class skip (create-only streams; class slots < 1024)
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -120,6 +121,7 @@ struct __align__(16) HShared {
   int stop;            // K > 1: a poll timed out, every workgroup leaves its loop
   int pad_[3];
   unsigned long long prof[kHProf];
+  unsigned dead[32];   // class slots with no feasible node (create-only streams: for good)
 };
 static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned");
 
@@ -292,6 +294,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
   if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; sh.stop = 0; }
+  for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
   unsigned long long t_last = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -315,6 +318,18 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       for (int i = tid; i < ne * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
       for (int i = tid; i < ne; i += kHBlock) sh.evc[i] = gget(evc + step + i);
       __syncthreads();
+    }
+    // Dead-class skip (create-only streams): Filter is monotone in the resources a creation takes, so an
+    // event whose class found no feasible node before finds none now -- unscheduled, 0 feasible, nothing
+    // changes.  Every workgroup (every shard) holds the same dead set, taken from the same exchanges, so
+    // all skip the same steps; the changed node d is carried to the next decided step's refresh.
+    {
+      const int cs0 = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
+      if (a.skip && cs0 >= 0 && ((sh.dead[cs0 >> 5] >> (cs0 & 31)) & 1u)) {
+        if (w == 0 && tid == 0) gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
+        __syncthreads();
+        continue;
+      }
     }
     const int d = __builtin_amdgcn_readfirstlane(sh.d);  // changed rank in this slice, -1 none
     if (d >= 0) {
@@ -553,6 +568,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         }
         out = ResultDev{-1, 0, 0, nfeas, ST_UNSCHED};
         write = W == 0u && w == 0;  // nobody feasible: workgroup 0 reports
+        if (a.skip && W == 0u && lane == 0) sh.dead[cs >> 5] |= 1u << (cs & 31);  // for good (create-only)
         uint8_t h = 3;
         if (W != 0u) {
           const int wr = hkey_rank(W) - roff;  // the winner's rank in this shard

@@ -33,7 +33,9 @@ struct Scan1Args {
   ReplicaDev* reps;
   const int* rep_list;  // replica of each workgroup
   int N;
+  int skip;             // the dead-class skip (every replica's classes fit kDeadWords x 32 bits)
 };
+constexpr int kDeadWords = 32;  // dead-class bitmask: class ids < 1024
 
 struct __align__(16) Scan1Part {
   unsigned long long key;  // the wave's best packed key (0: nothing feasible)
@@ -45,7 +47,8 @@ struct __align__(16) Scan1Part {
 
 struct __align__(16) Scan1Shared {
   PodDev ev[kEvBuf];
-  Scan1Part part[2][kWaves];  // by step parity: a wave may write step s+1's while another reads step s's
+  Scan1Part part[2][kWaves];  // by decided-step parity: a wave may write step s+1's while another reads step s's
+  unsigned dead[kWaves][kDeadWords];  // each wave's copy of the dead classes (every wave decides alike)
 };
 static_assert(sizeof(Scan1Shared) % 16 == 0, "keep the node records 16-B aligned");
 
@@ -95,17 +98,29 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     for (int i = tid; i < N * kTagStride; i += kBlock) s_tags[i] = rp.tags[i];
   if (kReport)
     for (int i = tid; i < N; i += kBlock) s_last[i] = -1;
+  for (int i = tid; i < kWaves * kDeadWords; i += kBlock) (&sh.dead[0][0])[i] = 0u;
+  unsigned* dead = sh.dead[wv];
+  int nd = 0;  // decided (not skipped) steps so far: the partial table's parity
+  __syncthreads();
 
   for (int step = 0; step < rp.n_events; ++step) {
     const int eb = step & (kEvBuf - 1);
     if (eb == 0) {
-      // every thread has passed the previous step's barrier, so nobody reads the old window
+      // skipped steps have no barrier: wait until no wave reads the old window any more
+      if (step > 0) __syncthreads();
       const int nl = min(kEvBuf, rp.n_events - step) * 2;
       const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
       for (int i = tid; i < nl; i += kBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
       __syncthreads();
     }
     const PodDev p = uniform_pod(&sh.ev[eb]);
+    // Dead-class skip (create-only streams): Filter is monotone in the resources a creation takes, so an
+    // event whose class found no feasible node before finds none now -- unscheduled, 0 feasible, nothing
+    // changes.  Every wave keeps its own copy of the dead set and decides alike, so no barrier is needed.
+    if (a.skip && ((dead[p.pad >> 5] >> (p.pad & 31)) & 1u)) {
+      if (tid == 0) rp.res[step] = ResultDev{-1, 0, 0, 0, ST_UNSCHED};
+      continue;
+    }
     // ---- scan: Filter + Score of this thread's slots
     unsigned long long best = 0ull;
     int cnt = 0, lo = 0x7fffffff, hi = -1;
@@ -134,7 +149,8 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     cnt = wave_sum_dpp(cnt);
     const bool werr = __any(err);
     if (kMinMax) { lo = wave_min_dpp(lo); hi = wave_max_dpp(hi); }
-    Scan1Part* pt = sh.part[step & 1];
+    Scan1Part* pt = sh.part[nd & 1];
+    ++nd;
     if (lane == 0) pt[wv] = Scan1Part{best, cnt, werr ? 1 : 0, lo, hi, {0, 0}};
     __syncthreads();
     // ---- the cycle decision, by every wave (the same values): k_replay's commit at K = 1
@@ -148,6 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
       gerr |= q.err;
       if (kMinMax) { glo = min(glo, q.lo); ghi = max(ghi, q.hi); }
     }
+    if (a.skip && nfeas == 0 && lane == 0) dead[p.pad >> 5] |= 1u << (p.pad & 31);
     const int loc = key_loc(W);
     const int owner = W != 0ull ? (loc % kBlock) / 64 : 0;  // the wave that scans the winner's slot
     if (wv == owner) {
