@@ -759,9 +759,10 @@ void k_replay(ksim_replay::ReplayArgs a,
     sh.agg_hi = kPF ? INT_MIN : -1;
   };
   if (tid == 0) { sh.stop = 0; sh.nitems = 0; sh.pend_valid = 0; sh.pend_b = -1; reset_agg(); }
+  for (int i = tid; i < 32; i += kRBlock) sh.dead[i] = 0u;
 
   // wave 0's copy of the pending exchange (the previous pod step, published, not committed)
-  int p_step = 0, p_seq = 0, p_b = -1, p_mask = -1, seq = 0;
+  int p_step = 0, p_seq = 0, p_b = -1, p_mask = -1, seq = 0, p_cls = 0;
   int p_tag = -1;  // the pending Bind's affinity tag (policies keeping the tag counts in HBM)
   unsigned long long p_key = 0ull;
   int p_st0 = 0, p_st1 = 0, p_st2 = 0, p_st3 = 0;  // K == 1: the step's own totals
@@ -906,6 +907,8 @@ void k_replay(ksim_replay::ReplayArgs a,
   // into that node (Reserve + Bind were applied to it when it was prepared).  Lanes 0-6 copy.
   auto commit = [&](unsigned long long W, int nfeas, int gerr, int glo, int ghi) {
     const bool owner = W != 0ull && W == p_key;
+    // nothing feasible anywhere: the pending event's class stays infeasible (create-only streams)
+    if (a.skip && nfeas == 0 && lane == 0) sh.dead[p_cls >> 5] |= 1u << (p_cls & 31);
     ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
     int2 hrec = make_int2(-1, 0);
     bool writer = w == 0;
@@ -979,6 +982,17 @@ void k_replay(ksim_replay::ReplayArgs a,
     const PodDev p = uniform_pod(&sh.ev[eb]);
     const int2 pvb = *reinterpret_cast<const int2*>(&sh.pend_valid);
     const bool pend = __builtin_amdgcn_readfirstlane(pvb.x) != 0;
+    // Dead-class skip (create-only streams): Filter is monotone in the resources a creation takes, so an
+    // event whose class found no feasible node before finds none now -- unscheduled, 0 feasible, nothing
+    // changes.  The pending step is finished first (its commit may add to the dead set); every workgroup
+    // marks the same classes at the same commit, so all skip the same steps.
+    if (a.skip && ((sh.dead[p.pad >> 5] >> (p.pad & 31)) & 1u)) {
+      if (pend) finish_pending();
+      if (sh.stop) break;
+      if (tid == 0 && w == 0) rp.res[step] = ResultDev{-1, 0, 0, 0, ST_UNSCHED};
+      __syncthreads();
+      continue;
+    }
     if (kGeneral && (p.flags & kPodDelete)) {  // lean: launched on create-only streams
       if (pend) finish_pending();
       if (sh.stop) break;
@@ -1295,6 +1309,7 @@ void k_replay(ksim_replay::ReplayArgs a,
           }
         }
         p_step = step;
+        p_cls = p.pad;
         p_seq = seq;
         p_b = mk != 0ull ? mloc : -1;
         p_key = mk;
@@ -1368,6 +1383,7 @@ void k_replay(ksim_replay::ReplayArgs a,
           }
         }
         p_step = step;
+        p_cls = p.pad;
         p_seq = seq;
         p_b = mk != 0ull ? mloc : -1;
         p_key = mk;
@@ -3647,6 +3663,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     ra.hist_stride = std::max(max_ev, 1);
     ra.fail = e->d_fail;
     ra.prof = nullptr;
+    ra.skip = dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0;
     if (profile) {
       const size_t words = (size_t)Rg * K * ksim_replay::kProfPhases;
       if (words > e->prof_cap) {

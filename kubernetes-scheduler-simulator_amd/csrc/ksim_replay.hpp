@@ -61,6 +61,7 @@ struct ReplayArgs {
   int hist_stride;
   int* fail;
   unsigned long long* prof;  // optional [R*K][8] s_memrealtime phase sums (KSIM_PROFILE=1), else null
+  int skip;                  // the dead-class skip (create-only streams; class ids < 1024)
 };
 constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 
@@ -90,6 +91,7 @@ struct __align__(16) ReplayShared {
   unsigned long long prof[kProfPhases];  // KSIM_PROFILE phase sums (thread 0)
   unsigned long long prof_pad[4];
   PowerDev pw;                  // PWR policies: the replica's energy model
+  unsigned dead[32];            // classes with no feasible node (create-only streams: for good)
 };
 static_assert(sizeof(ReplayShared) % 16 == 0, "keep the node records 16-B aligned");
 
