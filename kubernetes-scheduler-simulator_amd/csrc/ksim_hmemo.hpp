@@ -326,8 +326,22 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     {
       const int cs0 = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
       if (a.skip && cs0 >= 0 && ((sh.dead[cs0 >> 5] >> (cs0 & 31)) & 1u)) {
-        if (w == 0 && tid == 0) gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
+        // the whole run of dead events up to the next live one (or the window's end) at once
+        const int wend = min(kEvBuf, rp.n_events - (step - eb));
+        int run = wend - eb;
+        for (int j0 = eb + 1; j0 < wend; j0 += 64) {
+          const int j = j0 + lane;
+          const int c = j < wend ? sh.evc[j] : 0;
+          const unsigned long long lb = __ballot(j < wend && (c < 0 || !((sh.dead[c >> 5] >> (c & 31)) & 1u)));
+          if (lb) {
+            run = j0 + (int)__builtin_ctzll(lb) - eb;
+            break;
+          }
+        }
+        if (w == 0)
+          for (int i = tid; i < run; i += kHBlock) gput(rp.res + step + i, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
         __syncthreads();
+        step += run - 1;
         continue;
       }
     }

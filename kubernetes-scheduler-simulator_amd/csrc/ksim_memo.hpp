@@ -907,15 +907,30 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     if constexpr (kSkip) {
       const int cls = __builtin_amdgcn_readfirstlane(sh.ev[eb].pad);  // the event's class (load_events)
       if (skip_ok && ((sh.dead[cls >> 5] >> (cls & 31)) & 1u)) {
-        if (is_w0 && tid == 0) gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
-        if (step + 1 < rp.n_events) {
-          const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + 1]);
+        // the whole run of dead events up to the next live one (or the window's end) at once: the dead
+        // set cannot change inside the run; every wave finds the same run
+        const int wend = min(kEvBuf, rp.n_events - (step - eb));
+        int run = wend - eb;
+        for (int j0 = eb + 1; j0 < wend; j0 += 64) {
+          const int j = j0 + lane;
+          const int c = j < wend ? sh.ev[j].pad : 0;
+          const unsigned long long lb = __ballot(j < wend && !((sh.dead[c >> 5] >> (c & 31)) & 1u));
+          if (lb) {
+            run = j0 + (int)__builtin_ctzll(lb) - eb;
+            break;
+          }
+        }
+        if (is_w0)
+          for (int i = tid; i < run; i += kMBlock) gput(rp.res + step + i, ResultDev{-1, 0, 0, 0, ST_UNSCHED});
+        if (step + run < rp.n_events) {  // the next event's owner precomputes its class's top-2
+          const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + run]);
           if (ocn >= 0 && (ocn >> 16) == w) {
             __syncthreads();
             top2(ocn & 0xff);
           }
         }
         __syncthreads();
+        step += run - 1;
         continue;
       }
     }
