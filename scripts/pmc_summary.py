@@ -31,9 +31,12 @@ def rows(pattern):
 def kernel_of(name):
     """Kernel family from a (mangled or demangled) name: k_memo, k_hmemo, k_replay<policy>, ..."""
     for k in ("k_hinit_gk", "k_hinit_keys", "k_hmemo", "k_memo_finish", "k_pmemo", "k_memo", "k_random_go", "k_report_delta", "k_report_scan",
-              "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance", "k_scan1"):
+              "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance"):
         if k in name:
             return k
+    if "k_scan1" in name:
+        m = re.search(r"k_scan1<(\d+)", name) or re.search(r"k_scan1ILi(\d+)E", name)
+        return "k_scan1<%s>" % (m.group(1) if m else "?")
     if "k_replay" in name:
         m = re.search(r"k_replay<(\d+)", name) or re.search(r"k_replayILi(\d+)E", name)
         return "k_replay<%s>" % (m.group(1) if m else "?")
