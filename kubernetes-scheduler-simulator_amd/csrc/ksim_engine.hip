@@ -2384,8 +2384,12 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     const int nwg = Rg * pl.K;
     std::vector<unsigned long long> h((size_t)nwg * kHProf);
     KSIM_HIP(hipMemcpy(h.data(), e->d_h_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    static const char* names[] = {"list | class pass", "(wave 0 F, inside the next)", "F + flagged blocks", "-", "-",
-                                   "class update | decide+bind"};
+    // waves 1-15 (the bulk: every class but the event's own): 0 + 2 on the F waves, 4 on the class
+    // waves beside them, then 3; wave 0: 1 (the own class's refresh, the critical path), 5 (the rest of
+    // its step: decide + Bind, then the end-of-step barrier)
+    static const char* names[] = {"bulk: list (wave 1)", "critical own-class refresh", "bulk: F (F waves)",
+                                   "bulk: join + class update", "class waves: class pass + flagged blocks",
+                                   "wave 0 decide+bind+wait"};
     std::fprintf(stderr, "ksim hmemo profile: %d replicas x K=%d (S %d), LDS %zu B, Cmax %d Gmax %d Smax %d; us/step mean [max]:",
                  Rg, pl.K, pl.S, pl.lds, pl.Cmax, pl.Gmax, pl.Smax);
     const double steps = std::max(max_ev, 1);
@@ -3753,7 +3757,8 @@ int ksim_engine_run(ksim_engine* e) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
     if (fail & 2) return KSIM_ERANGE;  // a raw PWR score outside the 24-bit key field
-    if (fail) return KSIM_ESTATE;  // a granule poll timed out (workgroups not co-resident)
+    if (fail & ~3) std::fprintf(stderr, "ksim: a k_hmemo bulk wait timed out (fail bits 0x%x)\n", fail);
+    if (fail) return KSIM_ESTATE;  // a granule poll or an LDS wait timed out
   }
   return KSIM_OK;
 }

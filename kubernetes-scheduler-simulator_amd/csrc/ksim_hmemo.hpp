@@ -53,6 +53,8 @@ constexpr int kMaxItems = 1 + 8 * kMaxGroups;
 constexpr int kEvBuf = 128;
 constexpr int kQuarters = kHBlock / 16;
 constexpr int kMaxPeers = 16;  // shard processes of a device exchange (ksim_engine_set_shard: world <= 16)
+constexpr int kFW = 7;                 // F waves of the bulk refresh (1..kFW: 112 quads, one listed state each)
+constexpr int kCW = kHWaves - 1 - kFW; // class waves (kFW+1..15)
 
 // Packed key of (class, node): [30:24] score + 1 | [23:4] kHRankMax - rank | [3:0] gpu field
 // (15 - g for a share pod placed on GPU g, 0 otherwise).  0 = infeasible.  Max key = max score,
@@ -114,12 +116,17 @@ struct __align__(16) HShared {
   int evc[kEvBuf];
   TypDev tp[kMaxTypical];
   double th[104];
-  NodeRec dold, dnew;  // the node the previous event changed: record before / after
-  int d;               // its rank, -1 none
-  unsigned dfirst;     // first_of_class(dnew, 0)
+  // The node the previous decided event changed (record before / after, its rank or -1, first_of_class
+  // of the new record), double-buffered: the bulk reads [cur] while wave 0's decision writes [cur ^ 1].
+  NodeRec dold[2], dnew[2];
+  int d[2];
+  unsigned dfirst[2];
   int nitems, nflag;
   int stop;            // K > 1: a poll timed out, every workgroup leaves its loop
-  int pad_[3];
+  int bar;             // the bulk waves' barrier counter
+  int cbar;            // the class waves' barrier counter
+  int lseq;            // the F list's hand-over: refreshes listed so far
+  int pad_[2];
   unsigned long long prof[kHProf];
   unsigned dead[32];   // class slots with no feasible node (create-only streams: for good)
 };
@@ -255,12 +262,12 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int* s_cnt = reinterpret_cast<int*>(smem + L.cnt);
   unsigned* s_bx = reinterpret_cast<unsigned*>(smem + L.bx);
   uint16_t* s_cgrp = reinterpret_cast<uint16_t*>(smem + L.cgrp);
-  uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
   uint8_t* s_code = reinterpret_cast<uint8_t*>(smem + L.code);
   uint8_t* s_igrp = reinterpret_cast<uint8_t*>(smem + L.igrp);
   uint8_t* s_fnew = reinterpret_cast<uint8_t*>(smem + L.fnew);
   uint8_t* s_fold = reinterpret_cast<uint8_t*>(smem + L.fold);
   int16_t* s_gbase = reinterpret_cast<int16_t*>(smem + L.gbase);
+  uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
   const int* evc = a.evc + (size_t)gi * a.stride;
@@ -293,7 +300,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     s_l1[i] = b0 + i % nb < a.nb ? a.l1[((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb] : 0u;
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
-  if (tid == 0) { sh.d = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst = 0u; sh.stop = 0; }
+  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; }
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
@@ -307,7 +314,33 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     }
   };
   __syncthreads();
+  // the bulk waves' phase timer (thread 64)
+  unsigned long long tb_last = t_last;
+  auto bmark = [&](int ph) {
+    if (prof && tid == 64) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      sh.prof[ph] += t - tb_last;
+      tb_last = t;
+    }
+  };
   const bool typed = rp.typed != 0;
+  int cur = 0;         // the d-record buffer of this step (toggled at the end of every decided step)
+  int bar_target = 0;  // the bulk barrier's count so far (waves 1-15)
+  int cbar_target = 0; // the class waves' barrier count so far
+  int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..kFW)
+  // A bounded wait on one of the bulk's LDS counters (lane 0 of a wave): past the limit the workgroup
+  // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over) instead of hanging.
+  auto spin_until = [&](int* ctr, int target, int bit) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+      if (++spins > 4 * ksim_replay::kSpinLimit) {
+        atomicOr(a.fail, bit);
+        __hip_atomic_store(&sh.stop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(0);
+    }
+  };
   int seq = 0;  // K > 1: exchanges so far (wave 0; every workgroup sees the same events)
 
   for (int step = 0; step < rp.n_events; ++step) {
@@ -345,59 +378,105 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         continue;
       }
     }
-    const int d = __builtin_amdgcn_readfirstlane(sh.d);  // changed rank in this slice, -1 none
-    if (d >= 0) {
-      const NodeV dn = uniform_node(&sh.dnew);
+    const int d = __builtin_amdgcn_readfirstlane(sh.d[cur]);  // changed rank in this slice, -1 none
+    const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);  // the event's class, -1 delete
+    const int own = d >= 0 ? cs : -1;                            // the class wave 0 refreshes itself
+    if (d >= 0 && wv != 0) {
+      // ===== the bulk (waves 1-15): every class but the event's own on d, beside wave 0's critical path;
+      //       needed from the next decision on.  Three phases, joined by LDS-counter barriers of these
+      //       15 waves (wave 0 does not stop for them).
+      const NodeV dn = uniform_node(&sh.dnew[cur]);
       const int b = d / kFan - b0;  // the slice's L1 block of d
-      // ---- 1. wave 0: the F list over every score group (d's current state + each group's candidates;
-      //         a group no class admits just goes unused) | waves 1-15: the class pass
-      if (wv == 0) {
-        const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
-        int base = 1;  // item 0: d's current state
-        for (int g0 = 0; g0 < G; g0 += 64) {
-          const int g = g0 + lane;
-          unsigned cm = 0u;
-          bool share = false;
-          if (g < G) {
-            const PodDev gp = s_gpod[g];
-            share = is_share_pod(gp);
-            cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
-          }
-          const int nc = __popc(cm);
-          int excl = 0, tot = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const unsigned long long m = __ballot((nc >> k) & 1);
-            excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << k;
-            tot += __popcll(m) << k;
-          }
-          int o = base + excl;
-          if (g < G) s_gbase[g] = (int16_t)o;
-          unsigned mm = cm;
-          while (mm) {
-            const int x = __builtin_ctz(mm);
-            mm &= mm - 1u;
-            s_code[o] = (uint8_t)(share ? 1 + x : 9);
-            s_igrp[o] = (uint8_t)g;
-            ++o;
-          }
-          base += tot;
-        }
+      const int bt = tid - 64;      // bulk thread
+      if (prof && tid == 64) tb_last = __builtin_amdgcn_s_memrealtime();
+      auto bulk_bar = [&]() {
+        bar_target += kHWaves - 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) {
-          s_code[0] = 0;
-          s_igrp[0] = 0;
-          sh.nitems = base;
+          __hip_atomic_fetch_add(&sh.bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          spin_until(&sh.bar, bar_target, 4);
         }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      };
+      // ---- 1+2. waves 1..kFW: F of every listed state -- wave 1 lists them (d's current state + each
+      //      score group's candidates; a group no class admits just goes unused) and hands the list over
+      //      through an LDS counter, then every quad of these waves evaluates one state (frag_F_quad) --
+      //      beside waves kFW+1..15: the class pass (Filter on d's new and old records; which classes
+      //      had d as the max of d's block: flagged), then the flagged blocks' loads (one quarter-wave
+      //      each) and their maxima without d
+      if (wv <= kFW) {
+        ++list_seq;
+        if (wv == 1) {
+          const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst[cur]);
+          int base = 1;  // item 0: d's current state
+          for (int g0 = 0; g0 < G; g0 += 64) {
+            const int g = g0 + lane;
+            unsigned cm = 0u;
+            bool share = false;
+            if (g < G) {
+              const PodDev gp = s_gpod[g];
+              share = is_share_pod(gp);
+              cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
+            }
+            const int nc = __popc(cm);
+            int excl = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const unsigned long long m = __ballot((nc >> k) & 1);
+              excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << k;
+              tot += __popcll(m) << k;
+            }
+            int o = base + excl;
+            if (g < G) s_gbase[g] = (int16_t)o;
+            unsigned mm = cm;
+            while (mm) {
+              const int x = __builtin_ctz(mm);
+              mm &= mm - 1u;
+              s_code[o] = (uint8_t)(share ? 1 + x : 9);
+              s_igrp[o] = (uint8_t)g;
+              ++o;
+            }
+            base += tot;
+          }
+          if (lane == 0) {
+            s_code[0] = 0;
+            s_igrp[0] = 0;
+            sh.nitems = base;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __hip_atomic_store(&sh.lseq, list_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          bmark(0);
+        } else {
+          if (lane == 0) spin_until(&sh.lseq, list_seq, 16);
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+        const int q = bt & 3;
+        for (int j = bt >> 2; j < nit; j += kFW * 16) {
+          const int code = s_code[j];
+          const PodDev gp = s_gpod[s_igrp[j]];
+          int cpuL, total;
+          uint32_t gs[4];
+          fgd_candidate(dn, code, gp, &cpuL, gs, &total);
+          const uint32_t tb = 1u << dn.gpu_type();
+          const double F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
+                                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          if (q == 0) s_F[j] = F;
+        }
+        if (prof && tid == 64) { sh.prof[7] += (unsigned long long)nit; sh.prof[9] += 1ull; }
+        bmark(2);
       } else {
-        // Filter on d's new and old records (feasible counts), and which classes had d as the max of
-        // d's block (flagged: their block max must be recomputed without d)
-        const NodeV dold = uniform_node(&sh.dold);
+        const int ct = tid - (kFW + 1) * 64;  // class-wave thread
+        const unsigned long long tc0 = (prof && ct == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        const NodeV dold = uniform_node(&sh.dold[cur]);
         const NodeSum sn = node_sum(dn), so = node_sum(dold);
-        for (int c = tid - 64; c < C; c += kHBlock - 64) {
+        for (int c = ct; c < C; c += kCW * 64) {
           const PodDev q = s_cls[c];
           s_fnew[c] = filter_sum(sn, dn, q) ? 1 : 0;
           s_fold[c] = filter_sum(so, dold, q) ? 1 : 0;
-          const unsigned old = s_l1[c * nb + b];
+          const unsigned old = c != own ? s_l1[c * nb + b] : 0u;  // the own class's row is wave 0's
           const bool fl = old != 0u && hkey_rank(old) == roff + d;
           const unsigned long long fm = __ballot(fl);
           if (fm) {
@@ -409,101 +488,133 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
                   (uint16_t)c;
           }
         }
-      }
-      __syncthreads();
-      mark(0);
-      // ---- 2. the flagged blocks' loads (one quarter-wave each, held in registers), F of every listed
-      //         state (one quad each), then the flagged blocks' maxima without d
-      const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
-      const int qid = tid >> 4, l16 = tid & 15;
-      uint4 bv = make_uint4(0u, 0u, 0u, 0u);
-      if (qid < nflag) {
-        const int c = s_flist[qid];
-        bv = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
-      }
-      {
-        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
-        const int q = tid & 3;
-        for (int j = tid >> 2; j < nit; j += kHBlock / 4) {
-          const int code = s_code[j];
-          const PodDev gp = s_gpod[s_igrp[j]];
-          int cpuL, total;
-          uint32_t gs[4];
-          fgd_candidate(dn, code, gp, &cpuL, gs, &total);
-          const uint32_t tb = 1u << dn.gpu_type();
-          const double F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
-                                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
-          if (q == 0) s_F[j] = F;
+        // the class waves' own barrier (LDS counter): every flag is listed
+        cbar_target += kCW;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) {
+          __hip_atomic_fetch_add(&sh.cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          spin_until(&sh.cbar, cbar_target, 8);
         }
-        if (prof && tid == 0) {
-          sh.prof[7] += (unsigned long long)nit; sh.prof[8] += (unsigned long long)nflag; sh.prof[9] += 1ull;
-          sh.prof[1] += __builtin_amdgcn_s_memrealtime() - t_last;  // wave 0's own F evaluations (inside phase 2)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
+        const int qid = ct >> 4, l16 = ct & 15;
+        constexpr int kCQ = kCW * 4;  // quarter-waves of the class waves
+        // two rows per quarter-wave in flight at once, then any further ones one by one
+        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+        const size_t boff = (size_t)(b0 + b) * kFan + 4 * l16;
+        if (qid < nflag) v0 = gld4(keys + (size_t)s_flist[qid] * a.Npad + boff);
+        if (qid + kCQ < nflag) v1 = gld4(keys + (size_t)s_flist[qid + kCQ] * a.Npad + boff);
+        if (qid < nflag) {
+          const unsigned m = block_max_excl(v0, (b0 + b) * kFan, l16, d);
+          if (l16 == 0) s_bx[s_flist[qid]] = m;
         }
+        if (qid + kCQ < nflag) {
+          const unsigned m = block_max_excl(v1, (b0 + b) * kFan, l16, d);
+          if (l16 == 0) s_bx[s_flist[qid + kCQ]] = m;
+        }
+        for (int i = 2 * kCQ + qid; i < nflag; i += kCQ) {
+          const int c = s_flist[i];
+          const uint4 v = gld4(keys + (size_t)c * a.Npad + boff);
+          const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
+          if (l16 == 0) s_bx[c] = m;
+        }
+        if (prof && ct == 0) { sh.prof[8] += (unsigned long long)nflag; sh.prof[4] += __builtin_amdgcn_s_memrealtime() - tc0; }
       }
-      if (qid < nflag) {
-        const unsigned m = block_max_excl(bv, (b0 + b) * kFan, l16, d);
-        if (l16 == 0) s_bx[s_flist[qid]] = m;
-      }
-      for (int i = kQuarters + qid; i < nflag; i += kQuarters) {  // more flagged classes than quarters
-        const int c = s_flist[i];
-        const uint4 v = gld4(keys + (size_t)c * a.Npad + (size_t)(b0 + b) * kFan + 4 * l16);
-        const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
-        if (l16 == 0) s_bx[c] = m;
-      }
-      __syncthreads();
-      mark(2);
-    }
-    // ---- 3 + 4. the class update beside the event: wave 0 updates the event's own class (the only
-    //      one the decision reads) and then decides, while waves 1-15 update every other class
-    const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);  // the event's class, -1 delete
-    const int own = d >= 0 ? cs : -1;                            // the class wave 0 updates itself
-    if (d >= 0) {
-      const int b = d / kFan - b0;
+      bulk_bar();
+      if (tid == 64) sh.nflag = 0;  // (read above, before the barrier; the next class pass adds to it)
+      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+      // ---- 3. every other class's group key on d (score steps of its candidates), key[c][d] (HBM
+      //         store), L1[c][d/64] (max with the new key, or the block max without d when d was the
+      //         block max), the feasible count
       const double F0 = s_F[0];
-      const int nit = sh.nitems;
-      // the group's key on d (if d passes the class's Filter: fn), from its candidates' F
-      auto class_key = [&](int c, bool fn, int i0) -> unsigned {
+      for (int c = bt; c < C; c += kHBlock - 64) {
+        if (c == own) continue;
+        const bool fn = s_fnew[c] != 0;
         unsigned k = 0u;
         if (fn) {
           const int g = s_cgrp[c];
           const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
           if (is_share_pod(s_gpod[g])) {
             k = hkey(0, roff + d, 0);  // feasible with no fitting GPU
-            for (int i = o + (i0 < 0 ? 0 : i0); i < oe; i += (i0 < 0 ? 1 : 64)) {  // i0 < 0: all, serially
+            for (int i = o; i < oe; ++i) {
               const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), roff + d, 15 - (s_code[i] - 1));
               k = x > k ? x : k;
             }
-          } else if (i0 <= 0) {
+          } else {
             k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), roff + d, 0);  // NodeResource.Sub state
           }
         }
-        return k;
-      };
-      // its key, L1 entry and feasible count
-      auto class_store = [&](int c, bool fn, unsigned k) {
         gst1(keys + (size_t)c * a.Npad + d, k);
         s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
         unsigned* l = &s_l1[c * nb + b];
         const unsigned old = *l;
         if (k > old) *l = k;
         else if (old != 0u && hkey_rank(old) == roff + d) *l = k > s_bx[c] ? k : s_bx[c];
-      };
-      if (wv != 0) {
-        for (int c = tid - 64; c < C; c += kHBlock - 64) {
-          if (c == own) continue;
-          const bool fn = s_fnew[c] != 0;
-          class_store(c, fn, class_key(c, fn, -1));
-        }
-      } else if (own >= 0) {
-        // lane i scores candidate i of the group (<= 8), the wave keeps the max; lane 0 stores
-        const bool fn = s_fnew[own] != 0;
-        const unsigned k = (unsigned)wave_max_dpp((int)class_key(own, fn, lane));
-        if (lane == 0) class_store(own, fn, k);
-        // the decision below reads this class's L1 row and count: the wave's LDS operations in order
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
       }
-      if (tid == 0) sh.nflag = 0;
+      bmark(3);
+    } else if (wv == 0 && own >= 0) {
+      // ===== the critical path (wave 0): the event's own class on d -- its Filter on d's new and old
+      //       records, its group's candidates (one quad each: quad 0 = d's current state, quad 1 + i = the
+      //       i-th candidate), its key, L1 entry and feasible count -- then the decision below reads it
+      const NodeV dn = uniform_node(&sh.dnew[cur]);
+      const NodeV dold = uniform_node(&sh.dold[cur]);
+      const int b = d / kFan - b0;
+      const PodDev q = uniform_pod(&s_cls[own]);
+      const bool fn = filter_node(dn, q), fo = filter_node(dold, q);
+      unsigned* l = &s_l1[own * nb + b];
+      const unsigned old = __builtin_amdgcn_readfirstlane(*l);
+      const bool flag = old != 0u && hkey_rank(old) == roff + d;  // d was the max of its block
+      uint4 bv = make_uint4(0u, 0u, 0u, 0u);
+      if (flag && lane < 16) bv = gld4(keys + (size_t)own * a.Npad + (size_t)(b0 + b) * kFan + 4 * lane);
+      unsigned k = 0u;
+      if (fn) {
+        const PodDev gp = uniform_pod(&s_gpod[s_cgrp[own]]);
+        const bool share = is_share_pod(gp);
+        const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst[cur]);
+        const unsigned cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
+        const int qd = lane >> 2, qq = lane & 3;
+        int code = -1;
+        if (qd == 0) {
+          code = 0;
+        } else {
+          unsigned mm = cm;
+          for (int i = 1; i < qd && mm; ++i) mm &= mm - 1u;
+          if (mm) code = share ? 1 + __builtin_ctz(mm) : 9;
+        }
+        double F = 0.0;
+        if (code >= 0) {
+          int cpuL, total;
+          uint32_t gs[4];
+          fgd_candidate(dn, code, gp, &cpuL, gs, &total);
+          const uint32_t tb = 1u << dn.gpu_type();
+          F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, qq)
+                    : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, qq);
+        }
+        const long long fb = __builtin_bit_cast(long long, F);
+        const double F0 = __builtin_bit_cast(double, ((long long)(unsigned)__builtin_amdgcn_readlane((int)(fb >> 32), 0) << 32) |
+                                                         (long long)(unsigned)__builtin_amdgcn_readlane((int)fb, 0));
+        unsigned x = 0u;
+        if (code > 0 && qq == 0)
+          x = hkey(ksim_memo::score_lookup_dev(F0 - F, sh.th), roff + d, share ? 15 - (code - 1) : 0);
+        k = (unsigned)wave_max_dpp((int)x);
+        if (share) {
+          const unsigned z = hkey(0, roff + d, 0);  // feasible with no fitting GPU
+          k = k > z ? k : z;
+        }
+      }
+      unsigned bx = 0u;
+      if (flag) bx = (unsigned)__builtin_amdgcn_readfirstlane((int)block_max_excl(bv, (b0 + b) * kFan, lane & 15, d));
+      if (lane == 0) {
+        gst1(keys + (size_t)own * a.Npad + d, k);
+        s_cnt[own] += (fn ? 1 : 0) - (fo ? 1 : 0);
+        if (k > old) *l = k;
+        else if (flag) *l = k > bx ? k : bx;
+      }
+      // the decision below reads this class's L1 row and count: the wave's LDS operations in order
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      mark(1);
     }
     // ---- 4. the event: the winner of its class (create) or the unbind (delete); wave 0
     if (wv == 0) {
@@ -653,24 +764,25 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         if (write) gput(rp.res + step, out);
         if (rk >= 0) {
           store_node(&s_nodes[rk - lo], after);
-          store_node(&sh.dold, before);
-          store_node(&sh.dnew, after);
+          store_node(&sh.dold[cur ^ 1], before);
+          store_node(&sh.dnew[cur ^ 1], after);
           if (rp.snap) {  // cluster report: the state this event left
             gput_node(rp.snap + step, after);
             gput(rp.prev + step, s_last[rk - lo]);
           }
           s_last[rk - lo] = step;
         }
-        sh.d = rk;
+        sh.d[cur ^ 1] = rk;
       }
       if (rk >= 0) {
         const unsigned fm = ksim_memo::first_mask_lanes(after, lane);
-        if (lane == 0) sh.dfirst = fm;
+        if (lane == 0) sh.dfirst[cur ^ 1] = fm;
       }
     }
     __syncthreads();
     mark(5);
-    if (Kt > 1 && sh.stop) break;
+    cur ^= 1;
+    if (sh.stop) break;  // K > 1: a poll timed out; any K: a bulk wait timed out
   }
   if (prof && tid == 0) {
     sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
