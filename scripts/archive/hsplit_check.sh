@@ -2,7 +2,7 @@
 # k_hmemo critical/bulk split: the k_hmemo parity tests, then C2 run_mode 5 / C4 / C5 timings and one
 # KSIM_PROFILE=1 phase print.  Every GPU step has its own time limit; the first failure ends the script.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/hsplit
 export TMPDIR=/tmp
 O=gpurun_out/hsplit

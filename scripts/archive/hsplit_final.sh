@@ -1,7 +1,7 @@
 #!/bin/bash
 # After the k_hmemo critical/bulk split: C4 x10 sweeps, the C5 / run_mode 5 lines, then counter profiles.
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/hsplit
 export TMPDIR=/tmp
 O=gpurun_out/hsplit

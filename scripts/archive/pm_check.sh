@@ -11,4 +11,4 @@ timeout -k 10 300 python bench.py --run-mode 6 --steps 5 --warmup 1 --no-cpu-bas
 rc=$?
 tail -1 gpurun_out/pm_bench.log | cut -c1-400
 [ $rc -eq 0 ] || exit $rc
-bash scripts/pm_prof.sh
+bash scripts/archive/pm_prof.sh

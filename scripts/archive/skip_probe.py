@@ -1,7 +1,7 @@
 """Dead-class skip probe: k_memo (lean) on C2 seed 42 -- the whole stream against its prefix before the
 first failure; with the skip, the tail's repeated failures cost little."""
 import os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "kubernetes-scheduler-simulator_amd")]
 import ksim
 t = ksim.Trace.openb("default")
