@@ -2335,6 +2335,10 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     std::iota(all.begin(), all.end(), 0);
     ma.skip = dead_skip(e, all) ? 1 : 0;
   }
+  {  // KSIM_HPF (one workgroup per replica): 1 = wave 0 lists the next refresh, 2 = + touches its flagged rows
+    const char* pf = std::getenv("KSIM_HPF");
+    ma.pf = pf ? std::atoi(pf) & 3 : 0;
+  }
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }

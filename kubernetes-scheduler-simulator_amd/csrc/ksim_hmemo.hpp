@@ -108,6 +108,8 @@ struct HMemoArgs {
   int npeer, epoch;
   unsigned long long* peer[kMaxPeers];
   int skip;                 // the dead-class skip (create-only streams; class slots < 1024)
+  int pf;                   // one workgroup per replica: 1 = wave 0 lists the next refresh's F evaluations after its
+                            // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -121,12 +123,17 @@ struct __align__(16) HShared {
   NodeRec dold[2], dnew[2];
   int d[2];
   unsigned dfirst[2];
-  int nitems, nflag;
+  int nitems[2];       // the F list's length (double-buffered)
+  int nflag;
   int stop;            // K > 1: a poll timed out, every workgroup leaves its loop
   int bar;             // the bulk waves' barrier counter
   int cbar;            // the class waves' barrier counter
   int lseq;            // the F list's hand-over: refreshes listed so far
-  int pad_[2];
+  // The class the last decided step found dead (-1 none), double-buffered like d: wave 0's decision runs
+  // while slower waves may still be reading this step's skip condition, so it writes [cur ^ 1] and folds
+  // [cur] into `dead`; every reader checks dead | pdead[cur] (the same answer before and after the fold).
+  int pdead[2];
+  int pad_[3];
   unsigned long long prof[kHProf];
   unsigned dead[32];   // class slots with no feasible node (create-only streams: for good)
 };
@@ -150,11 +157,11 @@ KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
   L.bx = o;    o = halign(o + (size_t)Cmax * 4);
   L.cgrp = o;  o = halign(o + (size_t)Cmax * 2);
   L.flist = o; o = halign(o + (size_t)Cmax * 2);
-  L.code = o;  o = halign(o + (size_t)kMaxItems);
-  L.igrp = o;  o = halign(o + (size_t)kMaxItems);
+  L.code = o;  o = halign(o + (size_t)2 * kMaxItems);  // the F list, double-buffered like d's records
+  L.igrp = o;  o = halign(o + (size_t)2 * kMaxItems);
   L.fnew = o;  o = halign(o + (size_t)Cmax);
   L.fold = o;  o = halign(o + (size_t)Cmax);
-  L.gbase = o; o = halign(o + (size_t)Gmax * 2);
+  L.gbase = o; o = halign(o + (size_t)Gmax * 2 * 2);
   L.total = o;
   return L;
 }
@@ -262,11 +269,11 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int* s_cnt = reinterpret_cast<int*>(smem + L.cnt);
   unsigned* s_bx = reinterpret_cast<unsigned*>(smem + L.bx);
   uint16_t* s_cgrp = reinterpret_cast<uint16_t*>(smem + L.cgrp);
-  uint8_t* s_code = reinterpret_cast<uint8_t*>(smem + L.code);
-  uint8_t* s_igrp = reinterpret_cast<uint8_t*>(smem + L.igrp);
+  uint8_t* const s_code_b = reinterpret_cast<uint8_t*>(smem + L.code);
+  uint8_t* const s_igrp_b = reinterpret_cast<uint8_t*>(smem + L.igrp);
   uint8_t* s_fnew = reinterpret_cast<uint8_t*>(smem + L.fnew);
   uint8_t* s_fold = reinterpret_cast<uint8_t*>(smem + L.fold);
-  int16_t* s_gbase = reinterpret_cast<int16_t*>(smem + L.gbase);
+  int16_t* const s_gbase_b = reinterpret_cast<int16_t*>(smem + L.gbase);
   uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
@@ -300,7 +307,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     s_l1[i] = b0 + i % nb < a.nb ? a.l1[((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb] : 0u;
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
-  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; }
+  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; }
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
@@ -328,12 +335,18 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int bar_target = 0;  // the bulk barrier's count so far (waves 1-15)
   int cbar_target = 0; // the class waves' barrier count so far
   int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..kFW)
+  const bool w0list = kSub == 0 && (a.pf & 1) != 0;  // wave 0 lists the next refresh's F evaluations
+  const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
   // A bounded wait on one of the bulk's LDS counters (lane 0 of a wave): past the limit the workgroup
   // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over) instead of hanging.
-  auto spin_until = [&](int* ctr, int target, int bit) {
+  auto spin_until = [&](int* ctr, int target, int bit, int step_, int d_) {
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
       if (++spins > 4 * ksim_replay::kSpinLimit) {
+        printf("ksim hmemo wait timeout: blk %d wave %d bit %d step %d d %d cur %d target %d ctr %d | bar %d cbar %d lseq %d "
+               "nflag %d nitems %d %d d[] %d %d\n",
+               (int)blockIdx.x, wv, bit, step_, d_, cur, target, *ctr, sh.bar, sh.cbar, sh.lseq, sh.nflag, sh.nitems[0],
+               sh.nitems[1], sh.d[0], sh.d[1]);
         atomicOr(a.fail, bit);
         __hip_atomic_store(&sh.stop, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
@@ -358,14 +371,15 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     // all skip the same steps; the changed node d is carried to the next decided step's refresh.
     {
       const int cs0 = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
-      if (a.skip && cs0 >= 0 && ((sh.dead[cs0 >> 5] >> (cs0 & 31)) & 1u)) {
+      const int pd = __builtin_amdgcn_readfirstlane(sh.pdead[cur]);
+      if (a.skip && cs0 >= 0 && (cs0 == pd || ((sh.dead[cs0 >> 5] >> (cs0 & 31)) & 1u))) {
         // the whole run of dead events up to the next live one (or the window's end) at once
         const int wend = min(kEvBuf, rp.n_events - (step - eb));
         int run = wend - eb;
         for (int j0 = eb + 1; j0 < wend; j0 += 64) {
           const int j = j0 + lane;
           const int c = j < wend ? sh.evc[j] : 0;
-          const unsigned long long lb = __ballot(j < wend && (c < 0 || !((sh.dead[c >> 5] >> (c & 31)) & 1u)));
+          const unsigned long long lb = __ballot(j < wend && (c < 0 || (c != pd && !((sh.dead[c >> 5] >> (c & 31)) & 1u))));
           if (lb) {
             run = j0 + (int)__builtin_ctzll(lb) - eb;
             break;
@@ -381,6 +395,9 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     const int d = __builtin_amdgcn_readfirstlane(sh.d[cur]);  // changed rank in this slice, -1 none
     const int cs = __builtin_amdgcn_readfirstlane(sh.evc[eb]);  // the event's class, -1 delete
     const int own = d >= 0 ? cs : -1;                            // the class wave 0 refreshes itself
+    uint8_t* const s_code = s_code_b + cur * kMaxItems;          // this step's F list
+    uint8_t* const s_igrp = s_igrp_b + cur * kMaxItems;
+    int16_t* const s_gbase = s_gbase_b + cur * a.Gmax;
     if (d >= 0 && wv != 0) {
       // ===== the bulk (waves 1-15): every class but the event's own on d, beside wave 0's critical path;
       //       needed from the next decision on.  Three phases, joined by LDS-counter barriers of these
@@ -394,7 +411,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) {
           __hip_atomic_fetch_add(&sh.bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          spin_until(&sh.bar, bar_target, 4);
+          spin_until(&sh.bar, bar_target, 4, step, d);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -407,7 +424,9 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       //      each) and their maxima without d
       if (wv <= kFW) {
         ++list_seq;
-        if (wv == 1) {
+        if (w0list) {
+          // listed by wave 0 after the previous decided step's Bind
+        } else if (wv == 1) {
           const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst[cur]);
           int base = 1;  // item 0: d's current state
           for (int g0 = 0; g0 < G; g0 += 64) {
@@ -442,17 +461,17 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           if (lane == 0) {
             s_code[0] = 0;
             s_igrp[0] = 0;
-            sh.nitems = base;
+            sh.nitems[cur] = base;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __hip_atomic_store(&sh.lseq, list_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           bmark(0);
         } else {
-          if (lane == 0) spin_until(&sh.lseq, list_seq, 16);
+          if (lane == 0) spin_until(&sh.lseq, list_seq, 16, step, d);
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+        const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
         const int q = bt & 3;
         for (int j = bt >> 2; j < nit; j += kFW * 16) {
           const int code = s_code[j];
@@ -493,7 +512,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) {
           __hip_atomic_fetch_add(&sh.cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          spin_until(&sh.cbar, cbar_target, 8);
+          spin_until(&sh.cbar, cbar_target, 8, step, d);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -523,7 +542,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       }
       bulk_bar();
       if (tid == 64) sh.nflag = 0;  // (read above, before the barrier; the next class pass adds to it)
-      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems);
+      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
       // ---- 3. every other class's group key on d (score steps of its candidates), key[c][d] (HBM
       //         store), L1[c][d/64] (max with the new key, or the block max without d when d was the
       //         block max), the feasible count
@@ -619,7 +638,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     // ---- 4. the event: the winner of its class (create) or the unbind (delete); wave 0
     if (wv == 0) {
       const PodDev p = uniform_pod(&sh.ev[eb]);
-      int rk = -1, mask = 0;
+      int rk = -1, mask = 0, ndead = -1;
       bool write = false;
       NodeV before{}, after{};
       ResultDev out{-1, 0, 0, 0, ST_DELETED};
@@ -693,7 +712,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         }
         out = ResultDev{-1, 0, 0, nfeas, ST_UNSCHED};
         write = W == 0u && w == 0;  // nobody feasible: workgroup 0 reports
-        if (a.skip && W == 0u && lane == 0) sh.dead[cs >> 5] |= 1u << (cs & 31);  // for good (create-only)
+        if (a.skip && W == 0u) ndead = cs;  // for good (create-only); published through pdead below
         uint8_t h = 3;
         if (W != 0u) {
           const int wr = hkey_rank(W) - roff;  // the winner's rank in this shard
@@ -773,10 +792,71 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           s_last[rk - lo] = step;
         }
         sh.d[cur ^ 1] = rk;
+        {  // the dead set: fold the previous decided step's class in, publish this one's for the next step
+          const int pc = sh.pdead[cur];
+          if (pc >= 0) sh.dead[pc >> 5] |= 1u << (pc & 31);
+          sh.pdead[cur ^ 1] = ndead;
+        }
       }
       if (rk >= 0) {
         const unsigned fm = ksim_memo::first_mask_lanes(after, lane);
         if (lane == 0) sh.dfirst[cur ^ 1] = fm;
+        if (w0list) {  // the next refresh's F list (wave 0 waits for the bulk at the end barrier anyway)
+          const unsigned dfirst = (unsigned)__builtin_amdgcn_readfirstlane((int)fm);
+          uint8_t* const ncode = s_code_b + (cur ^ 1) * kMaxItems;
+          uint8_t* const nigrp = s_igrp_b + (cur ^ 1) * kMaxItems;
+          int16_t* const ngbase = s_gbase_b + (cur ^ 1) * a.Gmax;
+          int base = 1;  // item 0: the node's current state
+          for (int g0 = 0; g0 < G; g0 += 64) {
+            const int g = g0 + lane;
+            unsigned cm = 0u;
+            bool share = false;
+            if (g < G) {
+              const PodDev gp = s_gpod[g];
+              share = is_share_pod(gp);
+              cm = share ? (dfirst & ksim_memo::ge_mask(after, gp.milli)) : 0x100u;
+            }
+            const int nc = __popc(cm);
+            int excl = 0, tot = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const unsigned long long m = __ballot((nc >> k) & 1);
+              excl += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << k;
+              tot += __popcll(m) << k;
+            }
+            int o = base + excl;
+            if (g < G) ngbase[g] = (int16_t)o;
+            unsigned mm = cm;
+            while (mm) {
+              const int x = __builtin_ctz(mm);
+              mm &= mm - 1u;
+              ncode[o] = (uint8_t)(share ? 1 + x : 9);
+              nigrp[o] = (uint8_t)g;
+              ++o;
+            }
+            base += tot;
+          }
+          if (lane == 0) {
+            ncode[0] = 0;
+            nigrp[0] = 0;
+            sh.nitems[cur ^ 1] = base;
+          }
+        }
+        if (w0pf) {
+          // touch the key rows of the classes whose block max is the node just bound: the next refresh
+          // reloads most of them (its flagged blocks), and this workgroup's L1 then holds them.  A hint
+          // only: the L1 values read here may be mid-update by the bulk.
+          const int nb2 = (rk - lo) / kFan;
+          unsigned acc = 0u;
+          for (int c = lane; c < C; c += 64) {
+            const unsigned o = s_l1[c * nb + nb2];
+            if (o != 0u && hkey_rank(o) == roff + rk) {
+              const unsigned* row = keys + (size_t)c * a.Npad + (size_t)(b0 + nb2) * kFan;
+              acc ^= row[0] ^ row[16] ^ row[32] ^ row[48];
+            }
+          }
+          asm volatile("" ::"v"(acc));
+        }
       }
     }
     __syncthreads();
