@@ -10,7 +10,7 @@ KSIM_HPF=1 timeout -k 10 500 python -u -m pytest -x -q --timeout 300 --timeout-m
   tests/test_gpu_memo.py tests/test_gpu_sweep.py tests/test_gpu_c5.py -m gpu > $O/pytest_hpf1.log 2>&1 || { echo "pytest rc=$?"; grep -E "timeout|FAIL|Error" $O/pytest_hpf1.log | head; tail -5 $O/pytest_hpf1.log; exit 1; }
 tail -1 $O/pytest_hpf1.log
 j() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], round(d['ms_per_step'],3))" "$@"; }
-for i in 1 2; do
+for i in 1; do
   for f in 0 1 3; do
     KSIM_HPF=$f timeout -k 10 200 python3 bench.py --config c4 --steps 10 --warmup 1 --no-cpu-baseline > $O/c4_$f.log 2>&1 || { echo "c4 hpf=$f rc=$?"; grep timeout $O/c4_$f.log | head -3; exit 1; }
     j $O/c4_$f.log "c4 hpf=$f"
