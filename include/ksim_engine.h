@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 1
+#define KSIM_ABI_VERSION 2  /* 2: 128-byte shard peer handles carrying the device, KSIM_EPEER */
 #define KSIM_MAX_GPU 8          /* pkg/type/const.go:52 MaxNumGpuPerNode */
 #define KSIM_MAX_TYPES 32       /* GPU-model vocabulary size (bit i of a type mask) */
 #define KSIM_MAX_TYPICAL 256
@@ -56,7 +56,9 @@ enum ksim_status {
     KSIM_ESTATE = -5,     /* call out of order (e.g. run before events are loaded) */
     KSIM_ENOTSUP = -6,    /* policy/config not supported */
     KSIM_ENODEV = -7,     /* no gfx950 device */
-    KSIM_EIO = -8         /* trace file unreadable / malformed */
+    KSIM_EIO = -8,        /* trace file unreadable / malformed */
+    KSIM_EPEER = -9       /* a peer shard's exchange buffer sits on a device this one cannot reach (not
+                             visible in this process, or no peer path: hipDeviceCanAccessPeer) */
 };
 
 /* Score plugins (one per replica; pkg/type/const.go:8-14) */
@@ -212,10 +214,8 @@ typedef struct {
                                       for FGD (KSIM_ENOTSUP otherwise), 4 = k_memo in decider mode (workgroup 0
                                       decides every event from the class owners' top lists; KSIM_ENOTSUP if it
                                       does not fit), 5 = k_hmemo required for FGD (one workgroup per replica,
-                                      keys in HBM; KSIM_ENOTSUP if it does not fit), 6 = k_pmemo required for FGD
-                                      (node slices of <= 64 ranks on co-resident workgroups, the previous
-                                      step's exchange overlapping the next step's key refresh; KSIM_ENOTSUP
-                                      if it does not apply) */
+                                      keys in HBM; KSIM_ENOTSUP if it does not fit); any other value:
+                                      KSIM_EINVAL at create (6 was the r03 k_pmemo trial, now archived) */
     int32_t reserved[3];
 } ksim_config;
 
@@ -261,8 +261,11 @@ int  ksim_engine_filter_score(ksim_engine* e, int replica, const ksim_pod* pod, 
 
 /* Reserve + Bind `pod` on `node` (GPU selection by the replica's gpusel) and
  * Unreserve/delete.  *gpu_mask_out receives the devices assigned.  Unreserve returns KSIM_ESTATE,
- * and changes nothing, when the node does not hold what the pod would release (a device would exceed
- * 1000 milli or the CPU its allocatable: e.g. the same pod unreserved twice). */
+ * and changes nothing, when releasing the pod would push a named device above 1000 milli left or the
+ * node's CPU above its allocatable.  That catches a second Unreserve of the same pod only while no
+ * other pod holds those devices / that CPU; it checks neither memory nor pod identity, so it is a
+ * guard, not a double-release detector: the caller's record of what it bound (the Go plugin's bound
+ * map, go/ksim_gpu.go) is what prevents a double release. */
 int  ksim_engine_reserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t step,
                          int32_t* gpu_mask_out);
 int  ksim_engine_unreserve(ksim_engine* e, int replica, const ksim_pod* pod, int node, int32_t gpu_mask);
@@ -326,8 +329,12 @@ int  ksim_shard_group_run(ksim_engine* const* engines, int world);
  * peers' buffers (its own handle must sit at its rank: KSIM_EINVAL otherwise).  ksim_engine_run then replays
  * the shard's slices on k_hmemo and, per pod step, stores its slice maxima straight into every peer's buffer
  * (xGMI) and polls its own: selectHost over the union, the owner of the winner binds (results as above).
- * Every rank must run the same runs.  Other policies, the report or a plan that does not fit: KSIM_ENOTSUP. */
-#define KSIM_SHARD_HANDLE_BYTES 64
+ * Every rank must run the same runs.  Other policies, the report or a plan that does not fit: KSIM_ENOTSUP.
+ * A handle is the buffer's hipIpcMemHandle_t (64 B), then "KSPH", the PCI domain / bus / device of the GPU
+ * holding it and the exporting pid (u32 each), zero padded.  set_shard_peers checks, before it opens a peer
+ * buffer on another GPU, that the GPU is visible here and reachable (hipDeviceCanAccessPeer): KSIM_EPEER
+ * otherwise, nothing mapped.  A malformed handle: KSIM_EINVAL. */
+#define KSIM_SHARD_HANDLE_BYTES 128
 int  ksim_shard_peer_handle(ksim_engine* e, uint8_t* out /* KSIM_SHARD_HANDLE_BYTES */);
 int  ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles /* world * KSIM_SHARD_HANDLE_BYTES */);
 
@@ -347,8 +354,8 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
  * KSIM_PATH_HMEMO (k_hmemo: memoised FGD keys in HBM, one workgroup per replica), KSIM_PATH_RANDOM_GO
  * (k_random_go: every replica Random on Go's stream, ksim_engine_set_go_stream), KSIM_PATH_SCAN1
  * (k_scan1: every replica a cheap policy on one 256-thread workgroup, every node scanned per pod;
- * a mix of k_scan1 and k_replay groups reports KSIM_PATH_REPLAY), KSIM_PATH_PMEMO (k_pmemo: pipelined
- * memoised FGD, node slices). */
+ * a mix of k_scan1 and k_replay groups reports KSIM_PATH_REPLAY).  (8 was KSIM_PATH_PMEMO, the archived
+ * r03 k_pmemo trial; it is not reused.) */
 #define KSIM_PATH_REPLAY  0
 #define KSIM_PATH_MEMO    1
 #define KSIM_PATH_MIXED   2
@@ -357,7 +364,6 @@ int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 #define KSIM_PATH_HMEMO   5
 #define KSIM_PATH_RANDOM_GO 6
 #define KSIM_PATH_SCAN1   7
-#define KSIM_PATH_PMEMO   8
 int  ksim_engine_last_run_path(ksim_engine* e, int* path);
 
 #ifdef __cplusplus

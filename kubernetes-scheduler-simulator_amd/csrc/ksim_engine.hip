@@ -25,6 +25,8 @@
 // a one-thread kernel advances base) so a whole trace replays with no host
 // round trip per pod.
 #include <dlfcn.h>
+#include <unistd.h>
+#include <string>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -656,7 +658,6 @@ __global__ void k_shard_gather(unsigned long long* const* sends, unsigned long l
 #include "ksim_report.hpp"
 #include "ksim_memo.hpp"
 #include "ksim_hmemo.hpp"
-#include "ksim_pmemo.hpp"
 
 // ---------------------------------------------------------------------------
 // k_replay: the whole event stream of every replica in one launch (see ksim_replay.hpp).
@@ -1596,13 +1597,6 @@ struct ksim_engine {
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
   size_t h_cap[14] = {};
   int last_hmemo = 0;
-  // k_pmemo (pipelined memoised FGD replay, ksim_pmemo.hpp): uses the k_hmemo plan's tables
-  bool pplan_ok = false;
-  int p_K = 0, p_S = 0;
-  size_t p_lds = 0;
-  int* d_p_evg = nullptr;
-  size_t p_cap = 0;
-  int last_pmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
   int scan1 = 2;       // single-workgroup cheap-policy groups on k_scan1, node records in VGPRs where they fit
@@ -2029,8 +2023,6 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   return KSIM_OK;
 }
 
-static int prepare_pmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev);
-
 // Plan and upload the k_memo launch of the FGD replicas (before the timed region of a run; cached
 // until events or policies change).
 static int prepare_memo(ksim_engine* e, int max_ev) {
@@ -2044,17 +2036,8 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   e->mplan_max_ev = max_ev;
   e->mplan_ok = false;
   e->hplan_ok = false;
-  e->pplan_ok = false;
   if (reps.empty()) return KSIM_OK;
   if (e->run_mode == 5) return prepare_hmemo(e, reps, max_ev);  // k_hmemo required
-  if (e->run_mode == 6) return prepare_pmemo(e, reps, max_ev);  // k_pmemo required
-  {  // auto: k_pmemo where it applies (KSIM_PMEMO=0: not)
-    const char* pm = std::getenv("KSIM_PMEMO");
-    if (e->run_mode == 0 && pm && pm[0] == '1') {
-      int rc = prepare_pmemo(e, reps, max_ev);
-      if (rc || e->pplan_ok) return rc;
-    }
-  }
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
   // run_mode 4 (or KSIM_MEMO_DECIDER=1 with run_mode 0): the decider variant of k_memo
@@ -2295,6 +2278,13 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
 
 static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps);
 
+// KSIM_HDELAY=<mask>: the memoised kernels' hand-over stress delays (ksim_hmemo.hpp hdelay, ksim_memo.hpp);
+// a nonzero mask selects the general (non-lean) instantiation, which alone carries them.
+static int hdelay_mask() {
+  const char* v = std::getenv("KSIM_HDELAY");
+  return v ? (int)(std::strtol(v, nullptr, 0) & 0xff) : 0;
+}
+
 // k_hmemo's arguments for the planned launch (one group of Rg replicas from d_replist + first).
 static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   using namespace ksim_hmemo;
@@ -2339,6 +2329,7 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     const char* pf = std::getenv("KSIM_HPF");
     ma.pf = pf ? std::atoi(pf) & 3 : 0;
   }
+  ma.delay = hdelay_mask();
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }
@@ -2368,9 +2359,10 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     KSIM_HIP(hipMemsetAsync(e->d_h_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * kHProf, st));
     ma.prof = e->d_h_prof;
   }
-  const void* f = pl.K == 1 ? (profile ? (const void*)k_hmemo<0, true> : (const void*)k_hmemo<0, false>)
-                  : pl.K <= 64 ? (profile ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
-                               : (profile ? (const void*)k_hmemo<4, true> : (const void*)k_hmemo<4, false>);
+  const bool gen = profile || ma.delay != 0;  // the general instantiation: timers, stress delays
+  const void* f = pl.K == 1 ? (gen ? (const void*)k_hmemo<0, true> : (const void*)k_hmemo<0, false>)
+                  : pl.K <= 64 ? (gen ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
+                               : (gen ? (const void*)k_hmemo<4, true> : (const void*)k_hmemo<4, false>);
   if (pl.K > 1 && Rg * pl.K > resident_cap(e, f, pl.lds)) {
     std::fprintf(stderr, "ksim: k_hmemo needs %d co-resident workgroups\n", Rg * pl.K);
     return KSIM_ERANGE;
@@ -2423,207 +2415,6 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   return KSIM_OK;
 }
 
-// ---- k_pmemo (pipelined memoised FGD replay, ksim_pmemo.hpp): the k_hmemo plan's tables (score
-// groups, their requests, the distinct initial states) plus the group of every event; K co-resident
-// workgroups per replica with <= 64 slots each.  Not eligible (pplan_ok stays false): deletes, the
-// cluster report, a GPU selector other than FGD / best / worst / random, more than 128 score groups,
-// clusters wider than 64 slots x the workgroups the CUs give each replica.
-static int prepare_pmemo(ksim_engine* e, const std::vector<int>& reps, int max_ev) {
-  using namespace ksim_pmemo;
-  e->pplan_ok = false;
-  if (e->report) return KSIM_OK;
-  for (int r : reps) {
-    if (e->has_delete[r]) return KSIM_OK;
-    const int sel = e->reps[r].gpusel;
-    if (sel != SEL_FGD && sel != SEL_BEST && sel != SEL_WORST && sel != SEL_RANDOM) return KSIM_OK;
-  }
-  const int Rg = (int)reps.size();
-  const int Kmax = std::min(kSlots, e->cus / std::max(Rg, 1));
-  int K = e->wgs_req > 0 ? e->wgs_req : Kmax;
-  if (K < 1 || K > Kmax) return KSIM_OK;
-  const int S = (e->N + K - 1) / K;
-  if (S > kSlots) return KSIM_OK;
-  K = (e->N + S - 1) / S;  // no empty workgroup
-  int rc = prepare_hmemo(e, reps, max_ev, K, S);  // (K, S only size its unused LDS estimate)
-  if (rc || !e->hplan_ok) return rc;
-  e->hplan_ok = false;  // the tables serve k_pmemo
-  const HPlan& pl = *e->hplan;
-  if (pl.Gmax > kMaxGroups) return KSIM_OK;
-  const size_t lds = pmemo_lds(pl.Gmax);
-  if (lds > 160 * 1024) return KSIM_OK;
-  if (K > 1 && Rg * K > resident_cap(e, (const void*)k_pmemo<false>, lds)) return KSIM_OK;
-  const int stride = std::max(max_ev, 1);
-  std::vector<int> evg((size_t)Rg * stride, -1);
-  for (int i = 0; i < Rg; ++i)
-    for (int k = 0; k < stride; ++k) {
-      const int c = pl.evc[(size_t)i * stride + k];
-      evg[(size_t)i * stride + k] = c < 0 ? -1 : (int)pl.cgrp[(size_t)i * pl.Cmax + c];
-    }
-  if ((rc = upload_vec(e->d_p_evg, e->p_cap, evg, e->stream))) return rc;
-  KSIM_HIP(hipStreamSynchronize(e->stream));
-  e->p_K = K;
-  e->p_S = S;
-  e->p_lds = lds;
-  e->pplan_ok = true;
-  return KSIM_OK;
-}
-
-static int launch_pmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
-  using namespace ksim_pmemo;
-  const HPlan& pl = *e->hplan;
-  const int stride = std::max(max_ev, 1);
-  // the group keys of the distinct initial states (k_hmemo's first init kernel)
-  ksim_hmemo::HInitArgs ia{};
-  ia.reps = e->d_reps;
-  ia.rep_list = e->d_replist + first;
-  ia.N = e->N;
-  ia.Npad = pl.Npad;
-  ia.nb = pl.nb;
-  ia.Cmax = pl.Cmax;
-  ia.Gmax = pl.Gmax;
-  ia.Smax = pl.Smax;
-  ia.cg = e->d_h_cg;
-  ia.cls = e->d_h_cls;
-  ia.cgrp = e->d_h_cgrp;
-  ia.gpod = e->d_h_gpod;
-  ia.roff = 0;
-  ia.st = e->d_h_st;
-  ia.ns = e->d_h_ns;
-  ia.nstate = e->d_h_nstate;
-  ia.gsc = e->d_h_gsc;
-  ia.th = e->d_th;
-  hipLaunchKernelGGL(ksim_hmemo::k_hinit_gk, dim3((unsigned)((pl.Smax + 255) / 256), (unsigned)pl.Gmax, (unsigned)Rg),
-                     dim3(256), 0, st, ia, (const TypDev*)e->d_tp);
-  KSIM_HIP(hipGetLastError());
-  const int K = e->p_K;
-  if (K > 1) KSIM_HIP(hipMemsetAsync(e->d_gran, 0, sizeof(unsigned long long) * (size_t)Rg * 2 * K, st));
-  PMemoArgs pa;
-  pa.reps = e->d_reps;
-  pa.rep_list = e->d_replist + first;
-  pa.N = e->N;
-  pa.K = K;
-  pa.S = e->p_S;
-  pa.Gmax = pl.Gmax;
-  pa.Smax = pl.Smax;
-  pa.Npad = pl.Npad;
-  pa.cg = e->d_h_cg;
-  pa.gpod = e->d_h_gpod;
-  pa.evg = e->d_p_evg;
-  pa.stride = stride;
-  pa.gsc = e->d_h_gsc;
-  pa.nstate = e->d_h_nstate;
-  pa.th = e->d_th;
-  pa.gran = e->d_gran;
-  pa.fail = e->d_fail;
-  pa.prof = nullptr;
-  pa.trace = nullptr;
-  pa.trace_steps = 0;
-  const char* pe = std::getenv("KSIM_PROFILE");
-  const bool profile = pe && (pe[0] == '1' || pe[0] == '2');
-  const bool tracing = pe && pe[0] == '2';
-  const int TS = std::min(max_ev, 4000);
-  unsigned long long* d_trace = nullptr;
-  if (tracing) {
-    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * kTr * (size_t)Rg * K * TS));
-    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * kTr * (size_t)Rg * K * TS, st));
-    pa.trace = d_trace;
-    pa.trace_steps = TS;
-  }
-  if (profile) {
-    int rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)Rg * K * kPProf);
-    if (rc) return rc;
-    KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * K * kPProf, st));
-    pa.prof = e->d_prof;
-  }
-  const TypDev* tpp = e->d_tp;
-  const void* f = profile ? (const void*)k_pmemo<true> : (const void*)k_pmemo<false>;
-  const int lrc = launch_persistent(f, Rg * K, kPBlock, e->p_lds, st, e->coop && K > 1, pa, tpp);
-  if (lrc) return lrc;
-  if (profile) {
-    KSIM_HIP(hipStreamSynchronize(st));
-    const int nwg = Rg * K;
-    std::vector<unsigned long long> h((size_t)nwg * kPProf);
-    KSIM_HIP(hipMemcpy(h.data(), e->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    static const char* names[] = {"F round", "D: job keys", "D: slice max", "D: exchange wait",
-                                  "D: publish+commit+virtual", "D: next list", "end barrier"};
-    const double steps = std::max(max_ev, 1);
-    std::fprintf(stderr, "ksim pmemo profile: %d replicas x K=%d (S %d), LDS %zu B; us/step mean [max]:", Rg, K, e->p_S,
-                 e->p_lds);
-    for (int ph = 0; ph < 7; ++ph) {
-      double sum = 0, mx = 0;
-      for (int b = 0; b < nwg; ++b) {
-        const double us = (double)h[(size_t)b * kPProf + ph] / 100.0 / steps;
-        sum += us;
-        mx = std::max(mx, us);
-      }
-      std::fprintf(stderr, " %s %.3f [%.3f];", names[ph], sum / nwg, mx);
-    }
-    double it = 0, jb = 0, cr = 0, cyc = 0, tick = 0;
-    for (int b = 0; b < nwg; ++b) {
-      it += (double)h[(size_t)b * kPProf + 7];
-      jb += (double)h[(size_t)b * kPProf + 8];
-      cr += (double)h[(size_t)b * kPProf + 9];
-      cyc += (double)h[(size_t)b * kPProf + 10];
-      tick += (double)h[(size_t)b * kPProf + 11];
-    }
-    std::fprintf(stderr, " per workgroup and step: critical items %.2f, critical jobs %.2f, bulk items %.2f;",
-                 it / nwg / steps, jb / nwg / steps, cr / nwg / steps);
-    if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz, wall %.3f ms", cyc / tick * 100.0, tick / nwg / 1e5);
-    std::fprintf(stderr, "\n");
-  }
-  if (tracing) {
-    // replica 0: per step, the first and the last workgroup to publish, and where their time went
-    std::vector<unsigned long long> h((size_t)kTr * Rg * K * TS);
-    KSIM_HIP(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-    KSIM_HIP(hipFree(d_trace));
-    auto at = [&](int wg, int s, int k) { return (double)h[((size_t)wg * TS + s) * kTr + k] / 100.0; };  // us
-    // phases of step s at one workgroup: prev lists done -> F start (barrier), F round, D start -> wait,
-    // wait, done -> publish, publish -> lists done
-    double ph_last[6] = {}, ph_first[6] = {}, spread = 0, vis = 0, period = 0;
-    int n = 0;
-    for (int s = 2; s + 2 < TS; ++s) {
-      int lastk = 0, firstk = 0;
-      bool okk = true;
-      for (int k = 0; k < K && okk; ++k)
-        for (int x = 0; x < kTr; ++x) okk = okk && at(k, s, x) > 0 && at(k, s - 1, x) > 0 && at(k, s + 1, x) > 0;
-      if (!okk) continue;
-      for (int k = 1; k < K; ++k) {
-        if (at(k, s, 4) > at(lastk, s, 4)) lastk = k;
-        if (at(k, s, 4) < at(firstk, s, 4)) firstk = k;
-      }
-      auto phases = [&](int k, double* ph) {
-        ph[0] += at(k, s, 0) - at(k, s - 1, 5);
-        ph[1] += at(k, s, 1) - at(k, s, 0);
-        ph[2] += at(k, s, 2) - at(k, s, 1);
-        ph[3] += at(k, s, 3) - at(k, s, 2);
-        ph[4] += at(k, s, 4) - at(k, s, 3);
-        ph[5] += at(k, s, 5) - at(k, s, 4);
-      };
-      phases(lastk, ph_last);
-      phases(firstk, ph_first);
-      spread += at(lastk, s, 4) - at(firstk, s, 4);
-      double vmin = 1e300;
-      for (int k = 0; k < K; ++k) vmin = std::min(vmin, at(k, s + 1, 3) - at(lastk, s, 4));
-      vis += vmin;
-      period += at(lastk, s + 1, 4) - at(lastk, s, 4);
-      ++n;
-    }
-    if (n) {
-      std::fprintf(stderr, "ksim pmemo trace (replica 0, %d steps, us): publish spread %.3f; last publish -> first exchange done %.3f; "
-                   "period %.3f; phases [barrier, F, D to wait, wait, to publish, lists] last publisher:", n, spread / n, vis / n,
-                   period / n);
-      for (int x = 0; x < 6; ++x) std::fprintf(stderr, " %.3f", ph_last[x] / n);
-      std::fprintf(stderr, "; first publisher:");
-      for (int x = 0; x < 6; ++x) std::fprintf(stderr, " %.3f", ph_first[x] / n);
-      std::fprintf(stderr, "\n");
-    }
-  }
-  hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
-                     e->d_reps, (const int*)(e->d_replist + first), e->N);
-  KSIM_HIP(hipGetLastError());
-  return KSIM_OK;
-}
-
 extern "C" {
 
 const char* ksim_strerror(int code) {
@@ -2637,6 +2428,7 @@ const char* ksim_strerror(int code) {
     case KSIM_ENOTSUP: return "not supported";
     case KSIM_ENODEV: return "no gfx950 device";
     case KSIM_EIO: return "trace I/O error";
+    case KSIM_EPEER: return "peer shard's device not reachable from this one";
     default: return "unknown error";
   }
 }
@@ -2661,6 +2453,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   if (!out || n_nodes <= 0 || n_replicas <= 0) return KSIM_EINVAL;
   *out = nullptr;
   if (n_nodes > kMaxRank) return KSIM_ERANGE;  // name ranks are 24-bit fields of the argmax key
+  if (cfg && (cfg->run_mode < 0 || cfg->run_mode > 5)) return KSIM_EINVAL;
   const int dev = cfg ? cfg->device : 0;
   int rc = check_gfx950(dev);
   if (rc) return rc;
@@ -2793,7 +2586,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_p_evg};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -3279,7 +3072,18 @@ static RcclApi* rccl() {
   static RcclApi api;
   static int state = 0;  // 0 untried, 1 ok, -1 unavailable
   if (state == 0) {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    // the RCCL beside the HIP runtime this process bound (torch's or /opt/rocm's, ksim.hip_runtime_path):
+    // an RCCL from another install would NEED its own runtime and take this library's streams across
+    // runtimes; the bare names last (a RUNPATH / SONAME match)
+    void* h = nullptr;
+    Dl_info di;
+    if (dladdr((const void*)(hipError_t(*)(void**, size_t))&hipMalloc, &di) && di.dli_fname) {
+      std::string dir(di.dli_fname);
+      dir = dir.substr(0, dir.find_last_of('/') + 1);
+      for (const char* nm : {"librccl.so.1", "librccl.so"})
+        if (!h) h = dlopen((dir + nm).c_str(), RTLD_NOW | RTLD_GLOBAL);
+    }
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
     state = -1;
     if (h) {
@@ -3517,7 +3321,6 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   int first = 0;
   e->last_memo = 0;
   e->last_hmemo = 0;
-  e->last_pmemo = 0;
   e->last_rgo = 0;
   e->last_scan1 = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
@@ -3530,10 +3333,6 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     if (!concurrent) break;
     if (gp.first == kPolRandomGo) continue;  // one workgroup per replica
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
-    if (gp.first == POL_FGD && e->run_mode != 2 && e->pplan_ok) {
-      if (e->p_K > 1) { concurrent = false; break; }
-      continue;
-    }
     if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) {
       if (e->hplan->K > 1) { concurrent = false; break; }  // a co-resident wide launch
       continue;  // one workgroup per replica
@@ -3595,15 +3394,6 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                                   pl.decider ? " (decider)" : "", Rg, pl.K, pl.Cw, pl.nfw, pl.lds);
         continue;
       }
-      if (e->pplan_ok) {  // k_pmemo: node slices, pipelined exchange, keys in LDS
-        const int rc = launch_pmemo(e, Rg, first, max_ev, gs);
-        if (rc) return rc;
-        e->last_K = e->p_K;
-        e->last_groups = (int)groups.size();
-        e->last_pmemo += Rg;
-        first += Rg;
-        continue;
-      }
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
         const int rc = launch_hmemo(e, Rg, first, max_ev, gs);
         if (rc) return rc;
@@ -3613,7 +3403,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         first += Rg;
         continue;
       }
-      if (e->run_mode >= 3 && e->run_mode <= 6) return KSIM_ENOTSUP;
+      if (e->run_mode >= 3 && e->run_mode <= 5) return KSIM_ENOTSUP;
     }
     int K = choose_wgs(e, Rg);
     int S = (e->N + K - 1) / K;
@@ -3821,6 +3611,23 @@ int ksim_engine_set_shard_exchange(ksim_engine* e, ksim_shard_exchange_fn fn, vo
 
 // ---- one shard per process: device-initiated exchange through IPC-mapped granule buffers ----
 constexpr size_t kPeerGranBytes = sizeof(unsigned long long) * 2 * 256 * 2;  // 2 slots x 256 columns x 2
+constexpr uint32_t kPeerMagic = 0x4850534bu;  // "KSPH" after the IPC handle (include/ksim_engine.h)
+
+// The device ordinal in this process of the GPU a peer handle names (PCI domain / bus / device), -1 if it
+// is not visible here; -2 for a malformed handle.
+static int peer_device(const uint8_t* hd) {
+  uint32_t tail[5];
+  std::memcpy(tail, hd + sizeof(hipIpcMemHandle_t), sizeof tail);
+  if (tail[0] != kPeerMagic) return -2;
+  char bus[32];
+  std::snprintf(bus, sizeof bus, "%04x:%02x:%02x.0", tail[1], tail[2], tail[3]);
+  int dev = -1;
+  if (hipDeviceGetByPCIBusId(&dev, bus) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return dev;
+}
 
 int ksim_shard_peer_handle(ksim_engine* e, uint8_t* out) {
   if (!e || !out) return KSIM_EINVAL;
@@ -3834,9 +3641,14 @@ int ksim_shard_peer_handle(ksim_engine* e, uint8_t* out) {
   if (e->pgran_handle.empty()) {
     hipIpcMemHandle_t h;
     KSIM_HIP(hipIpcGetMemHandle(&h, e->d_pgran));
-    static_assert(sizeof(hipIpcMemHandle_t) <= KSIM_SHARD_HANDLE_BYTES, "IPC handle size");
+    static_assert(sizeof(hipIpcMemHandle_t) + 20 <= KSIM_SHARD_HANDLE_BYTES, "IPC handle size");
+    hipDeviceProp_t prop;
+    KSIM_HIP(hipGetDeviceProperties(&prop, e->device));
+    const uint32_t tail[5] = {kPeerMagic, (uint32_t)prop.pciDomainID, (uint32_t)prop.pciBusID,
+                              (uint32_t)prop.pciDeviceID, (uint32_t)getpid()};
     e->pgran_handle.assign(KSIM_SHARD_HANDLE_BYTES, 0);
     std::memcpy(e->pgran_handle.data(), &h, sizeof h);
+    std::memcpy(e->pgran_handle.data() + sizeof h, tail, sizeof tail);
   }
   std::memcpy(out, e->pgran_handle.data(), KSIM_SHARD_HANDLE_BYTES);
   return KSIM_OK;
@@ -3847,6 +3659,8 @@ int ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles) {
   if (e->shard_world < 1 || !e->d_pgran || e->pgran_handle.empty() || !e->peers.empty()) return KSIM_ESTATE;
   KSIM_HIP(hipSetDevice(e->device));
   const int world = e->shard_world;
+  if (const char* ep = std::getenv("KSIM_PEER_EPOCH0"))  // tests: start the run epoch near its wrap
+    e->peer_epoch = (int)(std::strtol(ep, nullptr, 0) & 0xffffff);
   e->peers.assign(world, nullptr);
   e->peer_opened.assign(world, 0);
   if (e->pgran_handle.empty() ||
@@ -3854,6 +3668,26 @@ int ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles) {
                   KSIM_SHARD_HANDLE_BYTES) != 0) {
     e->peers.clear();
     return KSIM_EINVAL;  // this shard's own handle must sit at its rank
+  }
+  // every peer's device first: visible here and reachable (xGMI / P2P), or nothing is mapped
+  for (int q = 0; q < world; ++q) {
+    if (q == e->shard_rank) continue;
+    const int pd = peer_device(handles + (size_t)q * KSIM_SHARD_HANDLE_BYTES);
+    int can = pd == e->device ? 1 : 0;
+    if (pd >= 0 && pd != e->device) {
+      if (hipDeviceCanAccessPeer(&can, e->device, pd) != hipSuccess) {
+        (void)hipGetLastError();
+        can = 0;
+      }
+    }
+    if (pd < 0 || !can) {
+      std::fprintf(stderr, "ksim: shard %d's exchange buffer is %s\n", q,
+                   pd == -2 ? "a malformed handle" : pd == -1 ? "on a GPU not visible in this process"
+                                                               : "on a GPU without a peer path from this one");
+      e->peers.clear();
+      e->peer_opened.clear();
+      return pd == -2 ? KSIM_EINVAL : KSIM_EPEER;
+    }
   }
   for (int q = 0; q < world; ++q) {
     if (q == e->shard_rank) {
@@ -3913,7 +3747,7 @@ static int run_hmemo_peer(ksim_engine* e, int max_ev) {
   a.Ktot = Kt;
   a.gran = e->d_pgran;
   a.npeer = world;
-  e->peer_epoch = (e->peer_epoch + 1) & 0xff;  // every rank runs the same runs: the same epoch
+  e->peer_epoch = (e->peer_epoch + 1) & 0xffffff;  // every rank runs the same runs: the same epoch (24 bits)
   if (e->peer_epoch == 0) e->peer_epoch = 1;
   a.epoch = e->peer_epoch;
   for (int q = 0; q < world; ++q) a.peer[q] = e->peers[q];
@@ -3922,7 +3756,9 @@ static int run_hmemo_peer(ksim_engine* e, int max_ev) {
     a.hist = e->d_h_hist;
   }
   KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), st));
-  const void* f = Kt <= 64 ? (const void*)k_hmemo<1, false> : (const void*)k_hmemo<4, false>;
+  const bool gen = a.delay != 0;
+  const void* f = Kt <= 64 ? (gen ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
+                           : (gen ? (const void*)k_hmemo<4, true> : (const void*)k_hmemo<4, false>);
   if (K > resident_cap(e, f, e->hplan->lds)) return KSIM_ERANGE;
   KSIM_HIP(hipEventRecord(e->ev0, st));
   const TypDev* tpp = e->d_tp;
@@ -3988,7 +3824,9 @@ static int run_hmemo_group(ksim_engine* const* engines, int world, int max_ev, b
     e->mplan_dirty = true;  // the unsharded plan is not this one
     lds = std::max(lds, e->hplan->lds);
   }
-  const void* f = Kt <= 64 ? (const void*)k_hmemo_group<1> : (const void*)k_hmemo_group<4>;
+  const bool gen = hdelay_mask() != 0;  // KSIM_HDELAY: the general instantiation
+  const void* f = Kt <= 64 ? (gen ? (const void*)k_hmemo_group<1, true> : (const void*)k_hmemo_group<1, false>)
+                           : (gen ? (const void*)k_hmemo_group<4, true> : (const void*)k_hmemo_group<4, false>);
   if (Kt > resident_cap(e0, f, lds)) return KSIM_OK;
   hipStream_t st = e0->stream;
   KSIM_HIP(hipSetDevice(e0->device));
@@ -4179,10 +4017,9 @@ int ksim_engine_last_run_path(ksim_engine* e, int* path) {
   else if (e->run_mode == 1 || e->last_step_path) *path = KSIM_PATH_STEP;
   else if (e->last_rgo == e->R) *path = KSIM_PATH_RANDOM_GO;
   else if (e->last_scan1 == e->R) *path = KSIM_PATH_SCAN1;
-  else if (e->last_memo == 0 && e->last_hmemo == 0 && e->last_pmemo == 0) *path = KSIM_PATH_REPLAY;
+  else if (e->last_memo == 0 && e->last_hmemo == 0) *path = KSIM_PATH_REPLAY;
   else if (e->last_memo == e->R) *path = KSIM_PATH_MEMO;
   else if (e->last_hmemo == e->R) *path = KSIM_PATH_HMEMO;
-  else if (e->last_pmemo == e->R) *path = KSIM_PATH_PMEMO;
   else *path = KSIM_PATH_MIXED;
   return KSIM_OK;
 }

@@ -103,13 +103,14 @@ struct HMemoArgs {
   // One shard per process / GPU (ksim_engine_set_shard_peers): `gran` is this shard's own exchange buffer
   // (uncached device memory), peer[q] shard q's buffer mapped here (IPC; own included); each step's
   // granules are stored into every peer's buffer (system scope, over xGMI) and polled in the own one.
-  // epoch tags a run's granules (no reset between runs, so no rank can clear a granule a peer already
-  // wrote).  npeer = 0: the exchange buffer is shared in place (one launch).
+  // epoch (24 bits, never 0 with peers) tags a run's granules (no reset between runs, so no rank can clear
+  // a granule a peer already wrote).  npeer = 0: the exchange buffer is shared in place (one launch).
   int npeer, epoch;
   unsigned long long* peer[kMaxPeers];
   int skip;                 // the dead-class skip (create-only streams; class slots < 1024)
   int pf;                   // one workgroup per replica: 1 = wave 0 lists the next refresh's F evaluations after its
                             // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
+  int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -235,9 +236,27 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
   return (unsigned)row_max16((int)m);
 }
 
+// KSIM_HDELAY stress delays at the hand-over points of a step (general instantiations only): a wave about
+// to read something another wave of the same step may be writing sleeps 0-3 x ~3.4 us on about half the
+// steps (a hash of step, wave and workgroup), so the late-reader orders that are rare on an idle chip
+// happen thousands of times per run.  Bits: 1 waves 1-15 before reading the step's skip condition (the
+// r03 dead-set race: wave 0 decides and marks the class dead first), 2 wave 1 before its F list (the F
+// waves wait on the list hand-over), 4 wave 0 before its decision (the bulk finishes the step first),
+// 8 the class waves before the class pass.  Results must not change (tests/test_gpu_hdelay.py).
+__device__ __forceinline__ void hdelay(int mask, int bit, int step, int wave, int wg) {
+  if (!(mask & bit)) return;
+  unsigned h = (unsigned)step * 0x9E3779B1u ^ (unsigned)(wave * 0x85EBCA77) ^ (unsigned)(wg * 0xC2B2AE3D) ^ (unsigned)bit;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  if (h & 1u) return;
+  for (int i = (int)((h >> 1) & 3u); i > 0; --i) __builtin_amdgcn_s_sleep(127);
+}
+
 // kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1); kSub = 0: the lean one-
-// workgroup form (K = 1, the exchange compiled out).  kProf: the KSIM_PROFILE phase timers (compiled
-// out of the lean launches, as k_memo's: the step loop's scalar registers are what it runs short of).
+// workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the
+// KSIM_PROFILE phase timers and the KSIM_HDELAY stress delays (compiled out of the lean launches, as
+// k_memo's: the step loop's scalar registers are what it runs short of).
 template <int kSub, bool kProf>
 __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __restrict__ tp_all, const int wg) {
   using namespace ksim_replay;
@@ -370,6 +389,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     // changes.  Every workgroup (every shard) holds the same dead set, taken from the same exchanges, so
     // all skip the same steps; the changed node d is carried to the next decided step's refresh.
     {
+      if constexpr (kProf)
+        if (wv != 0) hdelay(a.delay, 1, step, wv, wg);
       const int cs0 = __builtin_amdgcn_readfirstlane(sh.evc[eb]);
       const int pd = __builtin_amdgcn_readfirstlane(sh.pdead[cur]);
       if (a.skip && cs0 >= 0 && (cs0 == pd || ((sh.dead[cs0 >> 5] >> (cs0 & 31)) & 1u))) {
@@ -427,6 +448,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         if (w0list) {
           // listed by wave 0 after the previous decided step's Bind
         } else if (wv == 1) {
+          if constexpr (kProf) hdelay(a.delay, 2, step, wv, wg);
           const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst[cur]);
           int base = 1;  // item 0: d's current state
           for (int g0 = 0; g0 < G; g0 += 64) {
@@ -489,6 +511,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       } else {
         const int ct = tid - (kFW + 1) * 64;  // class-wave thread
         const unsigned long long tc0 = (prof && ct == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        if constexpr (kProf) hdelay(a.delay, 8, step, wv, wg);
         const NodeV dold = uniform_node(&sh.dold[cur]);
         const NodeSum sn = node_sum(dn), so = node_sum(dold);
         for (int c = ct; c < C; c += kCW * 64) {
@@ -637,6 +660,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     }
     // ---- 4. the event: the winner of its class (create) or the unbind (delete); wave 0
     if (wv == 0) {
+      if constexpr (kProf) hdelay(a.delay, 4, step, wv, wg);
       const PodDev p = uniform_pod(&sh.ev[eb]);
       int rk = -1, mask = 0, ndead = -1;
       bool write = false;
@@ -650,8 +674,13 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           // the slices' maxima and feasible counts: granules {tag, key}, {tag, count} (k_replay's exchange)
           const size_t so = (size_t)(seq & 1) * Kt * 2;
           unsigned long long* slot = gr + so;
+          // tag: {epoch (24 bits) | seq mod 256} across processes (a peer is at most one exchange ahead,
+          // so a slot holds this exchange or the one two before: 8 bits of seq tell them apart, and a
+          // 24-bit epoch keeps the previous runs' granules out); {seq + 1 (24 bits)} in one launch, whose
+          // buffer is zeroed before it (never a zero tag)
           const unsigned long long tag =
-              (unsigned long long)(((unsigned)a.epoch << 24) | ((unsigned)(seq + 1) & 0xffffffu)) << 32;
+              (unsigned long long)(a.epoch ? (((unsigned)a.epoch << 8) | ((unsigned)(seq + 1) & 0xffu))
+                                           : ((unsigned)(seq + 1) & 0xffffffu)) << 32;
           const int np = a.npeer;
           if (np > 0) {  // lane q -> shard q's buffer
             if (lane < np) {
@@ -881,10 +910,10 @@ __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __
 
 // One launch over the shards of a node-sharded cluster on one device (ksim_shard_group_run): workgroup
 // blockIdx.x is workgroup blockIdx.x % K of shard blockIdx.x / K, with that shard engine's arguments.
-template <int kSub>
+template <int kSub, bool kProf>
 __global__ __launch_bounds__(kHBlock) void k_hmemo_group(const HMemoArgs* __restrict__ sa, int K) {
   const HMemoArgs a = sa[blockIdx.x / K];
-  hmemo_body<kSub, false>(a, a.tp, (int)blockIdx.x % K);
+  hmemo_body<kSub, kProf>(a, a.tp, (int)blockIdx.x % K);
 }
 
 // ---------------------------------------------------------------------------

@@ -22,8 +22,8 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libksim_hip.so")
 DATA_DIR = os.path.join(REPO_DIR, "data", "openb")
 
-KSIM_OK, KSIM_EINVAL, KSIM_ENOMEM, KSIM_EHIP, KSIM_ERANGE, KSIM_ESTATE, KSIM_ENOTSUP, KSIM_ENODEV, KSIM_EIO = \
-    0, -1, -2, -3, -4, -5, -6, -7, -8
+KSIM_OK, KSIM_EINVAL, KSIM_ENOMEM, KSIM_EHIP, KSIM_ERANGE, KSIM_ESTATE, KSIM_ENOTSUP, KSIM_ENODEV, KSIM_EIO, KSIM_EPEER = \
+    0, -1, -2, -3, -4, -5, -6, -7, -8, -9
 KSIM_TYPE_ANY = 0xFFFFFFFF
 MAX_GPU = 8
 NUM_TAGS = 9
@@ -198,12 +198,57 @@ def build(quiet=True):
     subprocess.run(cmd, check=True)
 
 
+def hip_runtime_path():
+    """The HIP runtime file this process binds libksim_hip.so to, or None for the one its RUNPATH finds
+    (/opt/rocm).  One HIP / HSA runtime per process: torch ships its own libamdhip64
+    (SONAME libamdhip64.so.7) and its libtorch_hip NEEDs it as "libamdhip64.so", a name the dynamic
+    linker never matches with /opt/rocm's libamdhip64.so.7.2.x, so a process that loads ksim first and
+    torch later maps two runtimes, each opening the device.  The other way round the linker does match:
+    loaded first by path, torch's copy satisfies this library's NEEDED libamdhip64.so.7 (by SONAME) and
+    torch's own later load (same file).  So where torch is installed its runtime is the process's.
+    KSIM_HIP_RUNTIME: auto (default: torch's if installed, else /opt/rocm's), torch (required),
+    system (/opt/rocm's: a process that never imports torch), or a path to a libamdhip64 file."""
+    mode = os.environ.get("KSIM_HIP_RUNTIME", "auto")
+    if mode == "system":
+        return None
+    if mode not in ("auto", "torch"):
+        return mode
+    import importlib.util
+    spec = importlib.util.find_spec("torch")  # (locates torch without importing it)
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so") if spec and spec.origin else None
+    if path and os.path.exists(path):
+        return path
+    if mode == "torch":
+        raise ImportError("KSIM_HIP_RUNTIME=torch but torch's libamdhip64.so was not found")
+    return None
+
+
+def hip_runtimes():
+    """The HIP and HSA runtime files mapped into this process (/proc/self/maps): one of each is the
+    contract (tests/test_runtime.py)."""
+    out = {"hip": set(), "hsa": set()}
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) < 6:
+                continue
+            base = os.path.basename(parts[5])
+            if base.startswith("libamdhip64.so"):
+                out["hip"].add(os.path.realpath(parts[5]))
+            elif base.startswith("libhsa-runtime64.so"):
+                out["hsa"].add(os.path.realpath(parts[5]))
+    return {k: sorted(v) for k, v in out.items()}
+
+
 def lib():
     global _LIB
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError("libksim_hip.so not built (%s); run `make -C %s` or __graft_entry__.build()"
                               % (LIB_PATH, PKG_DIR))
+        rt = hip_runtime_path()
+        if rt is not None:
+            C.CDLL(rt, mode=C.RTLD_GLOBAL)  # the process's HIP runtime, before the library binds one
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
@@ -383,8 +428,8 @@ class Engine:
     def __init__(self, n_nodes, n_replicas=1, device=0, nodes_per_block=0, steps_per_graph=0, wgs_per_replica=0,
                  run_mode=0):
         """run_mode (ksim_config.run_mode): 0 auto (FGD: k_memo, else k_hmemo, else k_replay), 1 k_step per
-        pod (hipGraph), 2 k_replay only, 3 k_memo required, 4 k_memo decider mode, 5 k_hmemo required,
-        6 k_pmemo required (pipelined memoised FGD on node slices of <= 64 ranks)."""
+        pod (hipGraph), 2 k_replay only, 3 k_memo required, 4 k_memo decider mode, 5 k_hmemo required
+        (anything else: KsimError KSIM_EINVAL)."""
         self.N, self.R = n_nodes, n_replicas
         cfg = Config(device, nodes_per_block, steps_per_graph, wgs_per_replica, run_mode)
         h = _VP()
@@ -584,13 +629,12 @@ class Engine:
         return s.value
 
     def last_run_path(self):
-        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go' | 'k_scan1' |
-        'k_pmemo': the kernels the last run()
+        """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go' | 'k_scan1': the kernels
+        the last run()
         used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
-        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1",
-                "k_pmemo"][k.value]
+        return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1"][k.value]
 
     def last_run_wgs(self):
         k = C.c_int(0)
@@ -622,7 +666,7 @@ class Engine:
 
 
 SHARD_ID_BYTES = 128
-SHARD_HANDLE_BYTES = 64
+SHARD_HANDLE_BYTES = 128
 # ksim_shard_exchange_fn
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p)
 

@@ -48,9 +48,9 @@ def test_struct_layouts_match_c():
 
 def test_abi_version_and_errors():
     L = ksim.lib()
-    assert L.ksim_abi_version() == 1
-    for code in range(0, -9, -1):
-        assert L.ksim_strerror(code)
+    assert L.ksim_abi_version() == 2
+    msgs = [L.ksim_strerror(code) for code in range(0, -10, -1)]
+    assert all(msgs) and len(set(msgs)) == len(msgs) and L.ksim_strerror(-10) == b"unknown error"
     # null / bad arguments are rejected before any device work
     assert L.ksim_engine_create(None, 0, 1, None) == ksim.KSIM_EINVAL
 

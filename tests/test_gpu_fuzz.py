@@ -1,7 +1,6 @@
 """Parity fuzz on adversarial synthetic clusters (tests/fuzz_cases.py): every policy through every
 execution path -- auto (k_memo for FGD, k_replay for the rest), k_replay forced, k_step per pod
-(hipGraph), k_hmemo forced for FGD (run_mode 5), k_memo forced for FGD, k_pmemo forced for FGD on create-only
-streams (run_mode 6) -- bit-exact against the oracle per event (node, GPU set, score,
+(hipGraph), k_hmemo forced for FGD (run_mode 5), k_memo forced for FGD -- bit-exact against the oracle per event (node, GPU set, score,
 feasible count, status) and in the final cluster state.  Every test needs a gfx950 device.
 """
 import pytest
@@ -214,21 +213,4 @@ def test_fuzz_scan1_records_in_lds(name, pol, sel):
         eng.close()
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert len(got) == len(want) and not bad, "first mismatch at event %d" % bad[0]
-    check_state(state, want_state)
-
-
-@pytest.mark.parametrize("wgs", [0, 1, 3])
-def test_fuzz_pmemo_forced_fgd(case, wgs):
-    # k_pmemo (run_mode 6): create-only streams on slices of <= 64 ranks (auto: one slot per workgroup on
-    # the small cases); streams with deletes and slicings past 64 ranks are refused loudly
-    want, want_state, _ = O.run_events(case["onodes"], case["otypical"], case["oevents"], policy=O.POL_FGD,
-                                       gpu_sel=O.SEL_FGD, threads=16)
-    try:
-        got, state = run_engine(case, "FGD", 6, wgs=wgs)
-    except ksim.KsimError as e:
-        has_delete = any(case["events"][i].is_delete for i in range(case["n_events"]))
-        if e.code != ksim.KSIM_ENOTSUP or not (has_delete or (wgs and len(case["onodes"]) > 64 * wgs)):
-            raise
-        pytest.skip("k_pmemo does not serve this case")
-    assert got == want
     check_state(state, want_state)

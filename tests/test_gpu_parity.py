@@ -243,7 +243,9 @@ def test_reserve_unreserve_roundtrip(default_trace):
     eng.unreserve(0, share, a, m1)
     assert bytes(eng.nodes(0)) == before
     # a second Unreserve of the same pod would push the devices past 1000 milli: reported, not applied
-    # (the cgo plugin also forgets a binding once released, go/ksim_gpu.go release)
+    # (ADVICE r2).  The guard checks devices and CPU only, so it catches this because the nodes hold no
+    # other pod; in general the caller's record of its bindings prevents a double release (the cgo plugin
+    # forgets a binding once released, go/ksim_gpu.go release; include/ksim_engine.h)
     for pod, node, mask in ((whole, b, m2), (share, a, m1)):
         with pytest.raises(ksim.KsimError) as ei:
             eng.unreserve(0, pod, node, mask)

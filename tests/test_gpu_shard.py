@@ -169,11 +169,13 @@ def test_host_exchange_bad_gather_fails(default_trace, bad):
     assert ei.value.code == ksim.KSIM_ESTATE
 
 
-def _device_rank_main(rank, world, port, n_ev, deletes, q):
+def _device_rank_main(rank, world, port, n_ev, deletes, q, epoch0=None, n_runs=2):
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if epoch0 is not None:
+        os.environ["KSIM_PEER_EPOCH0"] = epoch0  # the run epoch starts just below its 24-bit wrap
     dist.init_process_group("gloo", rank=rank, world_size=world)
     t = ksim.Trace.openb("default")
     rp = t.replay(seed=7)
@@ -183,18 +185,20 @@ def _device_rank_main(rank, world, port, n_ev, deletes, q):
         events, _ = helpers.delete_stream(t, rp, n_ev, p_delete=0.2, seed=4)
         n = len(events)
     runs = []
-    for _ in range(2):  # two runs: the second's granules carry the next epoch over the first's
+    for _ in range(n_runs):  # several runs: each run's granules carry the next epoch over the last's
         runs.append(SH.run_distributed(nodes, t.typical(), events, n, dist, policy="FGD", seed=3, exchange="device"))
-    q.put((rank, runs[0][0], runs[1][0], runs[0][1]))
+    q.put((rank, [r[0] for r in runs], runs[0][1]))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(150)
-@pytest.mark.parametrize("deletes", [False, True], ids=["create", "delete"])
-def test_device_exchange_two_processes(default_trace, deletes):
+@pytest.mark.parametrize("deletes,epoch0,n_runs", [(False, None, 2), (True, None, 2), (False, "0xfffffe", 3)],
+                         ids=["create", "delete", "epoch-wrap"])
+def test_device_exchange_two_processes(default_trace, deletes, epoch0, n_runs):
     # two shard processes on the one GPU, each a persistent k_hmemo over its slices, exchanging per-pod
     # granules through each other's IPC-mapped buffers (the one-process-per-GPU mode's exchange; on a
-    # node the peers' buffers sit on other GPUs, over xGMI)
+    # node the peers' buffers sit on other GPUs, over xGMI).  epoch-wrap: three runs at epochs 0xffffff,
+    # 1, 2 (the 24-bit run epoch wraps past 0), each bit-exact
     import multiprocessing as mp
     import socket
     n_ev = 600
@@ -204,7 +208,8 @@ def test_device_exchange_two_processes(default_trace, deletes):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_device_rank_main, args=(r, 2, port, n_ev, deletes, q)) for r in range(2)]
+    procs = [ctx.Process(target=_device_rank_main, args=(r, 2, port, n_ev, deletes, q, epoch0, n_runs))
+             for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -227,8 +232,34 @@ def test_device_exchange_two_processes(default_trace, deletes):
     want, _, _ = O.run_events(helpers.oracle_subset(default_trace, rp, keep), helpers.oracle_typical(default_trace),
                               oev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, seed=3, threads=16)
     for r in res:
-        assert r[1] == want and r[2] == want
-    print("device exchange world 2: %d events, rank times %.2f / %.2f ms" % (len(oev), res[0][3], res[1][3]))
+        assert len(r[1]) == n_runs and all(run == want for run in r[1])
+    print("device exchange world 2: %d events, rank times %.2f / %.2f ms" % (len(oev), res[0][2], res[1][2]))
+
+
+def test_peer_handle_refusals(default_trace):
+    # ksim_engine_set_shard_peers checks every peer's device before it maps anything: a handle naming a GPU
+    # that is not visible here is KSIM_EPEER, a malformed one KSIM_EINVAL (include/ksim_engine.h)
+    import struct
+    rp = default_trace.replay(seed=7)
+    nodes = helpers.subset_nodes(rp, list(range(0, default_trace.num_nodes, 8)))
+    parts = SH.partition(nodes, 2)
+    e = ksim.Engine(len(parts[0][2]), 1)
+    try:
+        e.set_shard(0, 2, parts[0][0], len(nodes), None)
+        own = e.shard_peer_handle()
+        assert len(own) == ksim.SHARD_HANDLE_BYTES and own[64:68] == b"KSPH"
+        foreign = bytearray(own)
+        foreign[68:80] = struct.pack("<III", 0xfff0, 0xfe, 0x1f)  # PCI fff0:fe:1f: no such GPU here
+        with pytest.raises(ksim.KsimError) as ei:
+            e.set_shard_peers([own, bytes(foreign)])
+        assert ei.value.code == ksim.KSIM_EPEER
+        bad = bytearray(own)
+        bad[64:68] = b"XXXX"
+        with pytest.raises(ksim.KsimError) as ei:
+            e.set_shard_peers([own, bytes(bad)])
+        assert ei.value.code == ksim.KSIM_EINVAL
+    finally:
+        e.close()
 
 
 def _host_rank_main(rank, world, port, policy, n_ev, q):
@@ -252,8 +283,8 @@ def test_host_exchange_two_processes(default_trace, name, pol, sel):
     # two shard processes on the one GPU, their per-step records exchanged over gloo: the shard
     # kernels and the commit of the multi-process mode with a real cross-process exchange (RCCL
     # refuses two ranks on one device, so the ncclAllGather itself stays world-1 here)
-    # stdlib multiprocessing: torch (which carries its own HIP runtime) is imported by the ranks
-    # only, never into this process, whose engines already hold /opt/rocm's
+    # stdlib multiprocessing: the ranks import torch.distributed for the gloo gather; ksim binds them to
+    # torch's HIP runtime (ksim.hip_runtime_path), one runtime per process
     import multiprocessing as mp
     import socket
     n_ev = 600
