@@ -272,6 +272,9 @@ def main():
     sweep_cpu = None
     if args.config == "c4" and rank == 0 and world == 1 and not args.no_cpu_baseline:
         sweep_cpu = cpu_baseline_sweep(workers=args.cpu_threads)
+    # world 1 never imports torch: the process holds the one HIP runtime ksim binds (a profiler's, under
+    # rocprofv3), and the engine's own run() synchronises and times the launch.  World > 1: torch.distributed
+    # for the timing barrier and the job reduction only (no collective on the data path)
     dist = None
     if world > 1:
         import torch
@@ -287,10 +290,6 @@ def main():
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl")
-    import torch
-
-    if world == 1:
-        torch.cuda.set_device(0)
 
     trace = ksim.Trace.openb("default")
     if args.config == "c4":
@@ -324,10 +323,9 @@ def main():
         eng.run()
 
     def barrier():
-        torch.cuda.synchronize()
+        # eng.run() returns after its stream synchronised, so the device is idle here
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
 
     barrier()
     t0 = time.perf_counter()
@@ -424,6 +422,7 @@ def main():
     if args.config == "c4" or args.report:
         line["report_ms_per_step"] = eng.last_report_ms()
     line["build_id"] = ksim.build_id()  # sha256 prefix of the library's sources (ksim.source_hash())
+    line["hip_runtime"] = ksim.hip_runtimes()  # one HIP / HSA runtime per process
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         # like for like: the GPU line's seeds as single-threaded replicas on as many cores; beside it one
         # replica with `cpu_threads` workers per cycle (parallelize.Until) and one thread on a prefix
@@ -435,6 +434,9 @@ def main():
         line["cpu_baseline"] = sweep_cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if os.environ.get("KSIM_MAPS_OUT"):  # the process's mappings, to symbolise an exit-path fault
+        with open("/proc/self/maps") as f, open(os.environ["KSIM_MAPS_OUT"], "w") as g:
+            g.write(f.read())
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

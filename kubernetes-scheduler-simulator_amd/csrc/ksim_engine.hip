@@ -2091,6 +2091,13 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   return KSIM_OK;
 }
 
+// KSIM_HDELAY=<mask>: the memoised kernels' hand-over stress delays (ksim_memo.hpp hdelay; the bits are
+// per kernel); a nonzero mask selects the general (non-lean) instantiation, which alone carries them.
+static int hdelay_mask() {
+  const char* v = std::getenv("KSIM_HDELAY");
+  return v ? (int)(std::strtol(v, nullptr, 0) & 0xff) : 0;
+}
+
 static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, int max_ev) {
   int rc;
   hipStream_t st = e->stream;
@@ -2126,14 +2133,16 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     const char* sk = std::getenv("KSIM_SKIP");
     ma.skip = !(sk && sk[0] == '0');
   }
+  ma.delay = hdelay_mask();
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   const bool tracing = pe && pe[0] == '2';
   unsigned long long* d_trace = nullptr;
   const int TS = std::min(max_ev, 4000);
+  constexpr int kT = ksim_memo::kTrace;
   if (tracing) {
-    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * 4 * (size_t)Rg * pl.K * TS));
-    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * (size_t)Rg * pl.K * TS, st));
+    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * kT * (size_t)Rg * pl.K * TS));
+    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * kT * (size_t)Rg * pl.K * TS, st));
     ma.trace = d_trace;
     ma.trace_steps = TS;
   }
@@ -2145,8 +2154,10 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   // the general instantiation for the profile / trace / report / deletes / no score table, else the lean one
   const bool general = profile || tracing || e->report || !e->d_th ||
                        std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; });
+  // KSIM_HDELAY: the lean kernel with the stress delays compiled in (or the general one, which has them)
   const void* f = pl.decider ? (const void*)ksim_memo::k_memo<true, true>
-                             : (general ? (const void*)ksim_memo::k_memo<false, true> : (const void*)ksim_memo::k_memo<false, false>);
+                  : general ? (const void*)ksim_memo::k_memo<false, true>
+                  : ma.delay ? (const void*)ksim_memo::k_memo<false, false, true> : (const void*)ksim_memo::k_memo<false, false>;
   const TypDev* tpp = e->d_tp;
   rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
   if (rc) return rc;
@@ -2158,12 +2169,12 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     // (s_memrealtime, 100 MHz); replica 0 only
     KSIM_HIP(hipStreamSynchronize(st));
     const int K = pl.K;
-    std::vector<unsigned long long> h((size_t)4 * Rg * K * TS);
+    std::vector<unsigned long long> h((size_t)kT * Rg * K * TS);
     KSIM_HIP(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     KSIM_HIP(hipFree(d_trace));
     std::vector<int> evo((size_t)TS);
     KSIM_HIP(hipMemcpy(evo.data(), e->d_m_evo, sizeof(int) * TS, hipMemcpyDeviceToHost));
-    auto at = [&](int w, int s, int k) { return (double)h[((size_t)w * TS + s) * 4 + k]; };
+    auto at = [&](int w, int s, int k) { return (double)h[((size_t)w * TS + s) * kT + k]; };
     double crit = 0, hand = 0, hmax = 0, period = 0, lag = 0, f0 = 0, spin = 0;
     int nc = 0, nh = 0, nf = 0;
     for (int s = 1; s + 1 < TS; ++s) {
@@ -2277,13 +2288,6 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
 }
 
 static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps);
-
-// KSIM_HDELAY=<mask>: the memoised kernels' hand-over stress delays (ksim_hmemo.hpp hdelay, ksim_memo.hpp);
-// a nonzero mask selects the general (non-lean) instantiation, which alone carries them.
-static int hdelay_mask() {
-  const char* v = std::getenv("KSIM_HDELAY");
-  return v ? (int)(std::strtol(v, nullptr, 0) & 0xff) : 0;
-}
 
 // k_hmemo's arguments for the planned launch (one group of Rg replicas from d_replist + first).
 static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {

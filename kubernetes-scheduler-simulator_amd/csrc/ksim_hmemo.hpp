@@ -236,22 +236,11 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
   return (unsigned)row_max16((int)m);
 }
 
-// KSIM_HDELAY stress delays at the hand-over points of a step (general instantiations only): a wave about
-// to read something another wave of the same step may be writing sleeps 0-3 x ~3.4 us on about half the
-// steps (a hash of step, wave and workgroup), so the late-reader orders that are rare on an idle chip
-// happen thousands of times per run.  Bits: 1 waves 1-15 before reading the step's skip condition (the
-// r03 dead-set race: wave 0 decides and marks the class dead first), 2 wave 1 before its F list (the F
-// waves wait on the list hand-over), 4 wave 0 before its decision (the bulk finishes the step first),
-// 8 the class waves before the class pass.  Results must not change (tests/test_gpu_hdelay.py).
-__device__ __forceinline__ void hdelay(int mask, int bit, int step, int wave, int wg) {
-  if (!(mask & bit)) return;
-  unsigned h = (unsigned)step * 0x9E3779B1u ^ (unsigned)(wave * 0x85EBCA77) ^ (unsigned)(wg * 0xC2B2AE3D) ^ (unsigned)bit;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  if (h & 1u) return;
-  for (int i = (int)((h >> 1) & 3u); i > 0; --i) __builtin_amdgcn_s_sleep(127);
-}
+// KSIM_HDELAY stress delays (ksim_memo::hdelay).  Bits here: 1 waves 1-15 before reading the step's
+// skip condition (the r03 dead-set race: wave 0 decides and marks the class dead first), 2 wave 1 before
+// its F list (the F waves wait on the list hand-over), 4 wave 0 before its decision (the bulk finishes the
+// step first), 8 the class waves before the class pass.  Results must not change (tests/test_gpu_hdelay.py).
+using ksim_memo::hdelay;
 
 // kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1); kSub = 0: the lean one-
 // workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the

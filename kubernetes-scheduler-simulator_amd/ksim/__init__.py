@@ -19,7 +19,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libksim_hip.so")
+# KSIM_LIB_PATH: another build of the library (A/B runs of two builds on one box); default the in-tree one
+LIB_PATH = os.environ.get("KSIM_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libksim_hip.so")
 DATA_DIR = os.path.join(REPO_DIR, "data", "openb")
 
 KSIM_OK, KSIM_EINVAL, KSIM_ENOMEM, KSIM_EHIP, KSIM_ERANGE, KSIM_ESTATE, KSIM_ENOTSUP, KSIM_ENODEV, KSIM_EIO, KSIM_EPEER = \
@@ -205,14 +206,23 @@ def hip_runtime_path():
     linker never matches with /opt/rocm's libamdhip64.so.7.2.x, so a process that loads ksim first and
     torch later maps two runtimes, each opening the device.  The other way round the linker does match:
     loaded first by path, torch's copy satisfies this library's NEEDED libamdhip64.so.7 (by SONAME) and
-    torch's own later load (same file).  So where torch is installed its runtime is the process's.
-    KSIM_HIP_RUNTIME: auto (default: torch's if installed, else /opt/rocm's), torch (required),
-    system (/opt/rocm's: a process that never imports torch), or a path to a libamdhip64 file."""
+    torch's own later load (same file).  So where torch is installed its runtime is the process's --
+    unless an HSA or HIP runtime is already mapped (a profiler's preload: rocprofv3 maps /opt/rocm's HSA
+    before the program starts), whose directory's libamdhip64 then binds, so that HIP and HSA match.
+    KSIM_HIP_RUNTIME: auto (default: as above), torch (required), system (/opt/rocm's: a process that
+    never imports torch), or a path to a libamdhip64 file."""
     mode = os.environ.get("KSIM_HIP_RUNTIME", "auto")
     if mode == "system":
         return None
     if mode not in ("auto", "torch"):
         return mode
+    if mode == "auto":
+        mapped = hip_runtimes()
+        for path in mapped["hip"] + mapped["hsa"]:
+            d = os.path.dirname(path)
+            for name in ("libamdhip64.so.7", "libamdhip64.so"):
+                if os.path.exists(os.path.join(d, name)):
+                    return os.path.join(d, name)
     import importlib.util
     spec = importlib.util.find_spec("torch")  # (locates torch without importing it)
     path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so") if spec and spec.origin else None

@@ -21,6 +21,8 @@ import ksim, bench
 t = ksim.Trace.openb('default'); eng = bench._engine_on(0, t, [42, 43], 0); eng.run()
 import torch; torch.cuda.set_device(0); torch.cuda.synchronize(); x = torch.ones(4, device='cuda'); print(float(x.sum()))
 eng.run(); eng.close(); print(json.dumps(ksim.hip_runtimes()))"
+step memotests 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu \
+  tests/test_gpu_memo.py
 step newtests 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_gpu_hdelay.py tests/test_gpu_shard.py -k "hdelay or delay or peer or device_exchange"
 step bench 300 python -u bench.py

@@ -1,5 +1,11 @@
 """Hand-over stress for the memoised FGD kernels (KSIM_HDELAY, round-3 verdict item 1).
 
+k_memo (since r04) has no end-of-step barrier either: every wave takes a step's outcome from the granule
+into its registers, the class found dead rides in a register until wave 0's fold is behind a barrier, and
+wave 0 stores the Bind into the cluster only after the next barrier (every wave has read the record before
+it).  Its delay points: 1 every wave before it takes the outcome, 2 wave 0 before the deferred Bind store,
+4 every wave before the step start; the lean kernel with them compiled in runs the dead-class skip too.
+
 k_hmemo has no workgroup barrier inside a step: wave 0 (the event's own class, the decision, the Bind) and
 waves 1-15 (every other class's refresh) hand work over through LDS counters and double-buffered state,
 and join once, at the end-of-step barrier.  A wave that reads something late -- after another wave of the
@@ -145,3 +151,42 @@ def test_hmemo_shard_group_delays(c5, monkeypatch):
         assert g.results() == want
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("mask", ["0x7", "0x1", "0x6"])
+def test_memo_c2_delays(default_trace, c2_replay, monkeypatch, mask):
+    # the C2 job on k_memo (run_mode 3: 25 co-resident workgroups per replica), the lean kernel with the delays
+    monkeypatch.setenv("KSIM_HDELAY", mask)
+    eng = c2_engine(default_trace, SEEDS, 3)
+    try:
+        eng.run()
+        assert eng.last_run_path() == "k_memo" and eng.last_run_wgs() == 25
+        got = [eng.results(r) for r in range(len(SEEDS))]
+    finally:
+        eng.close()
+    for r in range(len(SEEDS)):
+        assert got[r] == c2_replay[r], "seed %d differs from k_replay" % SEEDS[r]
+
+
+def test_memo_deletes_report_delays(default_trace, monkeypatch):
+    # the general k_memo (a create / delete stream with the per-event report) with every delay point on
+    monkeypatch.setenv("KSIM_HDELAY", "0x7")
+    rp = default_trace.replay(seed=44, tune_ratio=1.3, shuffle=True)
+    keep = list(range(0, default_trace.num_nodes, 3))
+    evs, oev = helpers.delete_stream(default_trace, rp, 1500, p_delete=0.3, seed=5)
+    arr, n = default_trace.typical()
+    eng = ksim.Engine(len(keep), 1, run_mode=3)
+    try:
+        eng.set_report(True)
+        eng.set_nodes(0, helpers.subset_nodes(rp, keep))
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        eng.load_events(0, evs, len(evs))
+        eng.run()
+        assert eng.last_run_path() == "k_memo"
+        got = eng.results(0)
+    finally:
+        eng.close()
+    want, _, _ = O.run_events(helpers.oracle_subset(default_trace, rp, keep), helpers.oracle_typical(default_trace),
+                              oev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=16)
+    assert got == want

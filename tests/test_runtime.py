@@ -35,21 +35,46 @@ def torch_installed():
     return importlib.util.find_spec("torch") is not None
 
 
-@pytest.mark.parametrize("order", ["ksim-then-torch", "torch-then-ksim", "bench"])
+@pytest.mark.parametrize("order", ["ksim-then-torch", "torch-then-ksim", "torchrun-rank"])
 def test_one_hip_and_hsa_runtime(order):
     if not torch_installed():
         pytest.skip("torch is not installed: only /opt/rocm's runtime exists")
     code = {
         "ksim-then-torch": "import ksim; ksim.lib(); import torch, torch.distributed",
         "torch-then-ksim": "import torch, torch.distributed; import ksim; ksim.lib()",
-        # what bench.py imports before and around its timed region (replica mode and torchrun ranks)
-        "bench": "import bench, ksim; ksim.lib(); import torch, torch.distributed; import ksim.shard, ksim.sweep",
+        # a bench.py rank under torchrun (world > 1): torch.distributed for the barrier, the engine, the shards
+        "torchrun-rank": "import bench, ksim; import torch, torch.distributed; ksim.lib(); import ksim.shard, ksim.sweep",
     }[order]
     rt = maps_after(code)
     assert len(rt["hip"]) == 1 and len(rt["hsa"]) == 1, rt
     # and it is torch's: the runtime torch's own libraries and its RCCL are bound to
     assert os.path.dirname(rt["hip"][0]) == os.path.dirname(rt["hsa"][0])
     assert "torch" in rt["hip"][0]
+
+
+def test_bench_world1_imports_no_torch():
+    # bench.py at world 1 (the driver's default run) never imports torch: its one runtime is ksim's
+    out = subprocess.run([sys.executable, "-c", PRELUDE + "import bench, ksim; ksim.lib(); import ksim.sweep\n"
+                          "print('torch' in sys.modules)"], capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "False"
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    main = src[src.index("def main():"):src.index("def _sharded_engine")]
+    # torch appears in main() only under world > 1
+    for i, ln in enumerate(main.splitlines()):
+        if "import torch" in ln:
+            assert "world > 1" in "\n".join(main.splitlines()[max(0, i - 8):i]), ln
+
+
+def test_runtime_follows_a_preloaded_hsa():
+    # under rocprofv3 /opt/rocm's HSA is mapped before the program runs: ksim then binds the HIP runtime
+    # beside it, so HIP and HSA match (ksim.hip_runtime_path)
+    hsa = "/opt/rocm/lib/libhsa-runtime64.so.1"
+    if not os.path.exists(hsa):
+        pytest.skip("no /opt/rocm HSA runtime")
+    rt = maps_after("import ctypes; ctypes.CDLL(%r, mode=ctypes.RTLD_GLOBAL); import ksim; ksim.lib()" % hsa)
+    assert len(rt["hip"]) == 1 and len(rt["hsa"]) == 1, rt
+    assert os.path.dirname(rt["hip"][0]) == os.path.dirname(rt["hsa"][0]) and "torch" not in rt["hip"][0]
 
 
 def test_system_runtime_without_torch():
