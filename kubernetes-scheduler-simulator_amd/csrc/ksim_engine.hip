@@ -795,35 +795,57 @@ void k_replay(ksim_replay::ReplayArgs a,
       }
     }
   };
-  // Wave 0, PWR+FGD: the A round of the current step (seq) -- publish this slice's min / max raw
-  // PWR score, feasible count and Score error, then every workgroup reduces all K of them.  The
-  // slots are safe to reuse two steps later for the same reason as the key round's.
-  auto exchange_a = [&](int c, int e, int l, int h, int* gc, int* ge, int* gl, int* gh) -> bool {
-    unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+  // Wave 0, PWR+FGD: the A round of the current step (seq), published BEFORE the pending key round
+  // completes, so that its hand-off overlaps that one.  This slice's aggregate without the pending best
+  // node b -- min / max raw PWR score, feasible count, Score error -- and b's raw score both as it is
+  // (pre) and as the pending Bind leaves it (post, the virtual slot): granules 4-6 and 3, 7.  Once the key
+  // round names its winner every workgroup reduces all K, taking post for the winner's slice when the
+  // pending step binds, pre for every other (collect_a).  The slots are safe to reuse two steps later for
+  // the same reason as the key round's.
+  struct AVar { int c0, e0, l0, h0, fpre, epre, rpre, fpost, epost, rpost; };
+  auto a_total = [](const AVar& v, bool post, int* c, int* e, int* l, int* h) {
+    const int f = post ? v.fpost : v.fpre, ev = post ? v.epost : v.epre, rv = post ? v.rpost : v.rpre;
+    *c = v.c0 + f;
+    *e = v.e0 | (f & ev);
+    *l = f ? min(v.l0, rv) : v.l0;
+    *h = f ? max(v.h0, rv) : v.h0;
+  };
+  auto publish_a = [&](const AVar& v) {
+    unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW + (size_t)w * kGranW;
     const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-    if (lane == 0) {
-      gstore(slot + (size_t)w * kGranW + 4, tag | (unsigned)l);
-      gstore(slot + (size_t)w * kGranW + 5, tag | (unsigned)h);
-      gstore(slot + (size_t)w * kGranW + 6, tag | ((unsigned)e << 31) | ((unsigned)c & 0x7fffffffu));
-    }
-    unsigned long long x0[kS], x1[kS], x2[kS];
+    gstore(slot + 4, tag | (unsigned)v.l0);
+    gstore(slot + 5, tag | (unsigned)v.h0);
+    gstore(slot + 6, tag | ((unsigned)v.e0 << 31) | ((unsigned)v.fpre << 30) | ((unsigned)v.epre << 29) |
+                         ((unsigned)v.fpost << 28) | ((unsigned)v.epost << 27) | ((unsigned)v.c0 & 0x7ffffffu));
+    gstore(slot + 3, tag | (unsigned)v.rpre);
+    gstore(slot + 7, tag | (unsigned)v.rpost);
+  };
+  auto collect_a = [&](int kstar, bool bind, int* gc, int* ge, int* gl, int* gh) -> bool {
+    const unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+    const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
+    unsigned long long x[kS][5];
     auto load = [&]() {
 #pragma unroll
       for (int j = 0; j < kS; ++j) {
         const int k = lane + 64 * j;
         if (k < a.K) {
-          x0[j] = gload(slot + (size_t)k * kGranW + 4);
-          x1[j] = gload(slot + (size_t)k * kGranW + 5);
-          x2[j] = gload(slot + (size_t)k * kGranW + 6);
+          x[j][0] = gload(slot + (size_t)k * kGranW + 4);
+          x[j][1] = gload(slot + (size_t)k * kGranW + 5);
+          x[j][2] = gload(slot + (size_t)k * kGranW + 6);
+          x[j][3] = gload(slot + (size_t)k * kGranW + 3);
+          x[j][4] = gload(slot + (size_t)k * kGranW + 7);
         }
       }
     };
     auto ready = [&]() {
       bool r = true;
 #pragma unroll
-      for (int j = 0; j < kS; ++j)
-        r = r && (lane + 64 * j >= a.K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag &&
-                                          (x2[j] & ~0xffffffffull) == tag));
+      for (int j = 0; j < kS; ++j) {
+        bool t = true;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) t = t && (x[j][q] & ~0xffffffffull) == tag;
+        r = r && (lane + 64 * j >= a.K || t);
+      }
       return r;
     };
     load();
@@ -834,27 +856,32 @@ void k_replay(ksim_replay::ReplayArgs a,
       __builtin_amdgcn_s_sleep(1);
       load();
     }
-    int cs = 0, lo = INT_MAX, hi = INT_MIN;
-    bool e1 = false;
+    int cs = 0, lo = INT_MAX, hi = INT_MIN, e1 = 0;
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
-      if (lane + 64 * j < a.K) {
-        const unsigned st = (unsigned)(x2[j] & 0xffffffffull);
-        cs += (int)(st & 0x7fffffffu);
-        e1 = e1 || (st >> 31) != 0u;
-        lo = min(lo, (int)(unsigned)(x0[j] & 0xffffffffull));
-        hi = max(hi, (int)(unsigned)(x1[j] & 0xffffffffull));
+      const int k = lane + 64 * j;
+      if (k < a.K) {
+        const unsigned st = (unsigned)x[j][2];
+        const AVar v{(int)(st & 0x7ffffffu), (int)(st >> 31), (int)(unsigned)x[j][0], (int)(unsigned)x[j][1],
+                     (int)((st >> 30) & 1u), (int)((st >> 29) & 1u), (int)(unsigned)x[j][3],
+                     (int)((st >> 28) & 1u), (int)((st >> 27) & 1u), (int)(unsigned)x[j][4]};
+        int c, e, l, h;
+        a_total(v, bind && k == kstar, &c, &e, &l, &h);
+        cs += c;
+        e1 |= e;
+        lo = min(lo, l);
+        hi = max(hi, h);
       }
     }
     *gc = wave_sum_dpp(cs);
-    *ge = __any(e1) ? 1 : 0;
+    *ge = __any(e1 != 0) ? 1 : 0;
     *gl = wave_min_dpp(lo);
     *gh = wave_max_dpp(hi);
     return ok;
   };
   // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
   // this workgroup's own totals (K == 1); g holds an earlier poll.  Returns the winning key.
-  auto exchange = [&](GranV<kS> g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
+  auto exchange = [&](GranV<kS>& g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
     *ok = true;
     if (a.K == 1) {
       *gc = p_st0; *ge = p_st1; *gl = p_st2; *gh = p_st3;
@@ -1223,33 +1250,50 @@ void k_replay(ksim_replay::ReplayArgs a,
     __syncthreads();
     mark(4);
     if constexpr (kPF) {
-      // 1. finish the pending key round (its latency overlapped the evaluation above) and commit it
-      //    with its own A round's totals
-      if (wv == 0 && pend) {
-        int gc, ge, gl, gh;
-        bool ok = true;
-        const unsigned long long W = exchange(pg, &gc, &ge, &gl, &gh, &ok);
-        if (ok) commit(W, p_st0, p_st1, p_st2, p_st3);
-        else if (lane == 0) { sh.stop = 1; atomicOr(a.fail, 1); }
-      }
-      __syncthreads();
-      if (sh.stop) break;
-      mark(5);
-      // 2. this step's A round: the slice's aggregate plus the pending best node as committed
       if (wv == 0) {
-        int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
+        // 1. this step's A round out first (publish_a): the slice without b, and b pre / post
+        AVar v{sh.agg_cnt, sh.agg_err, sh.agg_lo, sh.agg_hi, 0, 0, 0, 0, 0, 0};
         if (vb >= 0) {
-          const int inf = s_pinf[vb];
-          if (inf & kPfFeas) {
-            ++c;
-            e |= (inf & kPfErr) ? 1 : 0;
-            l = min(l, s_praw[vb]);
-            h = max(h, s_praw[vb]);
-          }
+          const int ip = s_pinf[vb], iq = s_pinf[ns];
+          v.fpre = (ip & kPfFeas) ? 1 : 0;
+          v.epre = (ip & kPfErr) ? 1 : 0;
+          v.rpre = s_praw[vb];
+          v.fpost = (iq & kPfFeas) ? 1 : 0;
+          v.epost = (iq & kPfErr) ? 1 : 0;
+          v.rpost = s_praw[ns];
         }
-        int gc = c, ge = e, gl = l, gh = h;
+        if (a.K > 1 && lane == 0) publish_a(v);
+        // 2. finish the pending key round (its latency overlapped the evaluation above) and commit it with
+        //    its own A round's totals; the column holding its winner
         bool ok = true;
-        if (a.K > 1) ok = exchange_a(c, e, l, h, &gc, &ge, &gl, &gh);
+        unsigned long long W = 0ull;
+        int kstar = -1;
+        if (pend) {
+          int gc_, ge_, gl_, gh_;
+          W = exchange(pg, &gc_, &ge_, &gl_, &gh_, &ok);
+          if (a.K == 1) {
+            kstar = W != 0ull && W == p_key ? 0 : -1;
+          } else {
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+              const unsigned long long kj = lane + 64 * j < a.K ? ((pg.g1[j] & 0xffffffffull) << 32) | (pg.g0[j] & 0xffffffffull)
+                                                                : 0ull;
+              const unsigned long long bm = __ballot(W != 0ull && kj == W);
+              if (bm && kstar < 0) kstar = 64 * j + (int)__builtin_ctzll(bm);
+            }
+          }
+          if (ok) commit(W, p_st0, p_st1, p_st2, p_st3);
+        }
+        // the pending step binds its winner (a Score error aborts the cycle, framework.go:650-656): post for
+        // the winner's slice
+        const bool bind = pend && W != 0ull && !(p_st0 > 1 && p_st1);
+        // 3. this step's A round totals
+        int gc, ge, gl, gh;
+        if (a.K > 1) {
+          ok = ok && collect_a(kstar, bind, &gc, &ge, &gl, &gh);
+        } else {
+          a_total(v, bind && kstar == 0, &gc, &ge, &gl, &gh);
+        }
         p_st0 = gc; p_st1 = ge; p_st2 = gl; p_st3 = gh;
         if (lane == 0) {
           sh.a_lo = gl;
@@ -1260,6 +1304,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       }
       __syncthreads();
       if (sh.stop) break;
+      mark(5);
       // 3. the slice's weighted totals w_pwr * NormalizeScore(PWR) + w_fgd * FGD (framework.go:686-704)
       {
         const int glo = sh.a_lo, ghi = sh.a_hi;
@@ -1592,10 +1637,11 @@ struct ksim_engine {
   unsigned* d_h_gsc = nullptr;
   unsigned* d_h_keys = nullptr;
   unsigned* d_h_l1 = nullptr;
+  unsigned* d_h_l2 = nullptr;  // k_hmemo: initial second maxima (HPlan::l2)
   int* d_h_cnt = nullptr;
   unsigned long long* d_h_prof = nullptr;
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
-  size_t h_cap[14] = {};
+  size_t h_cap[15] = {};
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
@@ -1873,6 +1919,7 @@ static const double* score_table() {
 struct HPlan {
   int Cmax = 1, Gmax = 1, Smax = 1, Npad = 0, nb = 0;
   int K = 1, S = 0, nbw = 0;      // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
+  bool l2 = false;                // the second maxima beside L1 (when they fit in LDS; KSIM_HL2=0: never)
   size_t lds = 0;
   std::vector<int> cg;            // [Rg][2] classes, groups
   std::vector<PodDev> cls, gpod;  // [Rg][Cmax] (sorted by group), [Rg][Gmax]
@@ -1956,7 +2003,11 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     }
     pl.Smax = std::max(pl.Smax, (int)sts[i].size());
   }
-  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw).total;
+  {
+    const char* v = std::getenv("KSIM_HL2");
+    pl.l2 = !(v && v[0] == '0') && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true).total <= 160 * 1024;
+  }
+  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, pl.l2).total;
   if (pl.lds > 160 * 1024) return false;
   pl.cg.assign((size_t)Rg * 2, 0);
   pl.cls.assign((size_t)Rg * pl.Cmax, PodDev{});
@@ -2013,6 +2064,7 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   if ((rc = ensure_buf(e->d_h_gsc, e->h_cap[8], (size_t)Rg * pl.Gmax * pl.Smax))) return rc;
   if ((rc = ensure_buf(e->d_h_keys, e->h_cap[9], (size_t)Rg * pl.Cmax * pl.Npad))) return rc;
   if ((rc = ensure_buf(e->d_h_l1, e->h_cap[10], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
+  if (pl.l2 && (rc = ensure_buf(e->d_h_l2, e->h_cap[14], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
   if ((rc = ensure_buf(e->d_h_cnt, e->h_cap[11], (size_t)Rg * pl.Cmax))) return rc;
   if (!e->d_th) {
     KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
@@ -2275,6 +2327,7 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
   ia.gsc = e->d_h_gsc;
   ia.keys = e->d_h_keys;
   ia.l1 = e->d_h_l1;
+  ia.l2 = pl.l2 ? e->d_h_l2 : nullptr;
   ia.cnt = e->d_h_cnt;
   ia.th = e->d_th;
   KSIM_HIP(hipMemsetAsync(e->d_h_cnt, 0, sizeof(int) * (size_t)Rg * pl.Cmax, st));
@@ -2309,6 +2362,7 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   ma.stride = stride;
   ma.keys = e->d_h_keys;
   ma.l1 = e->d_h_l1;
+  ma.l2 = pl.l2 ? e->d_h_l2 : nullptr;
   ma.cnt0 = e->d_h_cnt;
   ma.th = e->d_th;
   ma.prof = nullptr;
@@ -2589,7 +2643,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
-                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
+                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
                   e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
