@@ -2186,10 +2186,6 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     ma.skip = !(sk && sk[0] == '0');
   }
   ma.delay = hdelay_mask();
-  {
-    const char* v = std::getenv("KSIM_MEMO_TOP");
-    ma.keep_top = !(v && v[0] == '0');
-  }
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
   const bool tracing = pe && pe[0] == '2';

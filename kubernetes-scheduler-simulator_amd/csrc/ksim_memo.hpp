@@ -80,12 +80,10 @@ struct MemoArgs {
   const int* ev_cls;         // [launch replica][win_stride] class of each event, -1 delete
   unsigned* topg;            // [launch replica][win_stride][kTopWords] top granules, zeroed before launch
   int skip;                  // lean launches: the dead-class skip (KSIM_SKIP=0: off)
-  int keep_top;              // keep every class slot's top-2 up to date (KSIM_MEMO_TOP=0: scan every time)
   int delay;                 // KSIM_HDELAY (general instantiation only): 1 every wave before it takes the step's
                              // outcome, 2 wave 0 before its deferred Bind store, 4 the waves before the step start
 };
 constexpr int kTrace = 4;  // KSIM_PROFILE=2 trace words per workgroup and step
-constexpr unsigned kTopStale = 0xFFFFFFFFu;  // (keys are below 2^31)
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
                                  // 14 step-start loads, 15 owner's A, 16-20 owner's A split (wave 0)
 
@@ -110,9 +108,6 @@ struct __align__(16) MemoShared {
   unsigned wtop[kMWaves][2];
   unsigned wtop4[kMWaves][kTopN];  // decider mode: per-wave top keys of an upcoming event's class
   unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
-  // every owned class slot's top-2 keys kept up to date as its keys change (t2 kTopStale: unknown, t1
-  // kTopStale: nothing known), so that the next owner scans only when the second is unknown
-  unsigned t1s[kMaxCw], t2s[kMaxCw];
   int nitems;
   int crit_done;      // owner: critical F evaluations finished (waves 1-9 count up, wave 0 waits)
   int prk;            // the Bind wave 0 has yet to store into the cluster: rank (-1 none) and record
@@ -136,30 +131,6 @@ KSIM_HD int key32_rank(unsigned k) { return kMemoMaxRank - (int)((k >> 12) & 0xF
 KSIM_HD int key32_gpu(unsigned k) {
   const int gf = (int)((k >> 8) & 0xFu);
   return gf ? 15 - gf : -1;
-}
-
-// One class slot's kept top-2 (t1 > t2, keys of distinct nodes, or zeros) after node d's key changed to nk:
-// exact where the change decides it, else the unknown part goes stale (t1 stale = nothing known).
-__device__ __forceinline__ void top2_update(unsigned& t1, unsigned& t2, int d, unsigned nk) {
-  if (t1 == kTopStale) return;
-  const bool d1 = t1 != 0u && key32_rank(t1) == d;
-  if (t2 == kTopStale) {  // only the largest known
-    if (d1) t1 = nk >= t1 ? nk : kTopStale;
-    else if (nk > t1) { t2 = t1; t1 = nk; }
-    return;
-  }
-  const bool d2 = t2 != 0u && key32_rank(t2) == d;
-  if (d1) {
-    if (nk >= t2) t1 = nk;
-    else { t1 = t2; t2 = kTopStale; }
-  } else if (d2) {
-    if (nk > t1) { t2 = t1; t1 = nk; }
-    else if (nk >= t2) t2 = nk;
-    else t2 = kTopStale;
-  } else {
-    if (nk > t1) { t2 = t1; t1 = nk; }
-    else if (nk > t2) t2 = nk;
-  }
 }
 
 // Granule of step s: bit 0 written | bit 1 no feasible node | [23:8] rank + 1 (0: nothing bound) |
@@ -793,8 +764,6 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   const int* evo = a.ev_owner + (size_t)gi * a.win_stride;
   const bool is_w0 = w == 0;
   constexpr bool kSkip = !kDecider && !kGeneral;  // the dead-class skip (create-only streams)
-  // the kept top-2 per class slot (not in decider mode, whose owners publish top-4 lists instead)
-  const bool kTop = !kDecider && a.keep_top;
   const bool skip_ok = kSkip && a.skip && a.Cmax <= kMaxDeadWords * 32;
 
   // ---- start-up: the cluster in rank order, the owned classes, the typical table
@@ -815,7 +784,6 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   if (tid == 0) { sh.prk = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay[0] = sh.pay[1] = 0u; sh.crit_done = 0; }
   for (int i = tid; i < kMaxDeadWords; i += kMBlock) sh.dead[i] = 0u;
-  for (int i = tid; i < kMaxCw; i += kMBlock) { sh.t1s[i] = kTopStale; sh.t2s[i] = kTopStale; }
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
   const bool prof = kGeneral && a.prof != nullptr;
   unsigned long long* const trace = kGeneral ? a.trace : nullptr;
@@ -862,7 +830,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       a1 = lane < kMWaves ? sh.wtop[lane][0] : 0u;
       a2 = lane < kMWaves ? sh.wtop[lane][1] : 0u;
       wave_top2(a1, a2);
-      if (lane == 0) { sh.t2a = a1; sh.t2b = a2; sh.t1s[slot] = a1; sh.t2s[slot] = a2; }
+      if (lane == 0) { sh.t2a = a1; sh.t2b = a2; }
     }
   };
   const bool use_th = !kGeneral || a.th != nullptr;  // the lean instantiation is launched with a table
@@ -1179,12 +1147,6 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           const unsigned old = *kp;
           *kp = nk;
           sh.cnt[j] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
-          if (kTop) {
-            unsigned t1 = sh.t1s[j], t2 = sh.t2s[j];
-            top2_update(t1, t2, d, nk);
-            sh.t1s[j] = t1;
-            sh.t2s[j] = t2;
-          }
         }
       }
     }
@@ -1236,12 +1198,6 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         const unsigned old = *kp;
         *kp = nk;
         sh.cnt[lane] += (nk != 0u ? 1 : 0) - (old != 0u ? 1 : 0);
-        if (kTop) {
-          unsigned t1 = sh.t1s[lane], t2 = sh.t2s[lane];
-          top2_update(t1, t2, d, nk);
-          sh.t1s[lane] = t1;
-          sh.t2s[lane] = t2;
-        }
       }
       if (prof && lane == 0) sh.prof[13] += __builtin_amdgcn_s_memrealtime() - tl0;
     }
@@ -1259,13 +1215,8 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     } else if (step + 1 < rp.n_events) {
       const int ocn = __builtin_amdgcn_readfirstlane(sh.evo[eb + 1]);
       if (ocn >= 0 && (ocn >> 16) == w) {
-        __syncthreads();  // (the list wave's keys and kept top-2 of this step are in)
-        const int sl = ocn & 0xff;
-        if (kTop && (unsigned)__builtin_amdgcn_readfirstlane((int)sh.t2s[sl]) != kTopStale) {
-          if (tid == 0) { sh.t2a = sh.t1s[sl]; sh.t2b = sh.t2s[sl]; }  // (wave 0 reads them next step)
-        } else {
-          top2(sl);
-        }
+        __syncthreads();
+        top2(ocn & 0xff);
       }
     }
     mark(7);
