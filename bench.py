@@ -35,7 +35,7 @@ BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # dispatch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section) and its
 # VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/<round>/prof/<profile_key(args)>/pmc.json, the
 # newest round that profiled the configuration first.
-PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r03", "r02")]
+PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r04", "r03", "r02")]
 PROF_DIR = PROF_DIRS[0]
 # MI355X_MICROARCH.md, persistent-kernel price list: handoff-1to1 = one producer -> one consumer
 # granule hand-off between CUs, idle chip, 8 B: 0.8 us.  A pod step whose decision crosses CUs
@@ -440,6 +440,8 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+    elif os.environ.get("KSIM_DEVICE_RESET") == "1":
+        ksim.device_reset()  # world 1 holds no torch state: release the device before the exit handlers run
 
 
 def _sharded_engine(device, rank, world, trace, dist):

@@ -80,8 +80,9 @@ struct MemoArgs {
   const int* ev_cls;         // [launch replica][win_stride] class of each event, -1 delete
   unsigned* topg;            // [launch replica][win_stride][kTopWords] top granules, zeroed before launch
   int skip;                  // lean launches: the dead-class skip (KSIM_SKIP=0: off)
-  int delay;                 // KSIM_HDELAY (general instantiation only): 1 every wave before it takes the step's
-                             // outcome, 2 wave 0 before its deferred Bind store, 4 the waves before the step start
+  int delay;                 // KSIM_HDELAY (general and stress instantiations): 1 every wave before the end-of-step
+                             // barrier (wave 0 before it receives the step's granule), 2 the owner's critical waves
+                             // before their F, 4 every wave at the step start
 };
 constexpr int kTrace = 4;  // KSIM_PROFILE=2 trace words per workgroup and step
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
@@ -94,7 +95,9 @@ struct __align__(16) MemoShared {
   unsigned dead[kMaxDeadWords];  // lean launches: classes with no feasible node (create-only: for good)
   PodDev cls[kMaxCw];
   TypDev tp[kMaxTypical];
-  unsigned pad_[4];
+  NodeRec dnode;      // the record of the node the previous event changed (d)
+  unsigned dfirst;    // first_of_class(dnode, 0): GPUs holding the first occurrence of their milli-left value
+  unsigned pad_dfirst[3];
   double th[104];     // FGD score steps (build_score_thresholds), th[0] = -inf, th[101] = +inf
   unsigned long long grp[kMaxCw];
   int cls_id[kMaxCw];
@@ -110,10 +113,9 @@ struct __align__(16) MemoShared {
   unsigned t2a, t2b;  // top-2 keys of the next create event's class (its owner only)
   int nitems;
   int crit_done;      // owner: critical F evaluations finished (waves 1-9 count up, wave 0 waits)
-  int prk;            // the Bind wave 0 has yet to store into the cluster: rank (-1 none) and record
+  int dirty;          // node (rank) changed by the previous event, -1 none
   int stop;
-  unsigned pay[2];    // the owner's granule of step s, in [s & 1] (a late wave may still read step s - 1's)
-  NodeRec pnode;
+  unsigned pay;       // this step's granule (its owner)
   unsigned long long prof[kProfPhases];
 };
 static_assert(sizeof(MemoShared) % 16 == 0, "keep the node records 16-B aligned");
@@ -341,9 +343,10 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
 }
 
 // KSIM_HDELAY stress delays at the hand-over points of a step (the memoised kernels' general
-// instantiations only): a wave about to read something another wave of the same step may be writing sleeps
-// 0-3 x ~3.4 us on about half the steps (a hash of step, wave and workgroup), so the late-reader orders that
-// are rare on an idle chip happen thousands of times per run.  The bits name the points (k_hmemo, k_memo).
+// instantiations and k_memo's stress instantiation only): a wave about to read something another wave of
+// the same step may be writing sleeps 0-3 x ~3.4 us on about half the steps (a hash of step, wave and
+// workgroup), so the late-reader orders that are rare on an idle chip happen thousands of times per run.
+// The bits name the points (k_hmemo, k_memo).
 __device__ __forceinline__ void hdelay(int mask, int bit, int step, int wave, int wg) {
   if (!(mask & bit)) return;
   unsigned h = (unsigned)step * 0x9E3779B1u ^ (unsigned)(wave * 0x85EBCA77) ^ (unsigned)(wg * 0xC2B2AE3D) ^ (unsigned)bit;
@@ -782,7 +785,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   }
   for (int i = tid; i < rp.nt * 2; i += kMBlock)
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
-  if (tid == 0) { sh.prk = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay[0] = sh.pay[1] = 0u; sh.crit_done = 0; }
+  if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; sh.crit_done = 0; }
   for (int i = tid; i < kMaxDeadWords; i += kMBlock) sh.dead[i] = 0u;
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
   const bool prof = kGeneral && a.prof != nullptr;
@@ -904,38 +907,17 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   bool r_feas = false, r_need = false, r_skip = false;
   int r_base = 0, r_ni = 0;
 
-  // Carried from step to step in every wave's registers (no end-of-step barrier: each wave takes a step's
-  // outcome from its granule itself): the node the last decided event changed (-1 none), its record and
-  // first-occurrence GPU mask, and the class the last decided event found dead (-1 none; wave 0 folds it
-  // into sh.dead, which the other waves may read before or after the fold)
-  int d_c = -1, pdc = -1;
-  NodeV dn_c{};
-  unsigned df_c = 0u;
-  // wave 0: the Bind the other waves may still be reading the record before, stored after the next barrier
-  auto flush_bind = [&]() {
-    if constexpr (kDelays)
-      if (wv == 0) hdelay(a.delay, 2, sh.prk, wv, (int)blockIdx.x);
-    if (wv == 0 && lane == 0) {
-      const int pk = sh.prk;
-      if (pk >= 0) store_node(&s_nodes[pk], load_node(&sh.pnode));
-      sh.prk = -1;
-    }
-  };
   const bool decider = kDecider && w == 0;
   if constexpr (kDecider)
     if (decider) memo_decider(a, rp, sh, s_nodes, *reinterpret_cast<DeciderScratch*>(s_keys), s_fold, s_last, gi, tid);
   for (int step = 0; step < (decider ? 0 : rp.n_events); ++step) {
     const int eb = step & (kEvBuf - 1);
     if (eb == 0) {
-      // (no end-of-step barrier: a late wave may still be reading the last window's owner codes)
-      if (step > 0) __syncthreads();
       const int ne = min(kEvBuf, rp.n_events - step);
       const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
       for (int i = tid; i < ne * 2; i += kMBlock) reinterpret_cast<uint4*>(sh.ev)[i] = gget(src + i);
       for (int i = tid; i <= ne + kLag; i += kMBlock) sh.evo[i] = step + i < rp.n_events ? gget(evo + step + i) : -1;
       __syncthreads();
-      flush_bind();
-      if (sh.stop) break;
     }
     // Dead-class skip (lean launches, create-only streams): Filter is monotone in a node's resources and a
     // creation only takes resources, so once an event found no feasible node (its granule says so), every
@@ -945,7 +927,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     // still precomputes its top-2 (with the dirty node excluded there, as on any step).
     if constexpr (kSkip) {
       const int cls = __builtin_amdgcn_readfirstlane(sh.ev[eb].pad);  // the event's class (load_events)
-      if (skip_ok && (cls == pdc || ((sh.dead[cls >> 5] >> (cls & 31)) & 1u))) {
+      if (skip_ok && ((sh.dead[cls >> 5] >> (cls & 31)) & 1u)) {
         // the whole run of dead events up to the next live one (or the window's end) at once: the dead
         // set cannot change inside the run; every wave finds the same run
         const int wend = min(kEvBuf, rp.n_events - (step - eb));
@@ -953,7 +935,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         for (int j0 = eb + 1; j0 < wend; j0 += 64) {
           const int j = j0 + lane;
           const int c = j < wend ? sh.ev[j].pad : 0;
-          const unsigned long long lb = __ballot(j < wend && c != pdc && !((sh.dead[c >> 5] >> (c & 31)) & 1u));
+          const unsigned long long lb = __ballot(j < wend && !((sh.dead[c >> 5] >> (c & 31)) & 1u));
           if (lb) {
             run = j0 + (int)__builtin_ctzll(lb) - eb;
             break;
@@ -969,21 +951,19 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           }
         }
         __syncthreads();
-        flush_bind();
-        if (sh.stop) break;
         step += run - 1;
         continue;
       }
     }
     if (trace && tid == 0 && step < a.trace_steps)
-      trace[((size_t)blockIdx.x * a.trace_steps + step) * 4] = __builtin_amdgcn_s_memrealtime();
+      trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace] = __builtin_amdgcn_s_memrealtime();
     if constexpr (kDelays) hdelay(a.delay, 4, step, wv, (int)blockIdx.x);
-    // the event and its owner code (one LDS round trip); d, its record and mask from registers
+    // one LDS round trip: the event, its owner code, d and d's record
     const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
     const int oc = __builtin_amdgcn_readfirstlane(sh.evo[eb]);
-    const int d = d_c;
-    const NodeV dn = dn_c;
-    const unsigned dfirst = df_c;
+    const int d = __builtin_amdgcn_readfirstlane(sh.dirty);
+    const NodeV dn = ksim_replay::uniform_node(&sh.dnode);
+    const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst);
     const bool del = kGeneral && (p.flags & kPodDelete) != 0u;  // lean: launched on create-only streams
     const bool own = !kDecider && oc >= 0 && (oc >> 16) == w;  // decider mode: workgroup 0 decides
     const int oslot = own ? (oc & 0xff) : -1;
@@ -994,6 +974,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     // ---- A: the step's own class on d (owner, waves 0-8) | the list of d's other requests (list wave)
     if (d >= 0) {
       if (own && wv >= 1 && wv <= kCritWaves) {
+        if constexpr (kDelays) hdelay(a.delay, 2, step, wv, (int)blockIdx.x);
         // wave 1 + c evaluates candidate c of d for the step's class: 0 = d's current state,
         // 1..8 = the share pod on GPU c-1 (first GPU of its milli-left value), 1 = the Sub state
         // otherwise.  Nine waves over four SIMDs; wave 0 is left to the owner's bookkeeping.
@@ -1092,7 +1073,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           sh.crit_done = 0;
           if (prof) sh.prof[17] += __builtin_amdgcn_s_memrealtime() - t_loaded;
           if (trace && step < a.trace_steps)
-            trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+            trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace + 3] = __builtin_amdgcn_s_memrealtime();
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -1107,7 +1088,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         fresh = ofeas ? gk_crit : 0u;
         if (prof && tid == 0) sh.prof[18] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (trace && lane == 0 && step < a.trace_steps)
-          trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace + 2] = __builtin_amdgcn_s_memrealtime();
       }
       const unsigned W = fresh > ex ? fresh : ex;
       const int rk = W != 0u ? key32_rank(W) : -1;
@@ -1121,7 +1102,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
         asm volatile("" ::: "memory");
         if (prof) sh.prof[20] += __builtin_amdgcn_s_memrealtime() - t_loaded;
         if (trace && step < a.trace_steps)
-          trace[((size_t)blockIdx.x * a.trace_steps + step) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace + 1] = __builtin_amdgcn_s_memrealtime();
         const int nfeas = cnt_o + (d >= 0 ? (fresh != 0u ? 1 : 0) - (old_own != 0u ? 1 : 0) : 0);
         ResultDev out{-1, 0, 0, nfeas, ST_UNSCHED};
         if (W != 0u) {
@@ -1135,7 +1116,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           }
         }
         gput(rp.res + step, out);
-        sh.pay[step & 1] = pay;
+        sh.pay = pay;
         if (prof) sh.prof[19] += __builtin_amdgcn_s_memrealtime() - t_loaded;
       }
       if (d >= 0) {  // every class of the step's score group on d (its own included)
@@ -1153,8 +1134,6 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
     if (prof && tid == 0 && own) sh.prof[15] += __builtin_amdgcn_s_memrealtime() - t_loaded;  // owner's A
     mark(1);
     __syncthreads();
-    flush_bind();  // every wave has taken the last outcome: the Bind reaches the cluster
-    if (sh.stop) break;
     mark(2);
     mark(3);
     if (d >= 0) {
@@ -1220,70 +1199,83 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       }
     }
     mark(7);
-    // ---- this step's outcome, taken by EVERY wave from the granule (no end-of-step barrier): the changed
-    // node's record after the Bind (or the delete) in registers -- the next step's d -- its first-occurrence
-    // mask, the class found dead.  The record before the Bind is read from the cluster, so wave 0 stores the
-    // Bind after the next barrier, once every wave has read it (flush_bind).
     if constexpr (kDelays) hdelay(a.delay, 1, step, wv, (int)blockIdx.x);
-    {
-      unsigned pay = 0u;
-      int okr = 1;
+    // ---- this step's outcome on every workgroup: the Bind (or the delete) on the LDS cluster
+    if (wv == 0) {
+      int nd_w = -1;
+      NodeV nn{};
       if (lane == 0) {
-        if (del) {
-          if (p.ref >= 0 && p.ref < step) pay = gload32(win + p.ref);  // written before this wave passed step p.ref
-        } else if (own) {
-          pay = sh.pay[step & 1];
-        } else {
-          unsigned spins = 0;
-          while ((pay = gload32(win + step)) == 0u) {
-            if (++spins > kSpinLimit) { okr = 0; break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          if (trace && wv == 0 && step < a.trace_steps)
-            trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace + 1] = __builtin_amdgcn_s_memrealtime();
+      unsigned pay = 0u;
+      int sign = +1;
+      PodDev bp = p;
+      bool ok = true;
+      if (del) {
+        sign = -1;
+        if (p.ref >= 0 && p.ref < step) {
+          pay = gload32(win + p.ref);  // written before this workgroup passed step p.ref
+          bp = gget(rp.ev + p.ref);
         }
+      } else if (own) {
+        pay = sh.pay;
+      } else {
+        unsigned spins = 0;
+        while ((pay = gload32(win + step)) == 0u) {
+          if (++spins > kSpinLimit) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (trace && step < a.trace_steps)
+          trace[((size_t)blockIdx.x * a.trace_steps + step) * kTrace + 1] = __builtin_amdgcn_s_memrealtime();
       }
-      pay = (unsigned)__builtin_amdgcn_readfirstlane((int)pay);
-      okr = __builtin_amdgcn_readfirstlane(okr);
-      const int rk = okr ? (int)((pay >> 8) & 0xffffu) - 1 : -1;
-      const int mask = (int)(pay >> 24);
-      // this event's class has no feasible node, for good (lean: create-only streams)
-      pdc = (kSkip && skip_ok && okr && (pay & 2u)) ? (int)p.pad : -1;
-      if (rk >= 0) {
-        const PodDev bp = del ? ksim_replay::uniform_pod(rp.ev + p.ref) : p;
-        NodeV n = ksim_replay::uniform_node(&s_nodes[rk]);
-        bind_node(n, bp, mask, del ? -1 : +1);
-        dn_c = n;
-        df_c = first_mask_lanes(n, lane);
-      }
-      d_c = rk;
-      if (!okr && lane == 0) {  // (any wave: every wave breaks after the next barrier)
+      int nd = -1;
+      if (kSkip && skip_ok && ok && (pay & 2u))  // this event's class has no feasible node, for good
+        sh.dead[p.pad >> 5] |= 1u << (p.pad & 31);
+      if (!ok) {
         sh.stop = 1;
         atomicOr(a.fail, 1);
-      }
-      if (wv == 0 && lane == 0) {
-        if (pdc >= 0) sh.dead[pdc >> 5] |= 1u << (pdc & 31);
+      } else {
+        const int rk = (int)((pay >> 8) & 0xffffu) - 1;
+        const int mask = (int)(pay >> 24);
         if (rk >= 0) {
-          store_node(&sh.pnode, dn_c);
-          sh.prk = rk;
+          NodeV n = load_node(&s_nodes[rk]);
+          bind_node(n, bp, mask, sign);
+          store_node(&s_nodes[rk], n);
+          store_node(&sh.dnode, n);
+          nn = n;
           // (results carry name ranks and the affinity tags are applied by k_memo_finish: nothing
           // here waits on global memory)
           if (del && is_w0) gput(rp.res + step, ResultDev{rk, mask, 0, 0, ST_DELETED});
           if (kGeneral && rp.snap && (del ? is_w0 : own)) {  // cluster report: the state this event left
-            gput_node(rp.snap + step, dn_c);
+            gput_node(rp.snap + step, n);
             gput(rp.prev + step, s_last[rk]);
           }
           s_last[rk] = step;
+          nd = rk;
         } else if (del && is_w0) {
           gput(rp.res + step, ResultDev{-1, 0, 0, 0, ST_DELETED});
         }
       }
+      sh.dirty = nd;
+      nd_w = nd;
+      }  // lane 0
+      // the first-occurrence GPU mask of the changed node, for the next step's candidate lists
+      nd_w = __builtin_amdgcn_readfirstlane(nd_w);
+      if (nd_w >= 0) {
+        NodeV u;
+        u.cpu_left = __builtin_amdgcn_readfirstlane(nn.cpu_left);
+        u.mem_left = __builtin_amdgcn_readfirstlane(nn.mem_left);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) u.g[i] = __builtin_amdgcn_readfirstlane(nn.g[i]);
+        u.meta = __builtin_amdgcn_readfirstlane(nn.meta);
+        u.name_rank = __builtin_amdgcn_readfirstlane(nn.name_rank);
+        const unsigned fmk = first_mask_lanes(u, lane);
+        if (lane == 0) sh.dfirst = fmk;
+      }
     }
     mark(8);
+    __syncthreads();
     mark(9);
+    if (sh.stop) break;
   }
-  __syncthreads();
-  flush_bind();
   if (prof && tid == 0) {
     sh.prof[10] = __builtin_amdgcn_s_memtime() - c_start;
     sh.prof[11] = __builtin_amdgcn_s_memrealtime() - t_start;

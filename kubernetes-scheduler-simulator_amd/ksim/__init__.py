@@ -250,6 +250,16 @@ def hip_runtimes():
     return {k: sorted(v) for k, v in out.items()}
 
 
+def device_reset():
+    """hipDeviceReset on the process's HIP runtime: every queue, stream and allocation of the device released
+    now rather than by the runtime's exit handlers (bench.py before it exits, KSIM_DEVICE_RESET=1; DESIGN.md
+    §3 on the profiler's exit-time fault).  Only for a process that holds no other device state (no torch)."""
+    rt = hip_runtimes()["hip"]
+    if rt:
+        return C.CDLL(rt[0]).hipDeviceReset()
+    return None
+
+
 def lib():
     global _LIB
     if _LIB is None:

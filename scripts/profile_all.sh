@@ -9,7 +9,6 @@ for name in "$@"; do
     c2) a="";;
     c2-rm5) a="--run-mode 5";;
     c2-rm2) a="--run-mode 2";;
-    c2-rm6) a="--run-mode 6";;
     c2-BestFit) a="--policy BestFit";;
     c2-PWR) a="--policy PWR";;
     c2-PWR_500_FGD_500) a="--policy PWR_500_FGD_500";;

@@ -19,6 +19,7 @@ one() {  # tag bench-args-string env...
 for i in 1 2 3; do
   one c2_r03_$i "--steps 10 --warmup 2" $R03
   one c2_r04_$i "--steps 10 --warmup 2"
+  one c2_notop_$i "--steps 10 --warmup 2" KSIM_MEMO_TOP=0
 done
 for i in 1 2; do
   one pf_r03_$i "--steps 5 --warmup 1 --policy PWR_500_FGD_500" $R03
@@ -32,3 +33,7 @@ done
 KSIM_PROFILE=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/prof_memo.log 2>&1; grep "memo profile" $O/prof_memo.log
 KSIM_PROFILE=1 timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --run-mode 5 > $O/prof_rm5.log 2>&1; grep "hmemo profile" $O/prof_rm5.log
 timeout -k 10 300 python -u scripts/c4_fgd_traces.py > $O/c4_traces.log 2>&1; tail -17 $O/c4_traces.log
+# ONE cooperative-launch counter pass of the torch-free world-1 bench (round-3 verdict item 2), maps saved
+KSIM_MAPS_OUT=$O/maps.txt timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_coop.log 2>&1
+echo "pmc coop rc=$?"
+grep -A22 Aborted $O/pmc_coop.log | head -24

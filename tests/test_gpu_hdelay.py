@@ -1,10 +1,9 @@
 """Hand-over stress for the memoised FGD kernels (KSIM_HDELAY, round-3 verdict item 1).
 
-k_memo (since r04) has no end-of-step barrier either: every wave takes a step's outcome from the granule
-into its registers, the class found dead rides in a register until wave 0's fold is behind a barrier, and
-wave 0 stores the Bind into the cluster only after the next barrier (every wave has read the record before
-it).  Its delay points: 1 every wave before it takes the outcome, 2 wave 0 before the deferred Bind store,
-4 every wave before the step start; the lean kernel with them compiled in runs the dead-class skip too.
+k_memo hands its critical F over through an LDS counter (the owner's waves 1-9 to wave 0) and otherwise
+joins on barriers; its delay points: 1 every wave before the end-of-step barrier (wave 0 before it receives
+the granule), 2 the owner's critical waves before their F, 4 every wave at the step start.  The lean kernel
+with them compiled in (KSIM_HDELAY selects it) runs the dead-class skip too.
 
 k_hmemo has no workgroup barrier inside a step: wave 0 (the event's own class, the decision, the Bind) and
 waves 1-15 (every other class's refresh) hand work over through LDS counters and double-buffered state,
