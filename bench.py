@@ -93,6 +93,7 @@ def profile_rooflines(args, kernel):
 
 def cpu_baseline(trace, seed, threads):
     """Oracle ("port") on the host: one full seed replay (~11k events), FGD, `threads` workers."""
+    os.environ["KSIM_ORACLE_CACHE"] = "0"  # every timed replay runs (pyoracle memoises replays for the tests)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import helpers
@@ -120,6 +121,7 @@ def cpu_baseline(trace, seed, threads):
 
 def _c2_worker(seed):
     """One C2 replica on the oracle, single-threaded, replayed to completion (cpu_baseline_replicas)."""
+    os.environ["KSIM_ORACLE_CACHE"] = "0"
     sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
     import helpers
     import pyoracle as O
@@ -158,6 +160,7 @@ ORACLE_POLICY = {"01-Random": ("POL_RANDOM", "SEL_RANDOM"), "02-DotProd": ("POL_
 
 def _c4_worker(job):
     """One paper-sweep experiment on the oracle, single-threaded, over its first `prefix` events."""
+    os.environ["KSIM_ORACLE_CACHE"] = "0"
     sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
     import helpers
     import pyoracle as O

@@ -293,11 +293,34 @@ def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_w
              out[i].res.gpu_type.decode(), out[i].percentage) for i in range(k)]
 
 
+# Replays already made in this process (the GPU suite checks several kernels against the same reference
+# replay: a full openb trace takes the oracle seconds), keyed by a digest of every input that decides the
+# result; the worker-thread count does not.  KSIM_ORACLE_CACHE=0 turns it off.
+_RUN_CACHE = {}
+
+
 def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
                with_report=False, w_pwr=0, w_fgd=0, dim_ext=DIM_MERGE, norm=NORM_MAX, go_stream=None):
     """nodes: list of dicts {name,cpu,mem,pods,gpu,model}; events: list of dicts
     {cpu, cpu_nz, mem, milli, num, type, delete, ref}; typical_list: [(cpu,milli,num,type,freq)]
     go_stream: a GoRng (or (vec, tap, feed)) = the Random draw structure on Go's stream from that state"""
+    import copy
+    import hashlib
+    key = None
+    if go_stream is None and os.environ.get("KSIM_ORACLE_CACHE", "1") != "0":
+        key = hashlib.sha256(repr((nodes, typical_list, events, policy, gpu_sel, seed, with_report, w_pwr, w_fgd,
+                                   dim_ext, norm)).encode()).hexdigest()
+        if key in _RUN_CACHE:
+            return copy.deepcopy(_RUN_CACHE[key])
+    out = _run_events(nodes, typical_list, events, policy, gpu_sel, seed, threads, with_report, w_pwr, w_fgd,
+                      dim_ext, norm, go_stream)
+    if key is not None:
+        _RUN_CACHE[key] = copy.deepcopy(out)
+    return out
+
+
+def _run_events(nodes, typical_list, events, policy, gpu_sel, seed, threads, with_report, w_pwr, w_fgd, dim_ext,
+                norm, go_stream):
     nn = len(nodes)
     ns = (NodeSpec * nn)()
     for i, d in enumerate(nodes):

@@ -9,7 +9,8 @@
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-# plain launches of the same grids (rocprofv3 faults at exit after a cooperative launch; the grid size
+# plain launches of the same grids (rocprofv3 7.2 faults in the HIP runtime's exit handlers after a cooperative
+# launch, one runtime in the process or two: DESIGN.md §3; the grid size
 # is still bounded by the occupancy cap, and the kernels are the same)
 export KSIM_COOP=0
 NAME=$1; shift
