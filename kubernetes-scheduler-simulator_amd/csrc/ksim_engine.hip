@@ -2377,7 +2377,7 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   {  // KSIM_HPF (one workgroup per replica): 1 = wave 0 lists the next refresh (the default since r04: C4 190.7 ->
      // 178-185 ms, C2 run_mode 5 50.3 -> 47.7 ms, profiles/r04/memo/ab_runs.txt), 2 = touches its flagged rows, 0 = off
     const char* pf = std::getenv("KSIM_HPF");
-    ma.pf = pf ? std::atoi(pf) & 3 : 1;
+    ma.pf = pf ? std::atoi(pf) & 7 : 1;  // (4: the wide form lists on wave 0 too)
   }
   ma.delay = hdelay_mask();
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;

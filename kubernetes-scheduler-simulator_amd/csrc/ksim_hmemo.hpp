@@ -343,7 +343,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int bar_target = 0;  // the bulk barrier's count so far (waves 1-15)
   int cbar_target = 0; // the class waves' barrier count so far
   int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..kFW)
-  const bool w0list = kSub == 0 && (a.pf & 1) != 0;  // wave 0 lists the next refresh's F evaluations
+  // wave 0 lists the next refresh's F evaluations (one workgroup per replica; the wide form too with bit 4)
+  const bool w0list = (kSub == 0 || (a.pf & 4) != 0) && (a.pf & 1) != 0;
   const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
   // A bounded wait on one of the bulk's LDS counters (lane 0 of a wave): past the limit the workgroup
   // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over) instead of hanging.

@@ -1060,15 +1060,21 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
       const int mask_d_pre = d >= 0 && !d_gpu_from_key ? select_gpus(dn, p, rp.gpusel, -1, rp.seed, step) : -1;
       if (prof && tid == 0) sh.prof[16] += __builtin_amdgcn_s_memrealtime() - t_loaded;
       if (d >= 0) {
-        if (lane == 0) {  // wait for waves 1-9 (LDS counter; every one of them arrives; bounded)
-          unsigned spins = 0;
-          while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kCritWaves) {
-            if (++spins > 4 * kSpinLimit) {
-              sh.stop = 1;
-              atomicOr(a.fail, 32);  // (bit 2 is PWR's key-field overflow)
-              break;
+        if (lane == 0) {  // wait for waves 1-9 (LDS counter; every one of them arrives after its own F, nothing
+                          // else: the lean kernel's wait is r03's tight loop, the delayed ones are bounded)
+          if constexpr (kDelays) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kCritWaves) {
+              if (++spins > 4 * kSpinLimit) {
+                sh.stop = 1;
+                atomicOr(a.fail, 32);  // (bit 2 is PWR's key-field overflow)
+                break;
+              }
+              __builtin_amdgcn_s_sleep(0);
             }
-            __builtin_amdgcn_s_sleep(0);
+          } else {
+            while (__hip_atomic_load(&sh.crit_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kCritWaves)
+              __builtin_amdgcn_s_sleep(0);
           }
           sh.crit_done = 0;
           if (prof) sh.prof[17] += __builtin_amdgcn_s_memrealtime() - t_loaded;

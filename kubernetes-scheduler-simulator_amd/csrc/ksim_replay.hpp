@@ -258,6 +258,11 @@ __device__ __forceinline__ double qbc_d(double v) {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
+// 1.0 or +0.0 from a flag: the high word selected, the low word a constant 0 (one v_cndmask)
+__device__ __forceinline__ double sel01(bool f) {
+  return __builtin_bit_cast(double, (unsigned long long)(f ? 0x3FF00000u : 0u) << 32);
+}
+
 // Candidate state of `code` on node m: 0 current, 1..8 share pod on GPU code-1
 // (fgd_score.go:111-118), 9 NodeResource.Sub (fgd_score.go:137-141, resource.go:454-480).
 // g: packed u16 milli-left per GPU; *total: GetGpuMilliLeftTotal of the state.
@@ -315,10 +320,10 @@ __device__ __forceinline__ double frag_F_quad(int cpuL, const uint32_t (&g)[4], 
     code = tb + q < ncpu ? code : 4;
     int cj;
     double vj;
-    cj = qbc<0>(code); vj = qbc_d<0>(x); bc += (cj == q) ? vj : 0.0;
-    cj = qbc<1>(code); vj = qbc_d<1>(x); bc += (cj == q) ? vj : 0.0;
-    cj = qbc<2>(code); vj = qbc_d<2>(x); bc += (cj == q) ? vj : 0.0;
-    cj = qbc<3>(code); vj = qbc_d<3>(x); bc += (cj == q) ? vj : 0.0;
+    cj = qbc<0>(code); vj = qbc_d<0>(x); bc = __builtin_fma(vj, sel01(cj == q), bc);
+    cj = qbc<1>(code); vj = qbc_d<1>(x); bc = __builtin_fma(vj, sel01(cj == q), bc);
+    cj = qbc<2>(code); vj = qbc_d<2>(x); bc = __builtin_fma(vj, sel01(cj == q), bc);
+    cj = qbc<3>(code); vj = qbc_d<3>(x); bc = __builtin_fma(vj, sel01(cj == q), bc);
   }
   double bg = 0.0;
   // two rounds per iteration: both rounds' table entries are loaded before the first is classified
@@ -346,12 +351,15 @@ __device__ __forceinline__ double frag_F_quad(int cpuL, const uint32_t (&g)[4], 
       int code = acc ? (cpu_ok ? 1 : (gpu_ok ? 2 : 0)) : 3;
       code = tb + q < nt ? code : 4;
       const double v = (acc && cpu_ok && gpu_ok) ? y : x;
+      // bin q += (cj == q) ? vj : 0.0 as one fma with a 0 / 1 selector: vj * 1.0 and vj * 0.0 = +0.0 are exact
+      // (vj finite, >= 0), so fma(vj, sel, bin) rounds exactly as the add does, with one instruction less per
+      // typical pod than selecting both halves of vj (the fold's issue count bounds the large tables)
       double vj;
       int cj;
-      cj = qbc<0>(code); vj = qbc_d<0>(v); bg += (cj == q) ? vj : 0.0;
-      cj = qbc<1>(code); vj = qbc_d<1>(v); bg += (cj == q) ? vj : 0.0;
-      cj = qbc<2>(code); vj = qbc_d<2>(v); bg += (cj == q) ? vj : 0.0;
-      cj = qbc<3>(code); vj = qbc_d<3>(v); bg += (cj == q) ? vj : 0.0;
+      cj = qbc<0>(code); vj = qbc_d<0>(v); bg = __builtin_fma(vj, sel01(cj == q), bg);
+      cj = qbc<1>(code); vj = qbc_d<1>(v); bg = __builtin_fma(vj, sel01(cj == q), bg);
+      cj = qbc<2>(code); vj = qbc_d<2>(v); bg = __builtin_fma(vj, sel01(cj == q), bg);
+      cj = qbc<3>(code); vj = qbc_d<3>(v); bg = __builtin_fma(vj, sel01(cj == q), bg);
     }
   }
   const double b0 = qbc_d<0>(bg), b1 = qbc_d<1>(bg), b3 = qbc_d<2>(bg), b6 = qbc_d<3>(bg);

@@ -89,9 +89,12 @@ def test_hmemo_c2_seed_vs_oracle_with_delays(default_trace, monkeypatch):
     assert got == want
 
 
-def test_hmemo_wide_delays(default_trace, c2_replay, monkeypatch):
-    # the wide form (K = 7 co-resident workgroups per replica, the granule exchange per pod) on four C2 seeds
+@pytest.mark.parametrize("hpf", ["1", "5"])
+def test_hmemo_wide_delays(default_trace, c2_replay, monkeypatch, hpf):
+    # the wide form (K = 7 co-resident workgroups per replica, the granule exchange per pod) on four C2 seeds;
+    # KSIM_HPF=5: the workgroup that binds lists the next refresh on its wave 0 (bit 4: the wide form too)
     monkeypatch.setenv("KSIM_HDELAY", ALL)
+    monkeypatch.setenv("KSIM_HPF", hpf)
     eng = c2_engine(default_trace, SEEDS[:4], 5, wgs=7)
     try:
         eng.run()
