@@ -1637,10 +1637,11 @@ struct ksim_engine {
   unsigned* d_h_gsc = nullptr;
   unsigned* d_h_keys = nullptr;
   unsigned* d_h_l1 = nullptr;
+  unsigned* d_h_l2 = nullptr;  // k_hmemo: initial second maxima (HPlan::l2)
   int* d_h_cnt = nullptr;
   unsigned long long* d_h_prof = nullptr;
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
-  size_t h_cap[14] = {};
+  size_t h_cap[15] = {};
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
@@ -1918,6 +1919,7 @@ static const double* score_table() {
 struct HPlan {
   int Cmax = 1, Gmax = 1, Smax = 1, Npad = 0, nb = 0;
   int K = 1, S = 0, nbw = 0;      // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
+  bool l2 = false;                // the second maxima beside L1 (the wide form, when they fit in LDS; KSIM_HL2)
   size_t lds = 0;
   std::vector<int> cg;            // [Rg][2] classes, groups
   std::vector<PodDev> cls, gpod;  // [Rg][Cmax] (sorted by group), [Rg][Gmax]
@@ -2001,7 +2003,16 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     }
     pl.Smax = std::max(pl.Smax, (int)sts[i].size());
   }
-  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw).total;
+  {
+    // L2 spares the flagged blocks' key reloads.  They bound the wide form's class waves (C5: 100k nodes, the
+    // keys far beyond L2, 55 flagged rows per refresh from HBM), while one workgroup over an openb cluster
+    // keeps its keys in L2 and is bound by F: there L2 only adds update work (profiles/r04/hmemo/).
+    // KSIM_HL2=0 never, =1 also for one workgroup per replica.
+    const char* v = std::getenv("KSIM_HL2");
+    const bool want = v ? v[0] == '1' : pl.K > 1;
+    pl.l2 = want && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true).total <= 160 * 1024;
+  }
+  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, pl.l2).total;
   if (pl.lds > 160 * 1024) return false;
   pl.cg.assign((size_t)Rg * 2, 0);
   pl.cls.assign((size_t)Rg * pl.Cmax, PodDev{});
@@ -2058,6 +2069,7 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   if ((rc = ensure_buf(e->d_h_gsc, e->h_cap[8], (size_t)Rg * pl.Gmax * pl.Smax))) return rc;
   if ((rc = ensure_buf(e->d_h_keys, e->h_cap[9], (size_t)Rg * pl.Cmax * pl.Npad))) return rc;
   if ((rc = ensure_buf(e->d_h_l1, e->h_cap[10], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
+  if (pl.l2 && (rc = ensure_buf(e->d_h_l2, e->h_cap[14], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
   if ((rc = ensure_buf(e->d_h_cnt, e->h_cap[11], (size_t)Rg * pl.Cmax))) return rc;
   if (!e->d_th) {
     KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
@@ -2320,6 +2332,7 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
   ia.gsc = e->d_h_gsc;
   ia.keys = e->d_h_keys;
   ia.l1 = e->d_h_l1;
+  ia.l2 = pl.l2 ? e->d_h_l2 : nullptr;
   ia.cnt = e->d_h_cnt;
   ia.th = e->d_th;
   KSIM_HIP(hipMemsetAsync(e->d_h_cnt, 0, sizeof(int) * (size_t)Rg * pl.Cmax, st));
@@ -2354,6 +2367,7 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   ma.stride = stride;
   ma.keys = e->d_h_keys;
   ma.l1 = e->d_h_l1;
+  ma.l2 = pl.l2 ? e->d_h_l2 : nullptr;
   ma.cnt0 = e->d_h_cnt;
   ma.th = e->d_th;
   ma.prof = nullptr;
@@ -2635,7 +2649,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
-                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_cnt, e->d_h_prof,
+                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
                   e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {

@@ -87,6 +87,7 @@ struct HMemoArgs {
   int stride;
   unsigned* keys;           // [Rg][Cmax][Npad]
   const unsigned* l1;       // [Rg][Cmax][nb] initial L1 (k_hinit_keys)
+  const unsigned* l2;       // [Rg][Cmax][nb] initial second maxima, or null: no L2 (it does not fit in LDS)
   const int* cnt0;          // [Rg][Cmax] initial feasible counts
   const double* th;         // [102] FGD score steps
   unsigned long long* prof; // optional [Rg * K][kHProf] (KSIM_PROFILE=1)
@@ -134,7 +135,8 @@ struct __align__(16) HShared {
   // while slower waves may still be reading this step's skip condition, so it writes [cur ^ 1] and folds
   // [cur] into `dead`; every reader checks dead | pdead[cur] (the same answer before and after the fold).
   int pdead[2];
-  int pad_[3];
+  int f0seq;           // refreshes whose item 0 (d's current state) has its F in s_F[0] (the item keys' reference)
+  int pad_[2];
   unsigned long long prof[kHProf];
   unsigned dead[32];   // class slots with no feasible node (create-only streams: for good)
 };
@@ -142,20 +144,22 @@ static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned"
 
 // Dynamic LDS after HShared (16-B aligned regions).
 struct HLayout {
-  size_t cls, gpod, F, l1, nodes, last, cnt, bx, cgrp, flist, code, igrp, fnew, fold, gbase, total;
+  size_t cls, gpod, F, l1, l2, nodes, last, cnt, bx, bx2, cgrp, flist, code, igrp, fnew, fold, gbase, gkey, total;
 };
 KSIM_HD size_t halign(size_t x) { return (x + 15) & ~(size_t)15; }
-KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
+KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2) {
   HLayout L;
   size_t o = sizeof(HShared);
   L.cls = o;   o = halign(o + (size_t)Cmax * sizeof(PodDev));
   L.gpod = o;  o = halign(o + (size_t)Gmax * sizeof(PodDev));
   L.F = o;     o = halign(o + (size_t)kMaxItems * sizeof(double));
   L.l1 = o;    o = halign(o + (size_t)Cmax * nb * 4);
+  L.l2 = o;    o = halign(o + (l2 ? (size_t)Cmax * nb * 4 : 0));
   L.nodes = o; o = halign(o + (size_t)N * sizeof(NodeRec));
   L.last = o;  o = halign(o + (size_t)N * 4);
   L.cnt = o;   o = halign(o + (size_t)Cmax * 4);
   L.bx = o;    o = halign(o + (size_t)Cmax * 4);
+  L.bx2 = o;   o = halign(o + (l2 ? (size_t)Cmax * 4 : 0));
   L.cgrp = o;  o = halign(o + (size_t)Cmax * 2);
   L.flist = o; o = halign(o + (size_t)Cmax * 2);
   L.code = o;  o = halign(o + (size_t)2 * kMaxItems);  // the F list, double-buffered like d's records
@@ -163,6 +167,7 @@ KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb) {
   L.fnew = o;  o = halign(o + (size_t)Cmax);
   L.fold = o;  o = halign(o + (size_t)Cmax);
   L.gbase = o; o = halign(o + (size_t)Gmax * 2 * 2);
+  L.gkey = o;  o = halign(o + (size_t)Gmax * 2 * 4);  // every score group's key on d, double-buffered like the list
   L.total = o;
   return L;
 }
@@ -242,6 +247,48 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
 // step first), 8 the class waves before the class pass.  Results must not change (tests/test_gpu_hdelay.py).
 using ksim_memo::hdelay;
 
+// The top two keys of a 64-key block row (one uint4 per lane of a 16-lane row), node d's excluded: every
+// lane of the row ends with them (the quad / half-row / row DPP merges of wave_top2: disjoint halves).
+__device__ __forceinline__ void block_top2_excl(const uint4& v, int base, int l16, int d, unsigned& m1, unsigned& m2) {
+  const int n0 = base + 4 * l16;
+  const unsigned x[4] = {n0 + 0 != d ? v.x : 0u, n0 + 1 != d ? v.y : 0u, n0 + 2 != d ? v.z : 0u, n0 + 3 != d ? v.w : 0u};
+  unsigned a1 = 0u, a2 = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (x[i] > a1) { a2 = a1; a1 = x[i]; } else if (x[i] > a2) { a2 = x[i]; }
+  }
+  ksim_memo::merge2_dpp<0xB1>(a1, a2);
+  ksim_memo::merge2_dpp<0x4E>(a1, a2);
+  ksim_memo::merge2_dpp<0x141>(a1, a2);
+  ksim_memo::merge2_dpp<0x140>(a1, a2);
+  m1 = a1;
+  m2 = a2;
+}
+
+// L2: the second-largest key of each (class, block) beside L1's largest, so that the block's new maximum
+// is known without reloading its 64 keys when the node d that held the maximum changes (the flagged rows
+// of the class pass).  kL2Stale: unknown -- set when d held the maximum and dropped below the second, or
+// held the second and dropped (the new second is then max(d's key, the third)); a reload (the flagged row)
+// is needed only when d holds the maximum of a block whose second is unknown.  dr: d's key rank; k its new
+// key; x1, x2: the reloaded row's top two without d (used only when m2 is stale and d held the max).
+constexpr unsigned kL2Stale = 0xFFFFFFFFu;  // (keys are below 2^31)
+__device__ __forceinline__ void l12_update(unsigned& m1, unsigned& m2, unsigned k, int dr, unsigned x1, unsigned x2) {
+  const unsigned o1 = m1, o2 = m2;
+  const bool stale = o2 == kL2Stale;
+  if (o1 != 0u && hkey_rank(o1) == dr) {  // d held the maximum
+    if (stale) { m1 = k > x1 ? k : x1; m2 = k > x1 ? x1 : (k > x2 ? k : x2); }
+    else if (k >= o2) { m1 = k; }
+    else { m1 = o2; m2 = kL2Stale; }
+  } else if (!stale && o2 != 0u && hkey_rank(o2) == dr) {  // d held the second
+    if (k > o1) { m1 = k; m2 = o1; }
+    else if (k >= o2) { m2 = k; }
+    else { m2 = kL2Stale; }
+  } else {
+    if (k > o1) { m1 = k; m2 = o1; }  // (the old maximum is the largest of the others: exact even when stale)
+    else if (!stale && k > o2) { m2 = k; }
+  }
+}
+
 // kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1); kSub = 0: the lean one-
 // workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the
 // KSIM_PROFILE phase timers and the KSIM_HDELAY stress delays (compiled out of the lean launches, as
@@ -267,11 +314,14 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const int N = a.N, nb = a.nbw;  // nb: L1 blocks of this workgroup's slice
   const int lo = w * a.S, ns = min(a.S, N - lo), b0 = lo / kFan;
   const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
-  const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb);
+  const bool use_l2 = a.l2 != nullptr;
+  const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb, use_l2);
   PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
   double* s_F = reinterpret_cast<double*>(smem + L.F);
   unsigned* s_l1 = reinterpret_cast<unsigned*>(smem + L.l1);
+  unsigned* s_l2 = reinterpret_cast<unsigned*>(smem + L.l2);   // use_l2 only
+  unsigned* s_bx2 = reinterpret_cast<unsigned*>(smem + L.bx2); // use_l2 only
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + L.nodes);
   int* s_last = reinterpret_cast<int*>(smem + L.last);
   int* s_cnt = reinterpret_cast<int*>(smem + L.cnt);
@@ -282,6 +332,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   uint8_t* s_fnew = reinterpret_cast<uint8_t*>(smem + L.fnew);
   uint8_t* s_fold = reinterpret_cast<uint8_t*>(smem + L.fold);
   int16_t* const s_gbase_b = reinterpret_cast<int16_t*>(smem + L.gbase);
+  unsigned* const s_gkey_b = reinterpret_cast<unsigned*>(smem + L.gkey);
   uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
@@ -311,11 +362,15 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   for (int g = tid; g < G; g += kHBlock) {
     s_gpod[g] = a.gpod[(size_t)gi * a.Gmax + g];
   }
-  for (int i = tid; i < C * nb; i += kHBlock)
-    s_l1[i] = b0 + i % nb < a.nb ? a.l1[((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb] : 0u;
+  for (int i = tid; i < C * nb; i += kHBlock) {
+    const bool in = b0 + i % nb < a.nb;
+    const size_t gix = ((size_t)gi * a.Cmax + i / nb) * a.nb + b0 + i % nb;
+    s_l1[i] = in ? a.l1[gix] : 0u;
+    if (use_l2) s_l2[i] = in ? a.l2[gix] : 0u;
+  }
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
-  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; }
+  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; sh.f0seq = 0; }
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
@@ -347,7 +402,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const bool w0list = (kSub == 0 || (a.pf & 4) != 0) && (a.pf & 1) != 0;
   const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
   // A bounded wait on one of the bulk's LDS counters (lane 0 of a wave): past the limit the workgroup
-  // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over) instead of hanging.
+  // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over, 32 item 0's F hand-over)
+  // instead of hanging.
   auto spin_until = [&](int* ctr, int target, int bit, int step_, int d_) {
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
@@ -409,6 +465,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     uint8_t* const s_code = s_code_b + cur * kMaxItems;          // this step's F list
     uint8_t* const s_igrp = s_igrp_b + cur * kMaxItems;
     int16_t* const s_gbase = s_gbase_b + cur * a.Gmax;
+    unsigned* const s_gkey = s_gkey_b + cur * a.Gmax;
     if (d >= 0 && wv != 0) {
       // ===== the bulk (waves 1-15): every class but the event's own on d, beside wave 0's critical path;
       //       needed from the next decision on.  Three phases, joined by LDS-counter barriers of these
@@ -459,7 +516,10 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
               tot += __popcll(m) << k;
             }
             int o = base + excl;
-            if (g < G) s_gbase[g] = (int16_t)o;
+            if (g < G) {
+              s_gbase[g] = (int16_t)o;
+              s_gkey[g] = share ? hkey(0, roff + d, 0) : 0u;  // feasible with no fitting GPU; the items max into it
+            }
             unsigned mm = cm;
             while (mm) {
               const int x = __builtin_ctz(mm);
@@ -496,6 +556,27 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
                                  : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
           if (q == 0) s_F[j] = F;
         }
+        // every listed candidate's key into its score group's max (LDS atomics), against item 0's F (d's
+        // current state: quad 0 of wave 1 publishes it; the other F waves wait for it) -- the class update
+        // below then reads one key per class instead of scoring its group's candidates itself
+        if (wv == 1 && lane == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&sh.f0seq, list_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (kProf) hdelay(a.delay, 16, step, wv, wg);
+        if (lane == 0) spin_until(&sh.f0seq, list_seq, 32, step, d);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (q == 0) {
+          const double F0k = s_F[0];
+          for (int j = bt >> 2; j < nit; j += kFW * 16) {
+            if (j == 0) continue;
+            const int code = s_code[j];
+            const unsigned x =
+                hkey(ksim_memo::score_lookup_dev(F0k - s_F[j], sh.th), roff + d, code <= 8 ? 15 - (code - 1) : 0);
+            atomicMax(&s_gkey[s_igrp[j]], x);
+          }
+        }
         if (prof && tid == 64) { sh.prof[7] += (unsigned long long)nit; sh.prof[9] += 1ull; }
         bmark(2);
       } else {
@@ -509,7 +590,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           s_fnew[c] = filter_sum(sn, dn, q) ? 1 : 0;
           s_fold[c] = filter_sum(so, dold, q) ? 1 : 0;
           const unsigned old = c != own ? s_l1[c * nb + b] : 0u;  // the own class's row is wave 0's
-          const bool fl = old != 0u && hkey_rank(old) == roff + d;
+          // d held the block's maximum and (with L2) its second is unknown: reload the block's keys
+          const bool fl = old != 0u && hkey_rank(old) == roff + d && (!use_l2 || s_l2[c * nb + b] == kL2Stale);
           const unsigned long long fm = __ballot(fl);
           if (fm) {
             int o = 0;
@@ -537,52 +619,48 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         const size_t boff = (size_t)(b0 + b) * kFan + 4 * l16;
         if (qid < nflag) v0 = gld4(keys + (size_t)s_flist[qid] * a.Npad + boff);
         if (qid + kCQ < nflag) v1 = gld4(keys + (size_t)s_flist[qid + kCQ] * a.Npad + boff);
-        if (qid < nflag) {
-          const unsigned m = block_max_excl(v0, (b0 + b) * kFan, l16, d);
-          if (l16 == 0) s_bx[s_flist[qid]] = m;
-        }
-        if (qid + kCQ < nflag) {
-          const unsigned m = block_max_excl(v1, (b0 + b) * kFan, l16, d);
-          if (l16 == 0) s_bx[s_flist[qid + kCQ]] = m;
-        }
+        auto reduce_row = [&](const uint4& v, int c) {
+          if (use_l2) {
+            unsigned m1, m2;
+            block_top2_excl(v, (b0 + b) * kFan, l16, d, m1, m2);
+            if (l16 == 0) { s_bx[c] = m1; s_bx2[c] = m2; }
+          } else {
+            const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
+            if (l16 == 0) s_bx[c] = m;
+          }
+        };
+        if (qid < nflag) reduce_row(v0, s_flist[qid]);
+        if (qid + kCQ < nflag) reduce_row(v1, s_flist[qid + kCQ]);
         for (int i = 2 * kCQ + qid; i < nflag; i += kCQ) {
           const int c = s_flist[i];
           const uint4 v = gld4(keys + (size_t)c * a.Npad + boff);
-          const unsigned m = block_max_excl(v, (b0 + b) * kFan, l16, d);
-          if (l16 == 0) s_bx[c] = m;
+          reduce_row(v, c);
         }
         if (prof && ct == 0) { sh.prof[8] += (unsigned long long)nflag; sh.prof[4] += __builtin_amdgcn_s_memrealtime() - tc0; }
       }
       bulk_bar();
       if (tid == 64) sh.nflag = 0;  // (read above, before the barrier; the next class pass adds to it)
-      const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
-      // ---- 3. every other class's group key on d (score steps of its candidates), key[c][d] (HBM
-      //         store), L1[c][d/64] (max with the new key, or the block max without d when d was the
-      //         block max), the feasible count
-      const double F0 = s_F[0];
+      // ---- 3. every other class's key on d (its score group's, scored by the F waves above: the max over the
+      //         group's candidates, fgd_score.go:100-141), key[c][d] (HBM store), L1[c][d/64] (max with the new
+      //         key, or the block max without d when d was the block max), the feasible count
       for (int c = bt; c < C; c += kHBlock - 64) {
         if (c == own) continue;
         const bool fn = s_fnew[c] != 0;
-        unsigned k = 0u;
-        if (fn) {
-          const int g = s_cgrp[c];
-          const int o = s_gbase[g], oe = g + 1 < G ? s_gbase[g + 1] : nit;  // the group's candidates
-          if (is_share_pod(s_gpod[g])) {
-            k = hkey(0, roff + d, 0);  // feasible with no fitting GPU
-            for (int i = o; i < oe; ++i) {
-              const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - s_F[i], sh.th), roff + d, 15 - (s_code[i] - 1));
-              k = x > k ? x : k;
-            }
-          } else {
-            k = hkey(ksim_memo::score_lookup_dev(F0 - s_F[o], sh.th), roff + d, 0);  // NodeResource.Sub state
-          }
-        }
+        const unsigned k = fn ? s_gkey[s_cgrp[c]] : 0u;
         gst1(keys + (size_t)c * a.Npad + d, k);
         s_cnt[c] += (fn ? 1 : 0) - (s_fold[c] ? 1 : 0);
         unsigned* l = &s_l1[c * nb + b];
-        const unsigned old = *l;
-        if (k > old) *l = k;
-        else if (old != 0u && hkey_rank(old) == roff + d) *l = k > s_bx[c] ? k : s_bx[c];
+        if (use_l2) {
+          unsigned m1 = *l, m2 = s_l2[c * nb + b];
+          const bool rl = m1 != 0u && hkey_rank(m1) == roff + d && m2 == kL2Stale;  // reloaded in the class pass
+          l12_update(m1, m2, k, roff + d, rl ? s_bx[c] : 0u, rl ? s_bx2[c] : 0u);
+          *l = m1;
+          s_l2[c * nb + b] = m2;
+        } else {
+          const unsigned old = *l;
+          if (k > old) *l = k;
+          else if (old != 0u && hkey_rank(old) == roff + d) *l = k > s_bx[c] ? k : s_bx[c];
+        }
       }
       bmark(3);
     } else if (wv == 0 && own >= 0) {
@@ -596,7 +674,9 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       const bool fn = filter_node(dn, q), fo = filter_node(dold, q);
       unsigned* l = &s_l1[own * nb + b];
       const unsigned old = __builtin_amdgcn_readfirstlane(*l);
-      const bool flag = old != 0u && hkey_rank(old) == roff + d;  // d was the max of its block
+      const unsigned old2 = use_l2 ? (unsigned)__builtin_amdgcn_readfirstlane((int)s_l2[own * nb + b]) : 0u;
+      // d was the max of its block (and, with L2, the block's second is unknown): reload the block's keys
+      const bool flag = old != 0u && hkey_rank(old) == roff + d && (!use_l2 || old2 == kL2Stale);
       uint4 bv = make_uint4(0u, 0u, 0u, 0u);
       if (flag && lane < 16) bv = gld4(keys + (size_t)own * a.Npad + (size_t)(b0 + b) * kFan + 4 * lane);
       unsigned k = 0u;
@@ -635,13 +715,29 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           k = k > z ? k : z;
         }
       }
-      unsigned bx = 0u;
-      if (flag) bx = (unsigned)__builtin_amdgcn_readfirstlane((int)block_max_excl(bv, (b0 + b) * kFan, lane & 15, d));
+      unsigned bx = 0u, bx2 = 0u;
+      if (flag) {
+        if (use_l2) {
+          unsigned m1, m2;
+          block_top2_excl(bv, (b0 + b) * kFan, lane & 15, d, m1, m2);
+          bx = (unsigned)__builtin_amdgcn_readfirstlane((int)m1);
+          bx2 = (unsigned)__builtin_amdgcn_readfirstlane((int)m2);
+        } else {
+          bx = (unsigned)__builtin_amdgcn_readfirstlane((int)block_max_excl(bv, (b0 + b) * kFan, lane & 15, d));
+        }
+      }
       if (lane == 0) {
         gst1(keys + (size_t)own * a.Npad + d, k);
         s_cnt[own] += (fn ? 1 : 0) - (fo ? 1 : 0);
-        if (k > old) *l = k;
-        else if (flag) *l = k > bx ? k : bx;
+        if (use_l2) {
+          unsigned m1 = old, m2 = old2;
+          l12_update(m1, m2, k, roff + d, bx, bx2);
+          *l = m1;
+          s_l2[own * nb + b] = m2;
+        } else {
+          if (k > old) *l = k;
+          else if (flag) *l = k > bx ? k : bx;
+        }
       }
       // the decision below reads this class's L1 row and count: the wave's LDS operations in order
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -825,6 +921,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           uint8_t* const ncode = s_code_b + (cur ^ 1) * kMaxItems;
           uint8_t* const nigrp = s_igrp_b + (cur ^ 1) * kMaxItems;
           int16_t* const ngbase = s_gbase_b + (cur ^ 1) * a.Gmax;
+          unsigned* const ngkey = s_gkey_b + (cur ^ 1) * a.Gmax;
           int base = 1;  // item 0: the node's current state
           for (int g0 = 0; g0 < G; g0 += 64) {
             const int g = g0 + lane;
@@ -844,7 +941,10 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
               tot += __popcll(m) << k;
             }
             int o = base + excl;
-            if (g < G) ngbase[g] = (int16_t)o;
+            if (g < G) {
+              ngbase[g] = (int16_t)o;
+              ngkey[g] = share ? hkey(0, roff + rk, 0) : 0u;
+            }
             unsigned mm = cm;
             while (mm) {
               const int x = __builtin_ctz(mm);
@@ -927,6 +1027,7 @@ struct HInitArgs {
   unsigned* gsc;           // [Rg][Gmax][Smax] hkey(score, 0, gf) without the rank field
   unsigned* keys;          // [Rg][Cmax][Npad]
   unsigned* l1;            // [Rg][Cmax][nb]
+  unsigned* l2;            // [Rg][Cmax][nb] second maxima, or null
   int* cnt;                // [Rg][Cmax], zeroed before k_hinit_keys
   const double* th;
 };
@@ -974,9 +1075,11 @@ __global__ __launch_bounds__(256) void k_hinit_keys(HInitArgs a) {
   a.keys[((size_t)gi * a.Cmax + c) * a.Npad + rank] = k;
   const int lane = (int)(threadIdx.x & 63);
   const unsigned long long fb = __ballot(k != 0u);
-  const unsigned m = (unsigned)ksim_replay::wave_max_dpp((int)k);
+  unsigned m = k, m2 = 0u;
+  ksim_memo::wave_top2(m, m2);  // (every lane active: one wave = one block of 64 ranks)
   if (lane == 0) {
     a.l1[((size_t)gi * a.Cmax + c) * a.nb + rank / kFan] = m;
+    if (a.l2) a.l2[((size_t)gi * a.Cmax + c) * a.nb + rank / kFan] = m2;
     if (fb) atomicAdd(&a.cnt[(size_t)gi * a.Cmax + c], (int)__popcll(fb));
   }
 }
