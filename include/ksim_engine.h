@@ -294,7 +294,9 @@ int  ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int 
 /* The per-event power report of a replica with an energy model (ksim_engine_set_power_model, any
  * policy); KSIM_ESTATE without one or while the report is disabled. */
 int  ksim_engine_get_power_reports(ksim_engine* e, int replica, ksim_power_report* out, int n);
-/* Device time of the report kernels of the last run (ms; part of last_run_ms). */
+/* Device time of the report kernels of the last run that follows the whole replay (ms; part of
+ * last_run_ms).  Near 0 when the replay ran as concurrent groups: each group's report then runs on
+ * the group's stream right behind its replay, overlapping the groups still running. */
 int  ksim_engine_last_report_ms(ksim_engine* e, double* ms);
 
 /* Node-sharded single cluster (SURVEY §8(e), C5 across GPUs).  One engine (R = 1) per shard holds

@@ -1663,6 +1663,7 @@ struct ksim_engine {
   hipStream_t side[kSide] = {};
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
+  bool report_done = false;  // run_persistent ran the report behind each concurrent group (last run)
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
   bool report = false;
@@ -3112,14 +3113,15 @@ static int alloc_report(ksim_engine* e, int r) {
 }
 
 // The per-event cluster report of every replica from the run's snapshots (ksim_report.hpp).
-static int run_report(ksim_engine* e, int max_ev) {
-  if (max_ev <= 0) return KSIM_OK;
-  const dim3 grid((unsigned)((max_ev + ksim_rep::kDeltaBlock - 1) / ksim_rep::kDeltaBlock), (unsigned)e->R);
-  hipLaunchKernelGGL(ksim_rep::k_report_delta, grid, dim3(ksim_rep::kDeltaBlock), 0, e->stream,
-                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp);
+// list (device, nullable): only these R replicas -- one concurrent group's, on its own stream behind its replay.
+static int run_report(ksim_engine* e, int max_ev, hipStream_t st, const int* list, int R) {
+  if (max_ev <= 0 || R <= 0) return KSIM_OK;
+  const dim3 grid((unsigned)((max_ev + ksim_rep::kDeltaBlock - 1) / ksim_rep::kDeltaBlock), (unsigned)R);
+  hipLaunchKernelGGL(ksim_rep::k_report_delta, grid, dim3(ksim_rep::kDeltaBlock), 0, st,
+                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, list);
   KSIM_HIP(hipGetLastError());
-  hipLaunchKernelGGL(ksim_rep::k_report_scan, dim3(e->R), dim3(ksim_rep::kScanBlock), 0, e->stream,
-                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N);
+  hipLaunchKernelGGL(ksim_rep::k_report_scan, dim3(R), dim3(ksim_rep::kScanBlock), 0, st,
+                     (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N, list);
   KSIM_HIP(hipGetLastError());
   return KSIM_OK;
 }
@@ -3410,6 +3412,15 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     concurrent = K == 1;
   }
   int gidx = 0;
+  // The side streams share the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4), and two
+  // streams on one queue run their kernels one after the other.  So no more side streams than queues:
+  // the first group (FGD on k_hmemo, the longest in a paper sweep) gets one to itself, the others take
+  // the rest round robin (the engine stream, which only waits meanwhile, shares a queue with one of them).
+  int nq = 4;
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES")) nq = std::atoi(q) > 0 ? std::atoi(q) : nq;
+  if (const char* q = std::getenv("KSIM_SIDE_STREAMS")) nq = std::atoi(q) > 0 ? std::atoi(q) : nq;
+  nq = std::max(1, std::min(nq, (int)ksim_engine::kSide));
+  unsigned used = 0u;
   if (concurrent) {
     if (!e->ev_fork) KSIM_HIP(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
     KSIM_HIP(hipEventRecord(e->ev_fork, e->stream));
@@ -3418,13 +3429,14 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     const int Rg = gp.second;
     hipStream_t gs = e->stream;
     if (concurrent) {
-      const int i = gidx % ksim_engine::kSide;
+      const int i = (gidx == 0 || nq == 1) ? 0 : 1 + (gidx - 1) % (nq - 1);
       if (!e->side[i]) {
         KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
         KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
       }
       gs = e->side[i];
-      if (gidx < ksim_engine::kSide) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));
+      if (!(used & (1u << i))) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));
+      used |= 1u << i;
     }
     ++gidx;
     if (gp.first == kPolRandomGo) {
@@ -3554,8 +3566,24 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       print_replay_profile(e, Rg, K, max_ev);
     }
   }
+  if (concurrent && e->report) {
+    // each group's report on its own stream, behind its replay: the groups that finish early report while
+    // the longest still runs
+    int f = 0;
+    for (size_t g = 0; g < groups.size(); ++g) {
+      const int Rg = groups[g].second;
+      const int i = (g == 0 || nq == 1) ? 0 : 1 + ((int)g - 1) % (nq - 1);
+      int mev = 0;
+      for (int j = f; j < f + Rg; ++j) mev = std::max(mev, e->n_events[order[j]]);
+      const int rc = run_report(e, mev, e->side[i], e->d_replist + f, Rg);
+      if (rc) return rc;
+      f += Rg;
+    }
+    e->report_done = true;
+  }
   if (concurrent)  // join: the engine stream waits for every side stream used
-    for (int i = 0; i < std::min(gidx, (int)ksim_engine::kSide); ++i) {
+    for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
+      if (!(used & (1u << i))) continue;
       KSIM_HIP(hipEventRecord(e->side_ev[i], e->side[i]));
       KSIM_HIP(hipStreamWaitEvent(e->stream, e->side_ev[i], 0));
     }
@@ -3579,6 +3607,7 @@ int ksim_engine_run(ksim_engine* e) {
     max_ev = std::max(max_ev, e->n_events[r]);
   }
   KSIM_HIP(hipSetDevice(e->device));
+  e->report_done = false;
   int rc = prepare_memo(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
@@ -3598,8 +3627,8 @@ int ksim_engine_run(ksim_engine* e) {
   else rc = step_path ? run_graph(e, max_ev) : run_persistent(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
-  if (e->report) {
-    rc = run_report(e, max_ev);
+  if (e->report && !e->report_done) {
+    rc = run_report(e, max_ev, e->stream, nullptr, e->R);
     if (rc) return rc;
   }
   KSIM_HIP(hipEventRecord(e->ev1, e->stream));
@@ -3995,7 +4024,7 @@ int ksim_shard_group_run(ksim_engine* const* engines, int world) {
       if ((rc = shard_commit(engines[k], st, nullptr, s))) return rc;
   }
   for (int k = 0; k < world; ++k)
-    if (engines[k]->report && (rc = run_report(engines[k], max_ev))) return rc;
+    if (engines[k]->report && (rc = run_report(engines[k], max_ev, engines[k]->stream, nullptr, engines[k]->R))) return rc;
   KSIM_HIP(hipEventRecord(e0->ev1, st));
   KSIM_HIP(hipStreamSynchronize(st));
   float ms = 0;

@@ -84,8 +84,9 @@ __device__ __forceinline__ void store_rep(RepAcc* o, const __int128 (&f)[kFields
 }
 
 // grid (ceil(E_max / kDeltaBlock), R): the report delta of every event.
-__global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* reps, const TypDev* __restrict__ tp_all) {
-  const int r = (int)blockIdx.y;
+__global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
+                                                              const int* list) {
+  const int r = list ? list[blockIdx.y] : (int)blockIdx.y;  // list: one concurrent group's replicas
   const ReplicaDev rp = reps[r];
   if (!rp.rep) return;
   __shared__ TypDev s_tp[kMaxTypical];
@@ -161,8 +162,8 @@ __device__ __forceinline__ bool power_field(int k) { return k == 7 || k == 8 || 
 // grid R: the initial cluster's report, then the inclusive prefix over the events (in place),
 // one field at a time (keeps the 128-bit running sums in a few registers).
 __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
-                                                            int N) {
-  const int r = (int)blockIdx.x;
+                                                            int N, const int* list) {
+  const int r = list ? list[blockIdx.x] : (int)blockIdx.x;
   const ReplicaDev rp = reps[r];
   if (!rp.rep) return;
   __shared__ TypDev s_tp[kMaxTypical];

@@ -28,3 +28,8 @@ KSIM_PROFILE=1 timeout -k 10 200 python -u bench.py --run-mode 5 --steps 1 --war
 # PWR + FGD (k_replay<7>): the phase profile, then workgroups per replica
 KSIM_PROFILE=1 timeout -k 10 200 python -u bench.py --policy "PWR 500 FGD 500" --steps 1 --warmup 0 --no-cpu-baseline > $O/prof_pf.log 2>&1; grep -o "ksim profile.*" $O/prof_pf.log
 for k in 25 16 10 32; do one pf_k$k "--policy PWR_500_FGD_500 --wgs $k --steps 5 --warmup 1"; done
+# C4: the concurrent groups on no more side streams than hardware queues (default) vs six (r03's mapping shape)
+for i in 1 2; do
+  one c4_q4_$i "--config c4 --steps 3 --warmup 1"
+  one c4_q6_$i "--config c4 --steps 3 --warmup 1" KSIM_SIDE_STREAMS=6
+done

