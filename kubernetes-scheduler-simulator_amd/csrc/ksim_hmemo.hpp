@@ -135,7 +135,8 @@ struct __align__(16) HShared {
   // while slower waves may still be reading this step's skip condition, so it writes [cur ^ 1] and folds
   // [cur] into `dead`; every reader checks dead | pdead[cur] (the same answer before and after the fold).
   int pdead[2];
-  int pad_[3];
+  int f0seq;           // refreshes whose item 0 (d's current state) has its F in s_F[0] (the item keys' reference)
+  int pad_[2];
   unsigned long long prof[kHProf];
   unsigned dead[32];   // class slots with no feasible node (create-only streams: for good)
 };
@@ -143,7 +144,7 @@ static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned"
 
 // Dynamic LDS after HShared (16-B aligned regions).
 struct HLayout {
-  size_t cls, gpod, l1, l2, nodes, last, cnt, bx, bx2, cgrp, flist, code, igrp, fnew, fold, gbase, gkey, total;
+  size_t cls, gpod, F, l1, l2, nodes, last, cnt, bx, bx2, cgrp, flist, code, igrp, fnew, fold, gbase, gkey, total;
 };
 KSIM_HD size_t halign(size_t x) { return (x + 15) & ~(size_t)15; }
 KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2) {
@@ -151,6 +152,7 @@ KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2) {
   size_t o = sizeof(HShared);
   L.cls = o;   o = halign(o + (size_t)Cmax * sizeof(PodDev));
   L.gpod = o;  o = halign(o + (size_t)Gmax * sizeof(PodDev));
+  L.F = o;     o = halign(o + (size_t)kMaxItems * sizeof(double));
   L.l1 = o;    o = halign(o + (size_t)Cmax * nb * 4);
   L.l2 = o;    o = halign(o + (l2 ? (size_t)Cmax * nb * 4 : 0));
   L.nodes = o; o = halign(o + (size_t)N * sizeof(NodeRec));
@@ -316,6 +318,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb, use_l2);
   PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
+  double* s_F = reinterpret_cast<double*>(smem + L.F);
   unsigned* s_l1 = reinterpret_cast<unsigned*>(smem + L.l1);
   unsigned* s_l2 = reinterpret_cast<unsigned*>(smem + L.l2);   // use_l2 only
   unsigned* s_bx2 = reinterpret_cast<unsigned*>(smem + L.bx2); // use_l2 only
@@ -367,7 +370,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   }
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
-  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; }
+  if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; sh.f0seq = 0; }
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
@@ -399,7 +402,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const bool w0list = (kSub == 0 || (a.pf & 4) != 0) && (a.pf & 1) != 0;
   const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
   // A bounded wait on one of the bulk's LDS counters (lane 0 of a wave): past the limit the workgroup
-  // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over) instead of hanging.
+  // stops with a failure bit (4 bulk barrier, 8 class barrier, 16 list hand-over, 32 item 0's F hand-over)
+  // instead of hanging.
   auto spin_until = [&](int* ctr, int target, int bit, int step_, int d_) {
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
@@ -540,40 +544,38 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
-        const int q = bt & 3, qd = lane >> 2;
-        const uint32_t tb = 1u << dn.gpu_type();
-        auto eval_F = [&](int j) {
+        const int q = bt & 3;
+        for (int j = bt >> 2; j < nit; j += kFW * 16) {
           const int code = s_code[j];
           const PodDev gp = s_gpod[s_igrp[j]];
           int cpuL, total;
           uint32_t gs[4];
           fgd_candidate(dn, code, gp, &cpuL, gs, &total);
-          return typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
-                       : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
-        };
-        // Quad 0 of every F wave evaluates item 0 (d's current state) and quads 1-15 the listed candidates
-        // 1.., kFW x 15 per round; each candidate's key (fgd_score.go:100-141, against this wave's own item
-        // 0) goes into its score group's max by an LDS atomic, so the class update below reads one key per
-        // class and no F crosses waves.
-        constexpr int kPer = kFW * 15;
-        const int j0 = 1 + (wv - 1) * 15 + (qd - 1);  // quads 1-15: the first round's candidate
-        const int jr = qd == 0 ? 0 : j0;
-        double F = 0.0;
-        if (jr < nit) F = eval_F(jr);
-        const unsigned long long fb = __builtin_bit_cast(unsigned long long, F);
-        const double F0 = __builtin_bit_cast(double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
-                                                          (int)(unsigned)(fb >> 32), 0) << 32) |
-                                                         (unsigned)__builtin_amdgcn_readlane((int)(unsigned)fb, 0));
-        auto key_out = [&](int j, double Fj) {
-          const int code = s_code[j];
-          const unsigned x = hkey(ksim_memo::score_lookup_dev(F0 - Fj, sh.th), roff + d, code <= 8 ? 15 - (code - 1) : 0);
-          atomicMax(&s_gkey[s_igrp[j]], x);
-        };
-        if (qd != 0 && q == 0 && jr < nit) key_out(jr, F);
-        for (int j = j0 + kPer; j < nit; j += kPer) {  // lists longer than one round (quad 0 idles)
-          if (qd == 0) continue;
-          const double Fj = eval_F(j);
-          if (q == 0) key_out(j, Fj);
+          const uint32_t tb = 1u << dn.gpu_type();
+          const double F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
+                                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          if (q == 0) s_F[j] = F;
+        }
+        // every listed candidate's key into its score group's max (LDS atomics), against item 0's F (d's
+        // current state: quad 0 of wave 1 publishes it; the other F waves wait for it) -- the class update
+        // below then reads one key per class instead of scoring its group's candidates itself
+        if (wv == 1 && lane == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __hip_atomic_store(&sh.f0seq, list_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (kProf) hdelay(a.delay, 16, step, wv, wg);
+        if (lane == 0) spin_until(&sh.f0seq, list_seq, 32, step, d);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (q == 0) {
+          const double F0k = s_F[0];
+          for (int j = bt >> 2; j < nit; j += kFW * 16) {
+            if (j == 0) continue;
+            const int code = s_code[j];
+            const unsigned x =
+                hkey(ksim_memo::score_lookup_dev(F0k - s_F[j], sh.th), roff + d, code <= 8 ? 15 - (code - 1) : 0);
+            atomicMax(&s_gkey[s_igrp[j]], x);
+          }
         }
         if (prof && tid == 64) { sh.prof[7] += (unsigned long long)nit; sh.prof[9] += 1ull; }
         bmark(2);

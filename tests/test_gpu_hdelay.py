@@ -23,8 +23,8 @@ import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALL = "0xf"  # every delay point: bulk before the skip read, wave 1 before its list, wave 0 before its decision,
-             # the class waves before the class pass
+ALL = "0x1f"  # every delay point: bulk before the skip read, wave 1 before its list, wave 0 before its decision,
+              # the class waves before the class pass, the F waves before item 0's F hand-over (the group keys)
 SEEDS = list(range(42, 52))
 
 
