@@ -715,7 +715,7 @@ void k_replay(ksim_replay::ReplayArgs a,
   const int n_lo = w * a.S;
   const int ns = max(0, min(a.S, a.N - n_lo));
   constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
-  const RLayout L = replay_layout(a.S, kPol, kGeneral);
+  const RLayout L = replay_layout(a.S, kPol, kGeneral, kPF ? a.pm_c : 0);
   ReplayFgd& fs = *reinterpret_cast<ReplayFgd*>(smem + L.fgd);  // FGD launches only
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + L.nodes);
   uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + L.tags);  // kTags only
@@ -730,6 +730,20 @@ void k_replay(ksim_replay::ReplayArgs a,
   int* s_last = reinterpret_cast<int*>(smem + L.last);
   int* s_praw = reinterpret_cast<int*>(smem + L.praw);  // PWR+FGD per-slot scratch of the current step
   int* s_pinf = reinterpret_cast<int*>(smem + L.pinf);
+  // PWR+FGD memo (a.pm_c > 0): every class's Filter + Score of every real slot, kept while the slot's
+  // record is unchanged (s_pver), so a step evaluates only the slots changed since its class last came
+  // and the virtual slot
+  const bool pmon = kPF && a.pm_c > 0;
+  unsigned* s_pver = reinterpret_cast<unsigned*>(smem + L.pver);
+  uint2* s_pm = reinterpret_cast<uint2*>(smem + L.pm);
+  auto pm_bump = [&](int i) {  // (one lane) slot i's record changed: its entries are stale
+    unsigned v = s_pver[i] + 1u;
+    if (v == kPmInvalid) {  // the version field wraps: forget the slot's entries first
+      v = 0u;
+      for (int c = 0; c < a.pm_c; ++c) s_pm[(size_t)c * a.S + i].y = kPmInvalid << 18;
+    }
+    s_pver[i] = v;
+  };
   // hist[step]: (node, mask+1) bound here | (-1,0) no winner | (-2,0) winner elsewhere | (-3,0) Reserve failed here
   // (null when no replica of the launch has a delete event: nothing ever reads it)
   int2* hist = (kGeneral && a.hist) ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
@@ -746,6 +760,10 @@ void k_replay(ksim_replay::ReplayArgs a,
       reinterpret_cast<unsigned long long*>(&sh.pw)[i] = reinterpret_cast<const unsigned long long*>(rp.pw)[i];
     for (int i = tid; i < ns; i += kRBlock) s_pe[i] = energy_static(rp.cap[n_lo + i], rp.cpum[n_lo + i], *rp.pw);
     for (int i = tid; i <= ns; i += kRBlock) s_E0[i] = kEnergyStale;
+  }
+  if (pmon) {
+    for (int i = tid; i <= ns; i += kRBlock) s_pver[i] = a.pm_ver0;
+    for (int i = tid; i < a.pm_c * a.S; i += kRBlock) s_pm[i] = make_uint2(0u, kPmInvalid << 18);
   }
   if (kFgd) {
     for (int i = tid; i <= ns; i += kRBlock) s_F0[i] = -1.0;  // every cached F stale
@@ -959,6 +977,7 @@ void k_replay(ksim_replay::ReplayArgs a,
             else if (lane == 2 && !kTags && p_tag >= 0) g_tags[(size_t)p_b * kTagStride + p_tag] += 1;
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
             else if (lane == 8 && kPF) { s_praw[p_b] = s_praw[ns]; s_pinf[p_b] = s_pinf[ns]; }
+            else if (lane == 10 && pmon) pm_bump(p_b);
             else if (lane == 9 && (kPwr || kPF)) s_E0[p_b] = s_E0[ns];
             else if (lane == 7 && snap) {  // cluster report: the post-Bind record (the virtual slot)
               store_node(snap + p_step, load_node(&s_nodes[ns]));
@@ -1034,6 +1053,7 @@ void k_replay(ksim_replay::ReplayArgs a,
                      h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
           if (kPwr || kPF) s_E0[loc] = kEnergyStale;
+          if (pmon) pm_bump(loc);
           if (snap) {
             store_node(snap + step, load_node(&s_nodes[loc]));
             rp.prev[step] = s_last[loc];
@@ -1095,7 +1115,14 @@ void k_replay(ksim_replay::ReplayArgs a,
         const bool valid = (tid >> 3) < cn;
         NodeV n{};
         bool feas = false;
-        if (valid) {
+        // PWR+FGD memo: a real slot unchanged since this class last came reuses its entry
+        bool hit = false;
+        uint2 me = make_uint2(0u, 0u);
+        if (pmon && valid && i < ns) {
+          me = s_pm[(size_t)p.pad * a.S + i];
+          hit = pf_memo_hit(me, s_pver[i]);
+        }
+        if (valid && !hit) {
           n = load_node(&s_nodes[i]);
           feas = filter_node(n, p);
         }
@@ -1179,12 +1206,20 @@ void k_replay(ksim_replay::ReplayArgs a,
         if constexpr (kPF) {
           // the node's raw PWR score and GPU choice (pwr_score.go:48-91) beside its FGD score
           int pgpu = -1;
-          const int praw = pwr8_finish(pv, &pgpu);
+          int praw = pwr8_finish(pv, &pgpu);
+          int pinf = feas ? (kPfFeas | (perr ? kPfErr : 0) | (raw & 0xff) | ((pgpu + 1) & 0xf) << 8 |
+                             ((gpu + 1) & 0xf) << 12)
+                          : 0;
+          if (hit) {
+            praw = (int)me.x;
+            pinf = pf_memo_pinf(me);
+            feas = (pinf & kPfFeas) != 0;
+            perr = (pinf & kPfErr) != 0;
+          }
           if (valid && g == 0) {
             s_praw[i] = praw;
-            s_pinf[i] = feas ? (kPfFeas | (perr ? kPfErr : 0) | (raw & 0xff) | ((pgpu + 1) & 0xf) << 8 |
-                                ((gpu + 1) & 0xf) << 12)
-                             : 0;
+            s_pinf[i] = pinf;
+            if (pmon && !hit && i < ns) s_pm[(size_t)p.pad * a.S + i] = pf_memo_pack(praw, pinf, s_pver[i]);
           }
           route_a(valid && g == 0, i, feas, perr, praw);
         } else {
@@ -1663,7 +1698,8 @@ struct ksim_engine {
   hipStream_t side[kSide] = {};
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
-  bool report_done = false;  // run_persistent ran the report behind each concurrent group (last run)
+  bool report_done = false;
+  int last_pf_memo = 0;      // PWR+FGD memo class stride of the last k_replay<PWR+FGD> launch (0: none)  // run_persistent ran the report behind each concurrent group (last run)
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
   bool report = false;
@@ -2395,6 +2431,11 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     ma.pf = pf ? std::atoi(pf) & 7 : 1;  // (4: the wide form lists on wave 0 too)
   }
   ma.delay = hdelay_mask();
+  {  // F waves for the replicas with more than 64 typical pods (the rest of the 15 bulk waves run the class pass)
+    const char* fw = std::getenv("KSIM_HFW");
+    const int v = fw ? std::atoi(fw) : ksim_hmemo::kFW;
+    ma.fw_big = v >= 1 && v <= 13 ? v : ksim_hmemo::kFW;
+  }
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }
@@ -3525,8 +3566,30 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipMalloc(&e->d_hist, sizeof(int2) * need));
       e->hist_cap = need;
     }
-    const size_t lds = replay_lds(S, gp.first, general);
+    size_t lds = replay_lds(S, gp.first, general);
+    // PWR+FGD: the per-(class, slot) memo when every class of the group fits beside the slice
+    // (KSIM_PF_MEMO=0: evaluate every slot every step, as before r04)
+    int pm_c = 0;
+    if (gp.first == POL_PWR_FGD) {
+      const char* pm = std::getenv("KSIM_PF_MEMO");
+      if (!(pm && pm[0] == '0')) {
+        for (int j = first; j < first + Rg; ++j) pm_c = std::max(pm_c, (int)e->h_cls[order[j]].size());
+        const size_t lm = ksim_replay::replay_layout(S, gp.first, general, pm_c).total;
+        if (pm_c > 0 && lm <= 160 * 1024 &&
+            (K == 1 || resident_cap(e, replay_kernel(gp.first, K, general), lm) >= Rg * K))
+          lds = lm;
+        else
+          pm_c = 0;
+      }
+    }
+    e->last_pf_memo = pm_c;
     ksim_replay::ReplayArgs ra;
+    ra.pm_c = pm_c;
+    {
+      const char* v0 = std::getenv("KSIM_PF_MEMO_VER0");
+      const long v = v0 ? std::atol(v0) : 0;
+      ra.pm_ver0 = v > 0 && v < (long)ksim_replay::kPmInvalid ? (unsigned)v : 0u;
+    }
     ra.reps = e->d_reps;
     ra.rep_list = e->d_replist + first;
     ra.N = e->N;

@@ -112,6 +112,7 @@ struct HMemoArgs {
   int pf;                   // one workgroup per replica: 1 (default) = wave 0 lists the next refresh's F evaluations after its
                             // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
   int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
+  int fw_big;               // F waves of a replica with more than 64 typical pods (KSIM_HFW; kFW by default)
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -397,7 +398,10 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int cur = 0;         // the d-record buffer of this step (toggled at the end of every decided step)
   int bar_target = 0;  // the bulk barrier's count so far (waves 1-15)
   int cbar_target = 0; // the class waves' barrier count so far
-  int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..kFW)
+  int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..fw)
+  // F waves (1..fw) and class waves (fw+1..15): kFW, or a.fw_big for a replica with more than 64 typical
+  // pods (the F rounds grow with the table, the class pass does not)
+  const int fw = rp.nt > 64 ? a.fw_big : kFW, cw = kHWaves - 1 - fw;
   // wave 0 lists the next refresh's F evaluations (one workgroup per replica; the wide form too with bit 4)
   const bool w0list = (kSub == 0 || (a.pf & 4) != 0) && (a.pf & 1) != 0;
   const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
@@ -490,7 +494,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
       //      beside waves kFW+1..15: the class pass (Filter on d's new and old records; which classes
       //      had d as the max of d's block: flagged), then the flagged blocks' loads (one quarter-wave
       //      each) and their maxima without d
-      if (wv <= kFW) {
+      if (wv <= fw) {
         ++list_seq;
         if (w0list) {
           // listed by wave 0 after the previous decided step's Bind
@@ -545,7 +549,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         }
         const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
         const int q = bt & 3;
-        for (int j = bt >> 2; j < nit; j += kFW * 16) {
+        for (int j = bt >> 2; j < nit; j += fw * 16) {
           const int code = s_code[j];
           const PodDev gp = s_gpod[s_igrp[j]];
           int cpuL, total;
@@ -569,7 +573,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (q == 0) {
           const double F0k = s_F[0];
-          for (int j = bt >> 2; j < nit; j += kFW * 16) {
+          for (int j = bt >> 2; j < nit; j += fw * 16) {
             if (j == 0) continue;
             const int code = s_code[j];
             const unsigned x =
@@ -580,12 +584,12 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         if (prof && tid == 64) { sh.prof[7] += (unsigned long long)nit; sh.prof[9] += 1ull; }
         bmark(2);
       } else {
-        const int ct = tid - (kFW + 1) * 64;  // class-wave thread
+        const int ct = tid - (fw + 1) * 64;  // class-wave thread
         const unsigned long long tc0 = (prof && ct == 0) ? __builtin_amdgcn_s_memrealtime() : 0ull;
         if constexpr (kProf) hdelay(a.delay, 8, step, wv, wg);
         const NodeV dold = uniform_node(&sh.dold[cur]);
         const NodeSum sn = node_sum(dn), so = node_sum(dold);
-        for (int c = ct; c < C; c += kCW * 64) {
+        for (int c = ct; c < C; c += cw * 64) {
           const PodDev q = s_cls[c];
           s_fnew[c] = filter_sum(sn, dn, q) ? 1 : 0;
           s_fold[c] = filter_sum(so, dold, q) ? 1 : 0;
@@ -603,7 +607,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           }
         }
         // the class waves' own barrier (LDS counter): every flag is listed
-        cbar_target += kCW;
+        cbar_target += cw;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) {
           __hip_atomic_fetch_add(&sh.cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -613,7 +617,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int nflag = __builtin_amdgcn_readfirstlane(sh.nflag);
         const int qid = ct >> 4, l16 = ct & 15;
-        constexpr int kCQ = kCW * 4;  // quarter-waves of the class waves
+        const int kCQ = cw * 4;  // quarter-waves of the class waves
         // two rows per quarter-wave in flight at once, then any further ones one by one
         uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
         const size_t boff = (size_t)(b0 + b) * kFan + 4 * l16;

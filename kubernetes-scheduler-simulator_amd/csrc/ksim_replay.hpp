@@ -62,6 +62,8 @@ struct ReplayArgs {
   int* fail;
   unsigned long long* prof;  // optional [R*K][8] s_memrealtime phase sums (KSIM_PROFILE=1), else null
   int skip;                  // the dead-class skip (create-only streams; class ids < 1024)
+  int pm_c;                  // PWR+FGD: class stride of the per-(class, slot) memo in LDS, 0 = no memo
+  unsigned pm_ver0;          // the slots' first version (KSIM_PF_MEMO_VER0: tests start near the wrap)
 };
 constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 
@@ -107,9 +109,11 @@ static_assert(sizeof(ReplayFgd) % 16 == 0, "keep the node records 16-B aligned")
 
 // The dynamic LDS layout of one k_replay workgroup (host and device).
 struct RLayout {
-  size_t fgd, nodes, tags, F0, E0, pe, last, praw, pinf, total;
+  size_t fgd, nodes, tags, F0, E0, pe, last, praw, pinf, pver, pm, total;
 };
-__host__ __device__ inline RLayout replay_layout(int S, int pol, bool general) {
+// pm_c > 0 (PWR+FGD): u32 pver[S+1] (each slot's state version) and uint2 pm[pm_c][S] (every class's
+// memoised Filter + Score of every real slot, valid while its version matches; pf_memo_* below)
+__host__ __device__ inline RLayout replay_layout(int S, int pol, bool general, int pm_c = 0) {
   const bool tags = pol == POL_CLUSTERING, fgd = pol == POL_FGD || pol == POL_PWR_FGD;
   const bool pwr = pol == POL_PWR || pol == POL_PWR_FGD, pf = pol == POL_PWR_FGD;
   const size_t S1 = (size_t)S + 1;
@@ -124,8 +128,23 @@ __host__ __device__ inline RLayout replay_layout(int S, int pol, bool general) {
   L.last = o;  o += general ? S1 * sizeof(int) : 0;
   L.praw = o;  o += pf ? S1 * sizeof(int) : 0;
   L.pinf = o;  o += pf ? S1 * sizeof(int) : 0;
+  L.pver = o;  o += (pf && pm_c > 0) ? (S1 * sizeof(unsigned) + 15) / 16 * 16 : 0;
+  L.pm = o;    o += (pf && pm_c > 0) ? (size_t)pm_c * S * sizeof(uint2) : 0;
   L.total = o;
   return L;
+}
+
+// PWR+FGD memo entry of one (class, slot): x = the raw PWR score, y = the packed FGD score / GPU choices
+// (pinf's low 16 bits), Filter's verdict (16), the Score error (17) and the slot version it was computed
+// at (18-31; kPmInvalid: never).  A slot's version advances whenever its node record changes.
+constexpr unsigned kPmInvalid = 0x3fffu;
+__device__ __forceinline__ bool pf_memo_hit(const uint2& e, unsigned ver) { return (e.y >> 18) == ver; }
+__device__ __forceinline__ uint2 pf_memo_pack(int praw, int pinf, unsigned ver) {
+  return make_uint2((unsigned)praw, ((unsigned)pinf & 0xffffu) | ((pinf & (1 << 30)) ? 1u << 16 : 0u) |
+                                        ((pinf & (1 << 29)) ? 1u << 17 : 0u) | (ver << 18));
+}
+__device__ __forceinline__ int pf_memo_pinf(const uint2& e) {  // back to pinf's layout (kPfFeas 30, kPfErr 29)
+  return (int)((e.y & 0xffffu) | ((e.y >> 16) & 1u) << 30 | ((e.y >> 17) & 1u) << 29);
 }
 
 __device__ __forceinline__ unsigned long long gload(const unsigned long long* p) {

@@ -166,3 +166,20 @@ def test_errors(default_trace):
     with pytest.raises(ksim.KsimError):
         eng.filter_score(0, rp.events[0])  # two plugins: no single plugin-level Score
     eng.close()
+
+
+@pytest.mark.parametrize("env", [{"KSIM_PF_MEMO": "0"}, {"KSIM_PF_MEMO_VER0": str(0x3fff - 3)}])
+def test_pf_memo_off_and_version_wrap(default_trace, monkeypatch, env):
+    # k_replay<PWR+FGD> keeps every class's Filter + Score of every slot in LDS while the slot's record is
+    # unchanged (the default): without the memo, and with the slot versions starting three changes before
+    # their 14-bit field wraps (every entry of a wrapping slot is forgotten first), the decisions stay the
+    # oracle's -- the subset replay at the default K and at K = 1
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rp = default_trace.replay(seed=45)
+    keep = list(range(2, default_trace.num_nodes, 7))
+    for kw in (dict(), dict(wgs_per_replica=1)):
+        res, state, path = engine_run(default_trace, rp, keep, 1500, "PWR 500 FGD 500", **kw)
+        want, want_state, _ = oracle_run(default_trace, rp, keep, 1500, "PWR 500 FGD 500")
+        assert path == "k_replay"
+        assert_same(res, want, state, want_state)
