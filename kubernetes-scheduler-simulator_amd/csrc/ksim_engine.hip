@@ -2474,7 +2474,14 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     return KSIM_ERANGE;
   }
   const TypDev* tpp = e->d_tp;
-  const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
+  // KSIM_HMEMO_EXCL=1 (K = 1): ask for a whole CU's LDS, so that no other group's workgroup shares a CU with a
+  // k_hmemo one (the paper sweep's concurrent groups)
+  size_t lds = pl.lds;
+  if (pl.K == 1) {
+    const char* ex = std::getenv("KSIM_HMEMO_EXCL");
+    if (ex && ex[0] == '1') lds = 160 * 1024;
+  }
+  const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, lds, st, e->coop && pl.K > 1, ma, tpp);
   if (lrc) return lrc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
