@@ -3479,7 +3479,14 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     if (concurrent) {
       const int i = (gidx == 0 || nq == 1) ? 0 : 1 + (gidx - 1) % (nq - 1);
       if (!e->side[i]) {
-        KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
+        // KSIM_SIDE_PRIO=1: the first group's stream at the device's greatest priority, so that its workgroups
+        // are dispatched ahead of the short groups' (measured within C4's run-to-run spread: off by default)
+        const char* pr = std::getenv("KSIM_SIDE_PRIO");
+        int lo = 0, hi = 0;
+        if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+          KSIM_HIP(hipStreamCreateWithPriority(&e->side[i], hipStreamNonBlocking, hi));
+        else
+          KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
         KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
       }
       gs = e->side[i];
