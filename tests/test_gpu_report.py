@@ -148,3 +148,36 @@ def test_report_full_openb_fgd_curves(default_trace):
         assert abs(cg["frag"][k] - cw["frag"][k]) <= 0.011, k  # 2-decimal printing of 1e-12-close values
     # expected_results/analysis_allo_discrete.csv, 06-FGD @ 130% arrived: 95.27-95.49 over seeds 42-51
     assert 94.5 < cg["alloc"][130] < 96.0
+
+
+@pytest.mark.parametrize("side", ["1", "3", "6"])
+def test_report_concurrent_groups_side_streams(default_trace, monkeypatch, side):
+    # six policy groups at one workgroup per replica run concurrently (FGD on k_hmemo, run_mode 5; the cheap
+    # policies on k_scan1), each group's report right behind its replay on that group's stream, over one, three
+    # (the FGD group alone + two shared) or six side streams: every event's report and result equal the oracle's
+    monkeypatch.setenv("KSIM_SIDE_STREAMS", side)
+    keep = list(range(4, default_trace.num_nodes, 9))
+    arr, n = default_trace.typical()
+    cfgs = [(42 + i, name, pol, sel) for i, (name, pol, sel) in enumerate(POLICIES)]
+    eng = ksim.Engine(len(keep), len(cfgs), run_mode=5, wgs_per_replica=1)
+    rps = []
+    try:
+        eng.set_report(True)
+        for r, (seed, name, _, _) in enumerate(cfgs):
+            rp = default_trace.replay(seed=seed)
+            rps.append(rp)
+            eng.set_nodes(r, helpers.subset_nodes(rp, keep))
+            eng.set_typical(r, arr, n)
+            eng.set_policy(r, name, seed=seed)
+            eng.load_events(r, rp.events, 700)
+        eng.run()
+        got = [(eng.results(r), eng.reports(r)) for r in range(len(cfgs))]
+    finally:
+        eng.close()
+    for r, (seed, name, pol, sel) in enumerate(cfgs):
+        onodes = helpers.oracle_subset(default_trace, rps[r], keep)
+        want_res, _, want = O.run_events(onodes, helpers.oracle_typical(default_trace),
+                                         helpers.oracle_events(default_trace, rps[r], 700), policy=pol, gpu_sel=sel,
+                                         seed=seed, threads=16, with_report=True)
+        assert got[r][0] == want_res, name
+        assert_reports(got[r][1], want)
