@@ -73,6 +73,15 @@ KSIM_HD void store_node(NodeRec* p, const NodeV& n) {
   q[1] = make_uint4(n.g[2], n.g[3], n.meta, n.name_rank);
 }
 
+// tags[tag] += sign on a node's u16 tag counts in HBM without reading them back: one fire-and-forget atomic on
+// the u32 word holding the pair (a count stays within its half), so no load latency sits on the Bind's path.
+// For the tag counts no kernel reads during the run (every policy but GpuClustering, whose counts sit in LDS).
+__device__ __forceinline__ void tag_add(uint16_t* tags, int tag, int sign) {
+  unsigned* w = reinterpret_cast<unsigned*>(tags + (tag & ~1));
+  const unsigned one = 1u << (16 * (tag & 1));
+  atomicAdd(w, sign > 0 ? one : 0u - one);
+}
+
 // One event of one replica: 32 B.
 struct __align__(16) PodDev {
   int32_t cpu_req;   // Filter / Requested

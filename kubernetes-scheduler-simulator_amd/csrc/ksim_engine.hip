@@ -974,7 +974,7 @@ void k_replay(ksim_replay::ReplayArgs a,
             else if (lane < 6 && kTags)
               reinterpret_cast<uint2*>(&s_tags[(size_t)p_b * kTagStride])[lane - 2] =
                   reinterpret_cast<const uint2*>(&s_tags[(size_t)ns * kTagStride])[lane - 2];
-            else if (lane == 2 && !kTags && p_tag >= 0) g_tags[(size_t)p_b * kTagStride + p_tag] += 1;
+            else if (lane == 2 && !kTags && p_tag >= 0) tag_add(g_tags + (size_t)p_b * kTagStride, p_tag, +1);
             else if (lane == 6 && kFgd) s_F0[p_b] = s_F0[ns];
             else if (lane == 8 && kPF) { s_praw[p_b] = s_praw[ns]; s_pinf[p_b] = s_pinf[ns]; }
             else if (lane == 10 && pmon) pm_bump(p_b);
@@ -1047,10 +1047,13 @@ void k_replay(ksim_replay::ReplayArgs a,
       if (tid == 0) {
         const int2 h = (p.ref >= 0 && p.ref < step) ? hist[p.ref] : make_int2(-1, 0);
         if (h.x >= 0) {
-          const PodDev cp = rp.ev[p.ref];
+          PodDev cp = rp.ev[p.ref];
           const int loc = h.x - n_lo;
-          apply_bind(&s_nodes[loc], kTags ? &s_tags[(size_t)loc * kTagStride] : g_tags + (size_t)loc * kTagStride, cp,
-                     h.y - 1, -1);
+          if (!kTags && cp.tag >= 0) {  // the HBM counts: an atomic, not a read-modify-write
+            tag_add(g_tags + (size_t)loc * kTagStride, cp.tag, -1);
+            cp.tag = -1;
+          }
+          apply_bind(&s_nodes[loc], kTags ? &s_tags[(size_t)loc * kTagStride] : nullptr, cp, h.y - 1, -1);
           if (kFgd) s_F0[loc] = -1.0;
           if (kPwr || kPF) s_E0[loc] = kEnergyStale;
           if (pmon) pm_bump(loc);
@@ -1323,7 +1326,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         // the winner's slice
         const bool bind = pend && W != 0ull && !(p_st0 > 1 && p_st1);
         // 3. this step's A round totals
-        int gc, ge, gl, gh;
+        int gc = 0, ge = 0, gl = 0, gh = 0;
         if (a.K > 1) {
           ok = ok && collect_a(kstar, bind, &gc, &ge, &gl, &gh);
         } else {

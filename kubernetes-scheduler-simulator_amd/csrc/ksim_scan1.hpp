@@ -210,8 +210,8 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
                 s_last[loc] = step;
               }
               if (p.tag >= 0) {
-                uint16_t* t = kTags ? &s_tags[(size_t)loc * kTagStride] : rp.tags + (size_t)loc * kTagStride;
-                t[p.tag] = (uint16_t)(t[p.tag] + 1);
+                if (kTags) s_tags[(size_t)loc * kTagStride + p.tag] += 1;
+                else tag_add(rp.tags + (size_t)loc * kTagStride, p.tag, +1);  // HBM: an atomic, no read on the path
               }
             }
             out.node = loc;
