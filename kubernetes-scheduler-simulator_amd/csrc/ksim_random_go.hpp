@@ -14,16 +14,20 @@
 // oracle checks (fgd_oracle.c, orc_policy.go_stream).
 //
 // One 1024-thread workgroup per replica: thread t owns the contiguous node range [t*c, t*c+c) so a
-// block-wide exclusive scan of the per-thread feasible counts orders the feasible list by node
-// index; lane 0 of wave 0 owns the generator (vec[607] in LDS, tap / feed in registers) and makes
-// every draw; the owner of the pick finds it in its range; lane 0 reserves and binds.  The node
-// records sit in LDS when they fit (kLds), else in HBM (a workgroup reads its own stores after a
-// barrier).
+// block-wide exclusive scan of the per-thread feasible counts (ballots per count bit, then the 16
+// waves' totals) orders the feasible list by node index; lane 0 of wave 0 owns the generator
+// (vec[607] in LDS, tap / feed in registers) and makes every draw; the owner of the pick finds it in
+// its range; lane 0 reserves and binds.  The node records sit in LDS when they fit (kLds), else in
+// HBM (a workgroup reads its own stores after a barrier); the events come through a 128-event LDS
+// window, and the GpuClustering tag counts (HBM) take fire-and-forget atomics, so neither a load
+// of the next event nor a tag read-modify-write sits on the step's chain.  (r04: 256 threads were
+// slower, 41.7 against 38.5-38.9 ms at C2: five nodes per thread in the Filter and the pick's search.)
 #pragma once
 
 namespace ksim_random_go {
 
 constexpr int kBlock = 1024;
+constexpr int kEvWin = 128;  // events per LDS window
 constexpr int kLen = 607, kTap = 273;  // rng.go rngLen, rngTap
 constexpr int kStateWords = kLen + 2;  // vec, tap, feed (the host's upload layout)
 
@@ -36,10 +40,12 @@ struct RandGoArgs {
 
 struct GoShared {
   unsigned long long vec[kLen];
+  PodDev ev[kEvWin];
   int wsum[kBlock / 64];
   int pick;  // index in the feasible list (-1: none)
   int node;  // the picked node
 };
+
 
 inline size_t lds_bytes(int N, bool lds_nodes) {
   return ((sizeof(GoShared) + 15) & ~(size_t)15) + (lds_nodes ? sizeof(NodeRec) * (size_t)N : 0);
@@ -86,14 +92,25 @@ __global__ __launch_bounds__(kBlock) void k_random_go(RandGoArgs a) {
   __syncthreads();
 
   for (int step = 0; step < rp.n_events; ++step) {
-    const PodDev p = rp.ev[step];
+    const int eb = step & (kEvWin - 1);
+    if (eb == 0) {  // the next window of events (every thread passed the previous step's last barrier)
+      const int nl = min(kEvWin, rp.n_events - step) * 2;
+      const uint4* src = reinterpret_cast<const uint4*>(rp.ev + step);
+      for (int i = tid; i < nl; i += kBlock) reinterpret_cast<uint4*>(sh.ev)[i] = src[i];
+      __syncthreads();
+    }
+    const PodDev p = ksim_replay::uniform_pod(&sh.ev[eb]);
     if (p.flags & kPodDelete) {  // simulator.go:416-422 deletePod -> removePod: no draw
       if (tid == 0) {
         ResultDev out{-1, 0, 0, 0, ST_DELETED};
         if (p.ref >= 0 && p.ref < step) {
           const ResultDev cr = rp.res[p.ref];
           if (cr.node >= 0 && cr.status == ST_OK) {
-            apply_bind(&nodes[cr.node], rp.tags + (size_t)cr.node * kTagStride, rp.ev[p.ref], cr.gpu_mask, -1);
+            PodDev cp = rp.ev[p.ref];
+            const int tg = cp.tag;
+            cp.tag = -1;
+            apply_bind(&nodes[cr.node], nullptr, cp, cr.gpu_mask, -1);
+            if (tg >= 0) tag_add(rp.tags + (size_t)cr.node * kTagStride, tg, -1);
             if (rp.snap) {
               store_node(rp.snap + step, load_node(&nodes[cr.node]));
               rp.prev[step] = rp.last[cr.node];
@@ -111,13 +128,14 @@ __global__ __launch_bounds__(kBlock) void k_random_go(RandGoArgs a) {
     // Filter over this thread's range, then the block-wide exclusive scan of the counts
     int cnt = 0;
     for (int i = lo; i < hi; ++i) cnt += filter_node(load_node(&nodes[i]), p) ? 1 : 0;
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
+    // this lane's exclusive prefix within the wave and the wave's total, one ballot per bit of the count
+    int wexcl = 0, wtot = 0;
+    for (int k = 0; (1 << k) <= c; ++k) {
+      const unsigned long long m = __ballot((cnt >> k) & 1);
+      wexcl += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << k;
+      wtot += __popcll(m) << k;
     }
-    if (lane == 63) sh.wsum[wv] = incl;
+    if (lane == 0) sh.wsum[wv] = wtot;
     __syncthreads();
     int base = 0, total = 0;
 #pragma unroll
@@ -126,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void k_random_go(RandGoArgs a) {
       base += w < wv ? s : 0;
       total += s;
     }
-    const int excl = base + incl - cnt;
+    const int excl = base + wexcl;
     if (tid == 0) {
       (void)gen.int31n(sh.vec, 100);  // scheduler.go:464
       int pick = -1;
@@ -167,7 +185,10 @@ __global__ __launch_bounds__(kBlock) void k_random_go(RandGoArgs a) {
         } else {
           out.status = ST_OK;
           out.score = result_score(rp, total, 0, 0, 0);
-          apply_bind(nr, rp.tags + (size_t)node * kTagStride, p, mask, +1);
+          PodDev q = p;
+          q.tag = -1;
+          apply_bind(nr, nullptr, q, mask, +1);
+          if (p.tag >= 0) tag_add(rp.tags + (size_t)node * kTagStride, p.tag, +1);
           if (rp.snap) {
             store_node(rp.snap + step, load_node(nr));
             rp.prev[step] = rp.last[node];
