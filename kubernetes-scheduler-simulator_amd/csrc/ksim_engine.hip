@@ -1702,6 +1702,11 @@ struct ksim_engine {
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
   bool report_done = false;
+  // KSIM_GROUP_TIMES=1: timing events at the fork and at each used side stream's end (the last run's
+  // concurrent groups, printed on stderr after the run)
+  hipEvent_t tev_fork = nullptr;
+  hipEvent_t tev_side[kSide] = {};
+  unsigned tev_used = 0u;
   int last_pf_memo = 0;      // PWR+FGD memo class stride of the last k_replay<PWR+FGD> launch (0: none)  // run_persistent ran the report behind each concurrent group (last run)
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
@@ -2707,6 +2712,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
     if (e->side_ev[i]) (void)hipEventDestroy(e->side_ev[i]);
+    if (e->tev_side[i]) (void)hipEventDestroy(e->tev_side[i]);
   }
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
@@ -2716,6 +2722,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (size_t q = 0; q < e->peers.size(); ++q)
     if (e->peer_opened[q]) (void)hipIpcCloseMemHandle(e->peers[q]);
   if (e->d_pgran) (void)hipFree(e->d_pgran);
+  if (e->tev_fork) (void)hipEventDestroy(e->tev_fork);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e->mplan;
   delete e->hplan;
@@ -3475,6 +3482,11 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   if (concurrent) {
     if (!e->ev_fork) KSIM_HIP(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
     KSIM_HIP(hipEventRecord(e->ev_fork, e->stream));
+    const char* gt0 = std::getenv("KSIM_GROUP_TIMES");
+    if (gt0 && gt0[0] == '1') {
+      if (!e->tev_fork) KSIM_HIP(hipEventCreate(&e->tev_fork));
+      KSIM_HIP(hipEventRecord(e->tev_fork, e->stream));
+    }
   }
   for (const auto& gp : groups) {
     const int Rg = gp.second;
@@ -3486,10 +3498,16 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         // are dispatched ahead of the short groups' (measured within C4's run-to-run spread: off by default)
         const char* pr = std::getenv("KSIM_SIDE_PRIO");
         int lo = 0, hi = 0;
-        if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+        // KSIM_SIDE_CUMASK=1: every side stream with an all-CU mask, which gives it a hardware queue of its own
+        const char* cm = std::getenv("KSIM_SIDE_CUMASK");
+        if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
           KSIM_HIP(hipStreamCreateWithPriority(&e->side[i], hipStreamNonBlocking, hi));
-        else
+        } else if (cm && cm[0] == '1') {
+          std::vector<uint32_t> mask((size_t)(e->cus + 31) / 32, 0xffffffffu);
+          KSIM_HIP(hipExtStreamCreateWithCUMask(&e->side[i], (uint32_t)mask.size(), mask.data()));
+        } else {
           KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
+        }
         KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
       }
       gs = e->side[i];
@@ -3661,6 +3679,17 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     e->report_done = true;
   }
+  e->tev_used = 0u;
+  const char* gt = std::getenv("KSIM_GROUP_TIMES");
+  if (concurrent && gt && gt[0] == '1') {
+    if (!e->tev_fork) KSIM_HIP(hipEventCreate(&e->tev_fork));
+    for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
+      if (!(used & (1u << i))) continue;
+      if (!e->tev_side[i]) KSIM_HIP(hipEventCreate(&e->tev_side[i]));
+      KSIM_HIP(hipEventRecord(e->tev_side[i], e->side[i]));
+    }
+    e->tev_used = used;
+  }
   if (concurrent)  // join: the engine stream waits for every side stream used
     for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
       if (!(used & (1u << i))) continue;
@@ -3718,6 +3747,15 @@ int ksim_engine_run(ksim_engine* e) {
   KSIM_HIP(hipEventElapsedTime(&rms, e->ev_mid, e->ev1));
   e->last_ms = ms;
   e->last_report_ms = e->report ? rms : 0.0;
+  if (e->tev_used) {  // KSIM_GROUP_TIMES=1
+    std::fprintf(stderr, "ksim group times (ms from the fork to each side stream's end):");
+    for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
+      float gms = 0.f;
+      if ((e->tev_used >> i) & 1u && hipEventElapsedTime(&gms, e->tev_fork, e->tev_side[i]) == hipSuccess)
+        std::fprintf(stderr, " side%d %.3f;", i, gms);
+    }
+    std::fprintf(stderr, " run %.3f\n", ms);
+  }
   e->last_steps = max_ev;
   e->last_step_path = step_path;
   if (!step_path && e->shard_world == 0) {
