@@ -294,9 +294,10 @@ int  ksim_engine_get_reports(ksim_engine* e, int replica, ksim_report* out, int 
 /* The per-event power report of a replica with an energy model (ksim_engine_set_power_model, any
  * policy); KSIM_ESTATE without one or while the report is disabled. */
 int  ksim_engine_get_power_reports(ksim_engine* e, int replica, ksim_power_report* out, int n);
-/* Device time of the report kernels of the last run that follows the whole replay (ms; part of
- * last_run_ms).  Near 0 when the replay ran as concurrent groups: each group's report then runs on
- * the group's stream right behind its replay, overlapping the groups still running. */
+/* Device time of the report kernels of the last run (ms).  After a sequential replay: the report that
+ * follows it (part of last_run_ms).  After concurrent groups: the sum over groups of each group's report
+ * kernels, which run on the group's stream right behind its replay and overlap the groups still running
+ * (so the sum can exceed the report's share of last_run_ms). */
 int  ksim_engine_last_report_ms(ksim_engine* e, double* ms);
 
 /* Node-sharded single cluster (SURVEY §8(e), C5 across GPUs).  One engine (R = 1) per shard holds
@@ -348,6 +349,10 @@ int  ksim_engine_time_steps(ksim_engine* e, int n_steps, double* mean_kernel_us)
 int  ksim_engine_last_run_ms(ksim_engine* e, double* ms);
 /* Steps executed by the last run (max events over replicas). */
 int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
+/* Persistent replay launches of the last run (one per kernel group: FGD's k_memo / k_hmemo, the cheap
+ * policies' k_scan1_mix or one k_scan1 / k_replay per policy, k_random_go) and the side streams they ran
+ * on concurrently (0: back to back on the engine stream).  Introspection for the tests and the bench. */
+int  ksim_engine_last_run_launches(ksim_engine* e, int* launches, int* side_streams);
 /* Workgroups per replica used by the last run. */
 int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 /* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),

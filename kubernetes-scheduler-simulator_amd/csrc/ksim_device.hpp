@@ -155,6 +155,7 @@ struct ReplicaDev {
   int32_t w_pwr, w_fgd;
   int32_t has_pw;        // an energy model was given: the cluster report adds the [Power] terms
   int32_t pad_pw;
+  const int32_t* mcap;   // [N] allocatable memory, MiB (the Unreserve guard)
 };
 
 // Per-event cluster report, exact (fixed point 2^-80 for the fp64 terms; see fix80).
@@ -785,6 +786,17 @@ KSIM_HD int clustering_score(const uint16_t* tags, int pod_tag, int total) {
   for (int k = 0; k < kNumTags; ++k) distinct += tags[k] > 0 ? 1 : 0;
   const int base = (100 / 4) * (kMaxSpecGpu - total) / kMaxSpecGpu;
   if (tags[pod_tag] > 0) return distinct == 1 ? base + 100 * 3 / 4 : base + 100 * 2 / 4;
+  return distinct == 0 ? base + 100 / 4 : base;
+}
+
+// clustering_score on a node whose non-zero tag counts are the bits of `m` (bit k: tags[k] > 0): the
+// score reads nothing else of the counts, so on a create-only stream (counts only grow) a presence mask
+// per node is all a scan needs (k_scan1)
+KSIM_HD int clustering_score_mask(unsigned m, int pod_tag, int total) {
+  if (pod_tag < 0) return 0;
+  const int distinct = __builtin_popcount(m & ((1u << kNumTags) - 1u));
+  const int base = (100 / 4) * (kMaxSpecGpu - total) / kMaxSpecGpu;
+  if ((m >> pod_tag) & 1u) return distinct == 1 ? base + 100 * 3 / 4 : base + 100 * 2 / 4;
   return distinct == 0 ? base + 100 / 4 : base;
 }
 

@@ -40,6 +40,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <chrono>
+#include <thread>
 
 #include "ksim_device.hpp"
 #include "ksim_engine.h"
@@ -1512,12 +1514,14 @@ __global__ __launch_bounds__(64) void k_reserve(ReplicaDev* reps, const TypDev* 
   NodeRec* nr = rp.nodes + node;
   uint16_t* tg = rp.tags + (size_t)node * kTagStride;
   if (sign < 0) {
-    // removePod (cache.go:96-111): every released device gets its milli back without exceeding the
-    // device (left + milli <= 1000, the invariant of the packed u16 lanes) and the CPU stays within
-    // the node's allocatable; else nothing changes (e.g. a second Unreserve of the same pod)
+    // removePod (cache.go:100-111, deviceinfo.go:39-60): every released device gets its milli back
+    // without exceeding the device (left + milli <= 1000, the invariant of the packed u16 lanes), and
+    // the CPU and memory stay within the node's allocatable; else nothing changes (e.g. a second
+    // Unreserve of the same pod on a node still hosting another one)
     if (tid == 0) {
       const NodeV n = load_node(nr);
-      bool ok = n.pods_left() < 32767 && (long long)n.cpu_left + p.cpu_req <= (long long)rp.cap[node];
+      bool ok = n.pods_left() < 32767 && (long long)n.cpu_left + p.cpu_req <= (long long)rp.cap[node] &&
+                (long long)n.mem_left + p.mem <= (long long)rp.mcap[node];
       for (int g = 0; g < kMaxGpu; ++g)
         if ((mask_in >> g) & 1) ok = ok && g < n.gpu_cnt() && n.gl(g) + (int)p.milli <= kMilli;
       if (ok) apply_bind(nr, tg, p, mask_in, -1);
@@ -1683,6 +1687,9 @@ struct ksim_engine {
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
+  int last_launches = 0, last_streams = 0;  // replay launches of the last run, side streams they ran on (0: none)
+  std::vector<hipEvent_t> grp_rev;  // concurrent groups' report kernels: a timing event pair per group
+  int grp_rev_used = 0;             // pairs recorded by the last run
   int scan1 = 2;       // single-workgroup cheap-policy groups on k_scan1, node records in VGPRs where they fit
                        // (KSIM_SCAN1=1: records in LDS; 0: k_replay)
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
@@ -1699,6 +1706,11 @@ struct ksim_engine {
   // side streams for concurrent single-workgroup k_replay groups (created on first use)
   static constexpr int kSide = 6;
   hipStream_t side[kSide] = {};
+  int side_key[kSide] = {};
+  int* h_started = nullptr;   // residency gate: host-mapped flags, one per FGD workgroup (hipHostMalloc)
+  int* d_started = nullptr;   // its device address
+  int started_cap = 0, gate_epoch = 0;   // how each side stream was created (plain 0, all-CU mask -1, CU range [0, k) k, complement -k)
+  int dev_cus = 256;          // the device's CUs (CU masks cover them all, whatever KSIM_CUS caps)
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
   bool report_done = false;
@@ -1712,6 +1724,7 @@ struct ksim_engine {
   // cluster report (ksim_engine_set_report)
   bool report = false;
   int32_t* d_cap = nullptr;   // [R][N] allocatable milli-CPU
+  int32_t* d_mcap = nullptr;  // [R][N] allocatable memory, MiB (Unreserve's removePod guard)
   int32_t* d_last = nullptr;  // [R][N] k_step: last event that changed each node
   std::vector<NodeRec*> d_snap;
   std::vector<int32_t*> d_prev;
@@ -2397,6 +2410,7 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   using namespace ksim_hmemo;
   const HPlan& pl = *e->hplan;
   HMemoArgs ma;
+  std::memset(&ma, 0, sizeof ma);  // every field a caller does not set (the gate, profile, exchange pointers) is null
   ma.reps = e->d_reps;
   ma.rep_list = e->d_replist + first;
   ma.N = e->N;
@@ -2448,13 +2462,16 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   return ma;
 }
 
-static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st) {
+static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st, int* started = nullptr,
+                        int gate_epoch = 0) {
   using namespace ksim_hmemo;
   const HPlan& pl = *e->hplan;
   const int stride = std::max(max_ev, 1);
   int irc = hmemo_init_keys(e, Rg, first, st, 0);
   if (irc) return irc;
   HMemoArgs ma = hmemo_args(e, first, stride);
+  ma.started = pl.K == 1 ? started : nullptr;
+  ma.gate_epoch = gate_epoch;
   bool any_delete = false;
   for (const int r : e->mplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
   if (pl.K > 1) {
@@ -2593,6 +2610,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     hipDeviceProp_t prop;
     KSIM_HIP(hipGetDeviceProperties(&prop, dev));
     e->cus = prop.multiProcessorCount;
+    e->dev_cus = prop.multiProcessorCount;
     // KSIM_CUS: use at most this many CUs for co-resident persistent grids (a device shared with
     // another process; also the tests' way to exercise the residency checks)
     if (const char* c = std::getenv("KSIM_CUS")) e->cus = std::max(1, std::min(e->cus, std::atoi(c)));
@@ -2629,6 +2647,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   KSIM_HIP(hipMalloc(&e->d_fail, sizeof(int)));
   KSIM_HIP(hipMalloc(&e->d_replist, sizeof(int) * (size_t)n_replicas));
   KSIM_HIP(hipMalloc(&e->d_cap, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMalloc(&e->d_mcap, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMalloc(&e->d_pw, sizeof(PowerDev) * (size_t)n_replicas));
   KSIM_HIP(hipMalloc(&e->d_cpum, (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMalloc(&e->d_pws, sizeof(int2) * (size_t)n_nodes * n_replicas));
@@ -2637,6 +2656,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->pw_set.assign(n_replicas, 0);
   KSIM_HIP(hipMalloc(&e->d_last, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMemset(e->d_cap, 0, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
+  KSIM_HIP(hipMemset(e->d_mcap, 0, sizeof(int32_t) * (size_t)n_nodes * n_replicas));
   KSIM_HIP(hipMemset(e->d_tags, 0, sizeof(uint16_t) * e->tags_stride * n_replicas));
   std::vector<Accum> acc(n_replicas);
   for (auto& a : acc) {
@@ -2670,6 +2690,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     rp.nodes = e->d_nodes + (size_t)r * n_nodes;
     rp.tags = e->d_tags + (size_t)r * e->tags_stride;
     rp.cap = e->d_cap + (size_t)r * n_nodes;
+    rp.mcap = e->d_mcap + (size_t)r * n_nodes;
     rp.init = e->d_nodes_init + (size_t)r * n_nodes;
     rp.last = e->d_last + (size_t)r * n_nodes;
     rp.pw = e->d_pw + r;
@@ -2703,7 +2724,7 @@ void ksim_engine_destroy(ksim_engine* e) {
   for (auto p : e->d_rep) (void)hipFree(p);
   void* bufs[] = {e->d_nodes, e->d_tags, e->d_nodes_init, e->d_tags_init, e->d_tp, e->d_acc, e->d_reps, e->d_base, e->d_scratch,
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
-                  e->d_cap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
+                  e->d_cap, e->d_mcap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
@@ -2723,6 +2744,8 @@ void ksim_engine_destroy(ksim_engine* e) {
     if (e->peer_opened[q]) (void)hipIpcCloseMemHandle(e->peers[q]);
   if (e->d_pgran) (void)hipFree(e->d_pgran);
   if (e->tev_fork) (void)hipEventDestroy(e->tev_fork);
+  for (hipEvent_t v : e->grp_rev) (void)hipEventDestroy(v);
+  if (e->h_started) (void)hipHostFree(e->h_started);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e->mplan;
   delete e->hplan;
@@ -2754,7 +2777,7 @@ static int to_pod_dev(const ksim_pod& s, PodDev* d) {
 int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
   if (!e || !nodes || replica < 0 || replica >= e->R) return KSIM_EINVAL;
   std::vector<NodeRec> h(e->N);
-  std::vector<int32_t> cap(e->N);
+  std::vector<int32_t> cap(e->N), mcap(e->N);
   std::vector<uint8_t> cpum(e->N);
   int64_t gpus = 0;
   std::vector<uint16_t> tags(e->tags_stride, 0);
@@ -2770,6 +2793,8 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
     if (lr >= (uint32_t)e->N || seen[lr]) return KSIM_EINVAL;
     if (s.cpu_alloc_milli < 0 || s.cpu_alloc_milli > 0x3fffffff) return KSIM_ERANGE;
     cap[i] = (int32_t)s.cpu_alloc_milli;
+    if (s.mem_alloc_mib < 0 || s.mem_alloc_mib > 0x3fffffff) return KSIM_ERANGE;
+    mcap[i] = (int32_t)s.mem_alloc_mib;
     if (s.cpu_model < 0 || s.cpu_model >= kMaxCpuModels) return KSIM_ERANGE;
     cpum[i] = (uint8_t)s.cpu_model;
     gpus += s.gpu_count;
@@ -2802,6 +2827,8 @@ int ksim_engine_set_nodes(ksim_engine* e, int replica, const ksim_node* nodes) {
   e->total_gpus[replica] = gpus;
   KSIM_HIP(hipSetDevice(e->device));
   KSIM_HIP(hipMemcpyAsync(e->d_cap + (size_t)replica * e->N, cap.data(), sizeof(int32_t) * e->N, hipMemcpyHostToDevice,
+                          e->stream));
+  KSIM_HIP(hipMemcpyAsync(e->d_mcap + (size_t)replica * e->N, mcap.data(), sizeof(int32_t) * e->N, hipMemcpyHostToDevice,
                           e->stream));
   KSIM_HIP(hipMemcpyAsync(e->d_cpum + (size_t)replica * e->N, cpum.data(), e->N, hipMemcpyHostToDevice, e->stream));
   KSIM_HIP(hipMemcpyAsync(e->reps[replica].nodes, h.data(), sizeof(NodeRec) * e->N, hipMemcpyHostToDevice, e->stream));
@@ -3436,8 +3463,6 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipStreamSynchronize(e->stream));  // h is a local
     }
   }
-  KSIM_HIP(hipMemcpyAsync(e->d_replist, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, e->stream));
-  KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
   bool any_delete = false;
   for (int r = 0; r < e->R; ++r) any_delete = any_delete || e->has_delete[r];
   const char* pe = std::getenv("KSIM_PROFILE");
@@ -3447,6 +3472,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   e->last_hmemo = 0;
   e->last_rgo = 0;
   e->last_scan1 = 0;
+  e->last_launches = (int)groups.size();
+  e->last_streams = 0;
   // Groups whose replicas each fit ONE workgroup (K = 1: no cross-workgroup exchange, so no
   // co-residency needed) run concurrently on side streams: a paper-sweep group fills 170 of 256 CUs,
   // the next group's workgroups take the rest.  Any group needing K > 1 (or a k_memo launch, or the
@@ -3469,6 +3496,43 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     concurrent = K == 1;
   }
+  // The cheap-policy groups a concurrent run would give one k_scan1 launch each become ONE k_scan1_mix
+  // launch (policy per workgroup), its replicas longest stream first: the run then needs one side stream
+  // beside the FGD group's, whatever the hardware-queue mapping of the process.
+  const bool reg1 = e->scan1 == 2 && e->N <= ksim_scan1::kBlock * ksim_scan1::kRegSlots;
+  const char* mixe = std::getenv("KSIM_SCAN1_MIX");
+  if (concurrent && !any_delete && e->scan1 && e->N <= kMaxSlice && !(mixe && mixe[0] == '0') &&
+      ksim_scan1::scan1_lds(e->N, ksim_scan1::kPolMix, e->report, reg1) <= 160 * 1024) {
+    std::vector<int> mix, norder;
+    std::vector<std::pair<int, int>> ngroups;
+    int f = 0, at = -1, nmix = 0;
+    for (const auto& gp : groups) {
+      bool m = gp.first >= POL_BESTFIT && gp.first <= POL_RANDOM;
+      for (int j = f; m && j < f + gp.second; ++j)
+        m = gp.first != POL_DOTPROD || e->reps[order[j]].dpcfg == (DIM_MERGE | NORM_MAX << 4);
+      if (m) {
+        mix.insert(mix.end(), order.begin() + f, order.begin() + f + gp.second);
+        if (at < 0) at = (int)ngroups.size();
+        ++nmix;
+      } else {
+        ngroups.push_back(gp);
+        norder.insert(norder.end(), order.begin() + f, order.begin() + f + gp.second);
+      }
+      f += gp.second;
+    }
+    if (nmix >= 2) {
+      std::stable_sort(mix.begin(), mix.end(), [&](int x, int y) { return e->n_events[x] > e->n_events[y]; });
+      int off = 0;
+      for (int g = 0; g < at; ++g) off += ngroups[g].second;
+      norder.insert(norder.begin() + off, mix.begin(), mix.end());
+      ngroups.insert(ngroups.begin() + at, {ksim_scan1::kPolMix, (int)mix.size()});
+      order.swap(norder);
+      groups.swap(ngroups);
+      e->last_launches = (int)groups.size();
+    }
+  }
+  KSIM_HIP(hipMemcpyAsync(e->d_replist, order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice, e->stream));
+  KSIM_HIP(hipMemsetAsync(e->d_fail, 0, sizeof(int), e->stream));
   int gidx = 0;
   // The side streams share the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4), and two
   // streams on one queue run their kernels one after the other.  So no more side streams than queues:
@@ -3488,27 +3552,42 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipEventRecord(e->tev_fork, e->stream));
     }
   }
+  // KSIM_SIDE_CUMASK (A/B): 1 = every side stream with an all-CU mask (a hardware queue of its own);
+  // 2 = the first group (FGD on k_hmemo, one workgroup per replica) on CUs [0, Rg), the other groups on
+  // the rest, so the long FGD replays start at once instead of waiting for CUs the short groups hold.
+  // CU-masked streams are blocking streams (they order with the null stream; nothing here uses it).
+  int cm_mode = 0, cm_split = 0;
+  if (const char* cm = std::getenv("KSIM_SIDE_CUMASK")) cm_mode = std::atoi(cm);
+  if (concurrent && cm_mode == 2 && groups.size() >= 2 && groups[0].first == POL_FGD && e->hplan_ok && e->run_mode != 2)
+    cm_split = std::max(1, std::min(groups[0].second, e->dev_cus - 32));
   for (const auto& gp : groups) {
     const int Rg = gp.second;
     hipStream_t gs = e->stream;
     if (concurrent) {
       const int i = (gidx == 0 || nq == 1) ? 0 : 1 + (gidx - 1) % (nq - 1);
+      const int key = cm_split > 0 ? (i == 0 ? cm_split : -cm_split) : (cm_mode == 1 ? -1 : 0);
+      if (e->side[i] && e->side_key[i] != key) {  // created for another mask: recreate
+        KSIM_HIP(hipStreamSynchronize(e->side[i]));
+        KSIM_HIP(hipStreamDestroy(e->side[i]));
+        e->side[i] = nullptr;
+      }
       if (!e->side[i]) {
         // KSIM_SIDE_PRIO=1: the first group's stream at the device's greatest priority, so that its workgroups
         // are dispatched ahead of the short groups' (measured within C4's run-to-run spread: off by default)
         const char* pr = std::getenv("KSIM_SIDE_PRIO");
         int lo = 0, hi = 0;
-        // KSIM_SIDE_CUMASK=1: every side stream with an all-CU mask, which gives it a hardware queue of its own
-        const char* cm = std::getenv("KSIM_SIDE_CUMASK");
-        if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
-          KSIM_HIP(hipStreamCreateWithPriority(&e->side[i], hipStreamNonBlocking, hi));
-        } else if (cm && cm[0] == '1') {
-          std::vector<uint32_t> mask((size_t)(e->cus + 31) / 32, 0xffffffffu);
+        if (key != 0) {
+          std::vector<uint32_t> mask((size_t)(e->dev_cus + 31) / 32, 0u);
+          for (int c = 0; c < e->dev_cus; ++c)
+            if (key == -1 || (key > 0 ? c < key : c >= -key)) mask[(size_t)c / 32] |= 1u << (c % 32);
           KSIM_HIP(hipExtStreamCreateWithCUMask(&e->side[i], (uint32_t)mask.size(), mask.data()));
+        } else if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
+          KSIM_HIP(hipStreamCreateWithPriority(&e->side[i], hipStreamNonBlocking, hi));
         } else {
           KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
         }
-        KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
+        e->side_key[i] = key;
+        if (!e->side_ev[i]) KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
       }
       gs = e->side[i];
       if (!(used & (1u << i))) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));
@@ -3532,6 +3611,21 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       first += Rg;
       continue;
     }
+    if (gp.first == ksim_scan1::kPolMix) {
+      const void* f = e->report ? (reg1 ? (const void*)ksim_scan1::k_scan1_mix<true, true> : (const void*)ksim_scan1::k_scan1_mix<true, false>)
+                                : (reg1 ? (const void*)ksim_scan1::k_scan1_mix<false, true> : (const void*)ksim_scan1::k_scan1_mix<false, false>);
+      const size_t lds = ksim_scan1::scan1_lds(e->N, ksim_scan1::kPolMix, e->report, reg1);
+      ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N,
+                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0};
+      KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      void* params[] = {(void*)&sa};
+      KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
+      e->last_K = 1;
+      e->last_groups = (int)groups.size();
+      e->last_scan1 += Rg;
+      first += Rg;
+      continue;
+    }
     // FGD: the memoised replay when the cluster and the classes fit (run_mode 0 / 3)
     if (gp.first == POL_FGD && e->run_mode != 2) {
       if (e->mplan_ok) {  // prepared by prepare_memo (the FGD replicas are the first group of `order`)
@@ -3547,8 +3641,32 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         continue;
       }
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
-        const int rc = launch_hmemo(e, Rg, first, max_ev, gs);
+        // The residency gate (concurrent groups behind a K = 1 FGD group; KSIM_C4_GATE=0 off): the long FGD
+        // replays take their CUs before any short group's workgroup is dispatched, so none of them waits
+        // for a CU that short replays hold.  The host waits for every workgroup's start flag (bounded: a
+        // gate that does not open in 2 s lets the launches go on, it orders work, it decides nothing).
+        const char* ge = std::getenv("KSIM_C4_GATE");
+        const bool gate = concurrent && gidx == 1 && groups.size() >= 2 && e->hplan->K == 1 && !(ge && ge[0] == '0');
+        if (gate && Rg > e->started_cap) {
+          if (e->h_started) KSIM_HIP(hipHostFree(e->h_started));
+          e->h_started = nullptr;
+          KSIM_HIP(hipHostMalloc((void**)&e->h_started, sizeof(int) * (size_t)Rg, hipHostMallocMapped | hipHostMallocCoherent));
+          std::memset(e->h_started, 0, sizeof(int) * (size_t)Rg);
+          KSIM_HIP(hipHostGetDevicePointer((void**)&e->d_started, e->h_started, 0));
+          e->started_cap = Rg;
+        }
+        const int epoch = gate ? (e->gate_epoch = (e->gate_epoch % 0x3fffffff) + 1) : 0;
+        const int rc = launch_hmemo(e, Rg, first, max_ev, gs, gate ? e->d_started : nullptr, epoch);
         if (rc) return rc;
+        if (gate) {
+          const auto t0 = std::chrono::steady_clock::now();
+          volatile int* fl = e->h_started;
+          for (int w = 0; w < Rg;) {
+            if (fl[w] == epoch) { ++w; continue; }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            std::this_thread::yield();
+          }
+        }
         e->last_K = e->hplan->K;
         e->last_groups = (int)groups.size();
         e->last_hmemo += Rg;
@@ -3561,7 +3679,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     int S = (e->N + K - 1) / K;
     const bool general = profile || e->report || any_delete;
     // one workgroup per replica, create-only, a cheap policy: the 256-thread k_scan1 (ksim_scan1.hpp)
-    const bool reg = e->scan1 == 2 && e->N <= ksim_scan1::kBlock * ksim_scan1::kRegSlots;
+    const bool reg = reg1;
     if (K == 1 && !profile && !any_delete && e->scan1 && e->N <= kMaxSlice && scan1_fn(gp.first, e->report, reg) &&
         ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg) <= 160 * 1024) {
       const void* f = scan1_fn(gp.first, e->report, reg);
@@ -3666,17 +3784,25 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   }
   if (concurrent && e->report) {
     // each group's report on its own stream, behind its replay: the groups that finish early report while
-    // the longest still runs
+    // the longest still runs; a timing event pair around each (last_report_ms sums them)
     int f = 0;
+    if (e->grp_rev.size() < 2 * groups.size()) {
+      const size_t had = e->grp_rev.size();
+      e->grp_rev.resize(2 * groups.size(), nullptr);
+      for (size_t q = had; q < e->grp_rev.size(); ++q) KSIM_HIP(hipEventCreate(&e->grp_rev[q]));
+    }
     for (size_t g = 0; g < groups.size(); ++g) {
       const int Rg = groups[g].second;
       const int i = (g == 0 || nq == 1) ? 0 : 1 + ((int)g - 1) % (nq - 1);
       int mev = 0;
       for (int j = f; j < f + Rg; ++j) mev = std::max(mev, e->n_events[order[j]]);
+      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g], e->side[i]));
       const int rc = run_report(e, mev, e->side[i], e->d_replist + f, Rg);
       if (rc) return rc;
+      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g + 1], e->side[i]));
       f += Rg;
     }
+    e->grp_rev_used = (int)groups.size();
     e->report_done = true;
   }
   e->tev_used = 0u;
@@ -3690,6 +3816,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     e->tev_used = used;
   }
+  e->last_streams = __builtin_popcount(used);
   if (concurrent)  // join: the engine stream waits for every side stream used
     for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
       if (!(used & (1u << i))) continue;
@@ -3717,6 +3844,10 @@ int ksim_engine_run(ksim_engine* e) {
   }
   KSIM_HIP(hipSetDevice(e->device));
   e->report_done = false;
+  e->grp_rev_used = 0;
+  e->tev_used = 0u;  // KSIM_GROUP_TIMES: only run_persistent's concurrent groups record side-stream ends
+  e->last_launches = 0;
+  e->last_streams = 0;
   int rc = prepare_memo(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
@@ -3747,6 +3878,11 @@ int ksim_engine_run(ksim_engine* e) {
   KSIM_HIP(hipEventElapsedTime(&rms, e->ev_mid, e->ev1));
   e->last_ms = ms;
   e->last_report_ms = e->report ? rms : 0.0;
+  for (int g = 0; g < e->grp_rev_used; ++g) {  // concurrent groups: each group's report on its side stream
+    float gms = 0.f;
+    KSIM_HIP(hipEventElapsedTime(&gms, e->grp_rev[2 * g], e->grp_rev[2 * g + 1]));
+    e->last_report_ms += gms;
+  }
   if (e->tev_used) {  // KSIM_GROUP_TIMES=1
     std::fprintf(stderr, "ksim group times (ms from the fork to each side stream's end):");
     for (int i = 0; i < (int)ksim_engine::kSide; ++i) {
@@ -4213,6 +4349,13 @@ int ksim_engine_get_power_reports(ksim_engine* e, int replica, ksim_power_report
 int ksim_engine_last_report_ms(ksim_engine* e, double* ms) {
   if (!e || !ms) return KSIM_EINVAL;
   *ms = e->last_report_ms;
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_launches(ksim_engine* e, int* launches, int* side_streams) {
+  if (!e || !launches || !side_streams) return KSIM_EINVAL;
+  *launches = e->last_launches;
+  *side_streams = e->last_streams;
   return KSIM_OK;
 }
 

@@ -113,6 +113,11 @@ struct HMemoArgs {
                             // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
   int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
   int fw_big;               // F waves of a replica with more than 64 typical pods (KSIM_HFW; kFW by default)
+  // Residency gate (a concurrent run's FGD group): each workgroup stores `gate_epoch` into started[its
+  // index] (host memory) as it starts, so the host launches the short groups only once every long replay
+  // holds its CU.  Null: no gate.
+  int* started;
+  int gate_epoch;
 };
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
@@ -999,6 +1004,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
 
 template <int kSub, bool kProf>
 __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
+  if (a.started != nullptr && threadIdx.x == 0)  // a vector store to host memory, system scope
+    __hip_atomic_store(a.started + blockIdx.x, a.gate_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   hmemo_body<kSub, kProf>(a, tp_all, (int)blockIdx.x);
 }
 

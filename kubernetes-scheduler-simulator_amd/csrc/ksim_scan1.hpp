@@ -14,6 +14,13 @@
 //     packed keys, the single-feasible shortcut, the Score-error abort: k_replay's commit);
 //   - the wave whose threads scan the winner's slot runs Reserve's GPU selector and the Bind on it
 //     and reports; slot s is only ever read by thread s % 256, so the Bind needs no second barrier.
+// GpuClustering keeps one presence bit per affinity tag and node (u16 in LDS) instead of the tag counts:
+// on a create-only stream a count only grows, and the score reads only which counts are non-zero
+// (clustering_score_mask); the counts themselves change in HBM by fire-and-forget atomics, as for the
+// other policies.
+// k_scan1_mix<kReport, kReg> runs replicas of all five policies in ONE launch (the policy is chosen per
+// workgroup, DotProduct in the paper's merge / max configuration only): the paper sweep's cheap groups
+// then need one stream beside the FGD group's instead of five (streams and queues).
 // Create-only streams without a profile (the host takes k_replay for anything else); with the
 // per-event cluster report (kReport) the Bind also records the node's new record and the previous
 // event that changed it (snap / prev, ksim_report.hpp), as k_replay's general form does.  Same
@@ -52,11 +59,13 @@ struct __align__(16) Scan1Shared {
 };
 static_assert(sizeof(Scan1Shared) % 16 == 0, "keep the node records 16-B aligned");
 
-// Dynamic LDS: Scan1Shared | NodeRec nodes[N] (not with kReg) | u16 tags[N][16] (GpuClustering) |
-// i32 last[N] (report)
+// Dynamic LDS: Scan1Shared | NodeRec nodes[N] (not with kReg) | u16 tag presence[N] rounded up to 16 B
+// (GpuClustering, and every k_scan1_mix launch) | i32 last[N] (report)
+constexpr int kPolMix = 65;  // scan1_lds's policy id of a k_scan1_mix launch (the presence bits always present)
+__host__ __device__ inline size_t scan1_tm_bytes(int N) { return ((size_t)N * sizeof(uint16_t) + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t scan1_lds(int N, int pol, bool report, bool reg = false) {
   return sizeof(Scan1Shared) + (reg ? 0 : (size_t)N * sizeof(NodeRec)) +
-         (pol == POL_CLUSTERING ? (size_t)N * kTagStride * sizeof(uint16_t) : 0) + (report ? (size_t)N * 4 : 0);
+         (pol == POL_CLUSTERING || pol == kPolMix ? scan1_tm_bytes(N) : 0) + (report ? (size_t)N * 4 : 0);
 }
 
 // x = c ? y : x field by field (a select of whole structs would take the array's address)
@@ -71,18 +80,19 @@ __device__ __forceinline__ void sel_node(NodeV& x, const NodeV& y, bool c) {
 
 // kReg: thread t keeps the records of its slots t + 256 k (k < kRegSlots) in VGPRs instead of LDS, so
 // a workgroup needs only a few KB of LDS and a CU holds as many replicas as its registers allow.
-template <int kPol, bool kReport, bool kReg>
-__global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
+// kDpMM: DotProduct in the merge / max configuration only (k_scan1_mix): the closed form, and the
+// DotProduct selector's group mask is the merge method's "" (0).  kLdsPol: the policy id the launch's
+// LDS layout was sized for (kPol, or kPolMix).
+template <int kPol, bool kReport, bool kReg, bool kDpMM = false, int kLdsPol = kPol>
+__device__ __forceinline__ void scan1_body(const Scan1Args& a, const ReplicaDev& rp, char* smem) {
   using namespace ksim_replay;
-  constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
+  constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag presence per pod step
   constexpr bool kMinMax = kPol == POL_BESTFIT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   Scan1Shared& sh = *reinterpret_cast<Scan1Shared*>(smem);
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(Scan1Shared));
-  uint16_t* s_tags = reinterpret_cast<uint16_t*>(smem + sizeof(Scan1Shared) + (kReg ? 0 : (size_t)a.N * sizeof(NodeRec)));
-  int* s_last = reinterpret_cast<int*>(smem + scan1_lds(a.N, kPol, false, kReg));  // report: last event per slot
+  uint16_t* s_tm = reinterpret_cast<uint16_t*>(smem + sizeof(Scan1Shared) + (kReg ? 0 : (size_t)a.N * sizeof(NodeRec)));
+  int* s_last = reinterpret_cast<int*>(smem + scan1_lds(a.N, kLdsPol, false, kReg));  // report: last event per slot
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
   const int N = a.N;
   NodeV rn[kReg ? kRegSlots : 1];  // kReg: the records of slots tid + 256 k
   if (kReg) {
@@ -95,7 +105,12 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     for (int i = tid; i < N; i += kBlock) store_node(&s_nodes[i], load_node(rp.nodes + i));
   }
   if (kTags)
-    for (int i = tid; i < N * kTagStride; i += kBlock) s_tags[i] = rp.tags[i];
+    for (int i = tid; i < N; i += kBlock) {
+      unsigned m = 0u;
+#pragma unroll
+      for (int k = 0; k < kNumTags; ++k) m |= rp.tags[(size_t)i * kTagStride + k] > 0 ? 1u << k : 0u;
+      s_tm[i] = (uint16_t)m;
+    }
   if (kReport)
     for (int i = tid; i < N; i += kBlock) s_last[i] = -1;
   for (int i = tid; i < kWaves * kDeadWords; i += kBlock) (&sh.dead[0][0])[i] = 0u;
@@ -128,9 +143,16 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
     auto visit = [&](const NodeV& n, int i) {
       if (filter_node(n, p)) {
         bool e1 = false;
-        const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[i] : 0;
-        const int raw = cheap_score<kPol>(n, p, rp.seed, kTags ? &s_tags[(size_t)i * kTagStride] : nullptr, step, &e1,
-                                          rp.dpcfg, cap);
+        int raw;
+        if constexpr (kTags) {
+          e1 = p.tag == -2;
+          raw = e1 ? 0 : clustering_score_mask(s_tm[i], p.tag, n.total());
+        } else if constexpr (kPol == POL_DOTPROD && kDpMM) {
+          raw = dotprod_merge_max(n, p);
+        } else {
+          const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[i] : 0;
+          raw = cheap_score<kPol>(n, p, rp.seed, nullptr, step, &e1, rp.dpcfg, cap);
+        }
         const unsigned long long k = pack_key((unsigned)raw, n.name_rank, -1, i);
         best = k > best ? k : best;
         ++cnt;
@@ -188,8 +210,9 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
           } else {
             bn = uniform_node(&s_nodes[loc]);
           }
-          const int mask = select_gpus(bn, p, rp.gpusel, sel_arg<kPol == POL_DOTPROD>(rp, bn, p, loc, key_gpu(W)),
-                                       rp.seed, step);
+          const int sarg = (kPol == POL_DOTPROD && kDpMM) ? (rp.gpusel == SEL_DOTPROD ? 0 : key_gpu(W))
+                                                          : sel_arg<kPol == POL_DOTPROD>(rp, bn, p, loc, key_gpu(W));
+          const int mask = select_gpus(bn, p, rp.gpusel, sarg, rp.seed, step);
           if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
             out.status = ST_ERROR;
             out.score = 0;
@@ -210,8 +233,8 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
                 s_last[loc] = step;
               }
               if (p.tag >= 0) {
-                if (kTags) s_tags[(size_t)loc * kTagStride + p.tag] += 1;
-                else tag_add(rp.tags + (size_t)loc * kTagStride, p.tag, +1);  // HBM: an atomic, no read on the path
+                if (kTags) s_tm[loc] |= (uint16_t)(1u << p.tag);
+                tag_add(rp.tags + (size_t)loc * kTagStride, p.tag, +1);  // HBM: an atomic, no read on the path
               }
             }
             out.node = loc;
@@ -230,8 +253,29 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
   } else {
     for (int i = tid; i < N; i += kBlock) store_node(rp.nodes + i, load_node(&s_nodes[i]));
   }
-  if (kTags)
-    for (int i = tid; i < N * kTagStride; i += kBlock) rp.tags[i] = s_tags[i];
+}
+
+template <int kPol, bool kReport, bool kReg>
+__global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
+  scan1_body<kPol, kReport, kReg>(a, rp, smem);
+}
+
+// Every cheap policy in one launch: workgroup b replays replica rep_list[b] under that replica's policy
+// (a uniform branch per workgroup).  The host lists the replicas longest stream first, so the launch
+// dispatches the long replays before the short ones fill in behind them.
+template <bool kReport, bool kReg>
+__global__ __launch_bounds__(kBlock) void k_scan1_mix(Scan1Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
+  switch (rp.policy) {
+    case POL_BESTFIT: scan1_body<POL_BESTFIT, kReport, kReg, false, kPolMix>(a, rp, smem); break;
+    case POL_DOTPROD: scan1_body<POL_DOTPROD, kReport, kReg, true, kPolMix>(a, rp, smem); break;
+    case POL_PACKING: scan1_body<POL_PACKING, kReport, kReg, false, kPolMix>(a, rp, smem); break;
+    case POL_CLUSTERING: scan1_body<POL_CLUSTERING, kReport, kReg, false, kPolMix>(a, rp, smem); break;
+    default: scan1_body<POL_RANDOM, kReport, kReg, false, kPolMix>(a, rp, smem); break;
+  }
 }
 
 }  // namespace ksim_scan1

@@ -163,6 +163,7 @@ SIGNATURES = {
     "ksim_engine_last_run_ms": (C.c_int, [_VP, _P(C.c_double)]),
     "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
     "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
+    "ksim_engine_last_run_launches": (C.c_int, [_VP, _P(C.c_int), _P(C.c_int)]),
     "ksim_engine_last_run_path": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
     "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
@@ -655,6 +656,12 @@ class Engine:
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
         return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1"][k.value]
+
+    def last_run_launches(self):
+        """(replay launches, side streams they ran on concurrently; 0 = back to back) of the last run()."""
+        n, s = C.c_int(0), C.c_int(0)
+        check(lib().ksim_engine_last_run_launches(self.h, C.byref(n), C.byref(s)), "last_run_launches")
+        return n.value, s.value
 
     def last_run_wgs(self):
         k = C.c_int(0)

@@ -295,8 +295,17 @@ def get_typical_pods(workload, threshold=95, step=1, involve_cpu=True, gpu_res_w
 
 # Replays already made in this process (the GPU suite checks several kernels against the same reference
 # replay: a full openb trace takes the oracle seconds), keyed by a digest of every input that decides the
-# result; the worker-thread count does not.  KSIM_ORACLE_CACHE=0 turns it off.
+# result; the worker-thread count does not.  KSIM_ORACLE_CACHE=0 turns it off.  The oracle's global
+# state also decides a replay (a census records deltas as it runs, set_exp_mode / set_exp_nudge change
+# math.Exp), so no replay is cached or served from the cache while any of it is away from the default
+# (ADVICE r4): _ORACLE_STATE mirrors what the setters below last set.
 _RUN_CACHE = {}
+_ORACLE_STATE = {"census": False, "exp_mode": 0, "exp_nudge": 0}
+
+
+def _cache_ok():
+    return (os.environ.get("KSIM_ORACLE_CACHE", "1") != "0" and not _ORACLE_STATE["census"]
+            and _ORACLE_STATE["exp_mode"] == 0 and _ORACLE_STATE["exp_nudge"] == 0)
 
 
 def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, seed=0, threads=1,
@@ -307,7 +316,7 @@ def run_events(nodes, typical_list, events, policy=POL_FGD, gpu_sel=SEL_FGD, see
     import copy
     import hashlib
     key = None
-    if go_stream is None and os.environ.get("KSIM_ORACLE_CACHE", "1") != "0":
+    if go_stream is None and _cache_ok():
         key = hashlib.sha256(repr((nodes, typical_list, events, policy, gpu_sel, seed, with_report, w_pwr, w_fgd,
                                    dim_ext, norm)).encode()).hexdigest()
         if key in _RUN_CACHE:
@@ -375,6 +384,7 @@ def score_thresholds():
 def census_begin():
     """Start the math.Exp census: every FGD score delta is compared with score_thresholds()."""
     assert lib().orc_census_begin() == 0
+    _ORACLE_STATE["census"] = True
 
 
 class CensusCase(C.Structure):
@@ -385,6 +395,7 @@ class CensusCase(C.Structure):
 def set_exp_nudge(ulps):
     """Move every math.Exp result of the oracle by `ulps` ulps (census runs; 0 restores it)."""
     lib().orc_set_exp_nudge(ulps)
+    _ORACLE_STATE["exp_nudge"] = int(ulps)
 
 
 def census_end():
@@ -393,6 +404,7 @@ def census_end():
     st, nd, k = C.c_int(0), C.c_int(0), C.c_int(0)
     n = C.c_longlong(0)
     lib().orc_census_end(C.byref(d), C.byref(x), C.byref(st), C.byref(nd), C.byref(k), C.byref(n), None)
+    _ORACLE_STATE["census"] = False
     near, crd, sens = C.c_longlong(0), C.c_longlong(0), C.c_longlong(0)
     cr_cases, sens_cases = (CensusCase * 16)(), (CensusCase * 16)()
     smax = C.c_double(0)
@@ -410,3 +422,4 @@ def set_exp_mode(mode):
     """0: the portable Go algorithm (the product's); 1: exp in x87 extended precision rounded to
     double, a stand-in for a correctly rounded exp (census runs only)."""
     lib().orc_set_exp_mode(mode)
+    _ORACLE_STATE["exp_mode"] = int(mode)

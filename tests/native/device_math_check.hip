@@ -168,6 +168,14 @@ int dm_clustering(const int* tags9, const int* gl8, int gpu_cnt, int milli, int 
   const PodDev p = pod(1000, milli, num, ~0u);
   return clustering_score(t, p.tag, n.total());
 }
+// k_scan1's form: the presence bits of the same counts (clustering_score_mask)
+int dm_clustering_mask(const int* tags9, const int* gl8, int gpu_cnt, int milli, int num) {
+  unsigned m = 0u;
+  for (int k = 0; k < 9; ++k) m |= tags9[k] > 0 ? 1u << k : 0u;
+  const NodeV n = mk(64000, 0, gl8, gpu_cnt, 0, 1);
+  const PodDev p = pod(1000, milli, num, ~0u);
+  return clustering_score_mask(m, p.tag, n.total());
+}
 int dm_exclusive(const int* gl8, int gpu_cnt, int milli, int num) {
   return exclusive_gpu_mask(mk(0, 0, gl8, gpu_cnt, 0, 1), pod(0, milli, num, ~0u));
 }

@@ -38,6 +38,7 @@ def dm():
     L.dm_go_tanh.restype = C.c_double
     L.dm_packing.argtypes = [I8, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
     L.dm_clustering.argtypes = [C.c_int * 9, I8, C.c_int, C.c_int, C.c_int]
+    L.dm_clustering_mask.argtypes = [C.c_int * 9, I8, C.c_int, C.c_int, C.c_int]
     L.dm_exclusive.argtypes = [I8, C.c_int, C.c_int, C.c_int]
     L.dm_frag_bins7.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double),
                                 C.c_double * 7]
@@ -142,6 +143,7 @@ def test_cheap_scores_and_exclusive_fuzz(dm):
         tag = -1 if num == 0 else (0 if (num == 1 and milli < 1000) else num)
         want = L.orc_clustering_score(C.byref(node), C.byref(pr), tag, (C.c_int32 * 9)(*tags))
         assert dm.dm_clustering((C.c_int * 9)(*tags), g8, cnt, milli, num) == want
+        assert dm.dm_clustering_mask((C.c_int * 9)(*tags), g8, cnt, milli, num) == want  # k_scan1's presence bits
 
 
 def test_frag_bins7_fuzz(dm, tables):

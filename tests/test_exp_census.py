@@ -72,3 +72,34 @@ def test_prefix_census_live(census):
     finally:
         O.set_exp_mode(0)
     assert cr == base
+
+
+def test_replay_cache_steps_aside_for_oracle_state(monkeypatch):
+    # a replay under a census, a nudged exp or the correctly rounded exp must run, never come
+    # from the cache a default-state replay of the same arguments filled
+    t = ksim.Trace.openb("default")
+    rp = t.replay(seed=43, tune_ratio=1.3, shuffle=True)
+    args = (helpers.oracle_nodes(t, rp)[:40], helpers.oracle_typical(t), helpers.oracle_events(t, rp, 60))
+    calls = []
+    real = O._run_events
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    monkeypatch.setattr(O, "_run_events", counting)
+    monkeypatch.setenv("KSIM_ORACLE_CACHE", "1")
+    base = O.run_events(*args)
+    n0 = len(calls)
+    assert O.run_events(*args) == base and len(calls) == n0          # default state: served from the cache
+    for enter, leave in ((lambda: O.set_exp_mode(1), lambda: O.set_exp_mode(0)),
+                         (lambda: O.set_exp_nudge(1), lambda: O.set_exp_nudge(0)),
+                         (O.census_begin, O.census_end)):
+        enter()
+        try:
+            before = len(calls)
+            O.run_events(*args)
+            assert len(calls) == before + 1
+        finally:
+            leave()
+    before = len(calls)
+    assert O.run_events(*args) == base and len(calls) == before      # back to the default: cached again

@@ -243,15 +243,47 @@ def test_reserve_unreserve_roundtrip(default_trace):
     eng.unreserve(0, share, a, m1)
     assert bytes(eng.nodes(0)) == before
     # a second Unreserve of the same pod would push the devices past 1000 milli: reported, not applied
-    # (ADVICE r2).  The guard checks devices and CPU only, so it catches this because the nodes hold no
-    # other pod; in general the caller's record of its bindings prevents a double release (the cgo plugin
-    # forgets a binding once released, go/ksim_gpu.go release; include/ksim_engine.h)
+    # (ADVICE r2).  The guard is removePod's invariant (devices, CPU and memory within the node's
+    # allocatable, cache.go:100-111); the caller's record of its bindings is what prevents a double
+    # release in general (the cgo plugin forgets a binding once released, go/ksim_gpu.go release)
     for pod, node, mask in ((whole, b, m2), (share, a, m1)):
         with pytest.raises(ksim.KsimError) as ei:
             eng.unreserve(0, pod, node, mask)
         assert ei.value.code == ksim.KSIM_ESTATE
     assert bytes(eng.nodes(0)) == before
     eng.close()
+
+
+def test_double_unreserve_on_a_shared_node_is_refused(default_trace):
+    # the node still hosts another pod, so the devices and the CPU would both stay
+    # within the allocatable after a second release of B; only the memory term catches it
+    rp = default_trace.replay(seed=4)
+    keep = list(range(0, default_trace.num_nodes, 12))
+    arr, n = default_trace.typical()
+    nodes = helpers.subset_nodes(rp, keep)
+    eng = ksim.Engine(len(keep), 1)
+    try:
+        eng.set_nodes(0, nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        node = max(range(len(keep)), key=lambda i: nodes[i].mem_alloc_mib - nodes[i].mem_used_mib)
+        free_mem = nodes[node].mem_alloc_mib - nodes[node].mem_used_mib
+        assert nodes[node].mem_used_mib == 0 and free_mem > 4096
+        a_pod = ksim.make_pod(8000, mem=256)          # much CPU, little memory
+        b_pod = ksim.make_pod(1000, mem=free_mem // 2)  # little CPU, much memory
+        before = bytes(eng.nodes(0))
+        assert eng.reserve(0, a_pod, node) == 0
+        assert eng.reserve(0, b_pod, node) == 0
+        eng.unreserve(0, b_pod, node, 0)
+        after_one = bytes(eng.nodes(0))
+        with pytest.raises(ksim.KsimError) as ei:
+            eng.unreserve(0, b_pod, node, 0)
+        assert ei.value.code == ksim.KSIM_ESTATE
+        assert bytes(eng.nodes(0)) == after_one
+        eng.unreserve(0, a_pod, node, 0)
+        assert bytes(eng.nodes(0)) == before
+    finally:
+        eng.close()
 
 
 def test_unreserve_rejects_what_the_node_does_not_hold(default_trace):
