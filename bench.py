@@ -263,6 +263,9 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="c5 only: ONE cluster node-sharded over the ranks (RCCL exchange per pod; strong "
                          "scaling) instead of one replica per rank")
+    ap.add_argument("--rank-share", default="",
+                    help="c4 only, 'k/N': time rank k's share of a world-N split of the sweep on this one GPU (the "
+                         "1-GPU rehearsal of the N-GPU strong-scaling run: the max over k predicts its time)")
     ap.add_argument("--random-stream", default="hash", choices=["hash", "go"],
                     help="Random policy: the hash contract (default) or the reference's draw structure on Go's "
                          "math/rand stream (k_random_go)")
@@ -297,7 +300,14 @@ def main():
     trace = ksim.Trace.openb("default")
     if args.config == "c4":
         import ksim.sweep as SW
-        exps = SW.shard(SW.plan(), rank, world)
+        items = SW.plan()
+        share_k, share_n = rank, world
+        if args.rank_share:
+            share_k, share_n = (int(x) for x in args.rank_share.split("/"))
+            assert world == 1 and 0 <= share_k < share_n, "--rank-share k/N runs one share on one GPU"
+        # longest-processing-time split by the cost model (ksim.sweep.plan_costs): the long FGD replays spread
+        # over the ranks, the totals balance
+        exps = SW.shard(items, share_k, share_n, SW.plan_costs(items) if share_n > 1 else None)
         sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs, random_stream=args.random_stream)
         eng = sweep.eng
         eng.total_events = sweep.total_events
@@ -401,6 +411,10 @@ def main():
                           "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
         # whole job: every rank's experiments per timed step (the reference: 1020 in ~10 h on 256 vCPU)
         line["experiments_per_s"] = args.replicas * world / (dt / args.steps)
+        if args.rank_share:
+            line["config"]["rank_share"] = args.rank_share
+            line["config"]["workload"] += " -- rank %s's share of the LPT split only (%d experiments)" % (
+                args.rank_share, args.replicas)
     if args.config == "c5" and args.sharded:
         line["scaling"] = "strong"
         line["config"] = {"workload": "C5: synthetic 100000 nodes x 1000000 pods, FGD, ONE cluster node-sharded "

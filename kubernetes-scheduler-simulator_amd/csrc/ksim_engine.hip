@@ -3890,6 +3890,12 @@ int ksim_engine_run(ksim_engine* e) {
       if ((e->tev_used >> i) & 1u && hipEventElapsedTime(&gms, e->tev_fork, e->tev_side[i]) == hipSuccess)
         std::fprintf(stderr, " side%d %.3f;", i, gms);
     }
+    for (int g = 0; g < e->grp_rev_used; ++g) {  // each group's replay end (= its report's start) and report end
+      float a = 0.f, b = 0.f;
+      if (hipEventElapsedTime(&a, e->tev_fork, e->grp_rev[2 * g]) == hipSuccess &&
+          hipEventElapsedTime(&b, e->tev_fork, e->grp_rev[2 * g + 1]) == hipSuccess)
+        std::fprintf(stderr, " g%d replay %.3f report %.3f;", g, a, b);
+    }
     std::fprintf(stderr, " run %.3f\n", ms);
   }
   e->last_steps = max_ev;

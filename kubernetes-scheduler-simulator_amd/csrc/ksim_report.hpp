@@ -127,28 +127,6 @@ __device__ __forceinline__ __int128 shfl_up128(__int128 v, int o) {
   return (__int128)(((unsigned __int128)hi << 64) | lo);
 }
 
-// Exclusive prefix over the workgroup (kScanBlock threads) and the total.  Integer adds: exact.
-__device__ __forceinline__ __int128 block_excl_scan128(__int128 v, __int128* s_w, __int128* total) {
-  const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __int128 incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const __int128 x = shfl_up128(incl, o);
-    if (lane >= o) incl += x;
-  }
-  if (lane == 63) s_w[w] = incl;
-  __syncthreads();
-  __int128 base = 0, t = 0;
-#pragma unroll
-  for (int i = 0; i < kScanBlock / 64; ++i) {
-    base += i < w ? s_w[i] : (__int128)0;
-    t += s_w[i];
-  }
-  *total = t;
-  __syncthreads();
-  return base + incl - v;
-}
-
 // Field k of a RepAcc (0-8 are 128-bit fixed point, 9-15 64-bit counters).
 __device__ __forceinline__ __int128 rep_get(const RepAcc* o, int k) {
   return k < kFx ? o->fx[k] : (__int128)o->cnt[k - kFx];
@@ -157,17 +135,51 @@ __device__ __forceinline__ void rep_set(RepAcc* o, int k, __int128 v) {
   if (k < kFx) o->fx[k] = v;
   else o->cnt[k - kFx] = (long long)v;
 }
-__device__ __forceinline__ bool power_field(int k) { return k == 7 || k == 8 || k == 15; }
 
-// grid R: the initial cluster's report, then the inclusive prefix over the events (in place),
-// one field at a time (keeps the 128-bit running sums in a few registers).
+// Exclusive prefix over the workgroup of every field at once (in place), and each field's total into
+// s_tot (LDS, may be null): a wave-inclusive scan per field (shuffles), the wave totals through LDS, one
+// barrier.  Integer adds: exact.
+__device__ __forceinline__ void block_excl_scan_fields(__int128 (&v)[kFields], __int128 (*s_w)[kFields], __int128* s_tot) {
+  const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) {
+    __int128 incl = v[k];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const __int128 x = shfl_up128(incl, o);
+      if (lane >= o) incl += x;
+    }
+    if (lane == 63) s_w[w][k] = incl;
+    const __int128 ex = shfl_up128(incl, 1);
+    v[k] = lane == 0 ? (__int128)0 : ex;
+  }
+  __syncthreads();
+  if (s_tot && tid < kFields) {
+    __int128 t = 0;
+    for (int i = 0; i < kScanBlock / 64; ++i) t += s_w[i][tid];
+    s_tot[tid] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) {
+    __int128 base = 0;
+    for (int i = 0; i < w; ++i) base += s_w[i][k];
+    v[k] += base;
+  }
+  __syncthreads();
+}
+
+// grid R: the initial cluster's report, then the inclusive prefix over the events (in place).  Every
+// thread owns a contiguous chunk of events: one pass sums the chunk's records (all fields at once), one
+// block scan gives each chunk's start, a second pass writes the running sums -- each record read twice and
+// written once (r05; the r01-r04 form took one read-sum and one read-write pass per field, 32 passes over
+// the records).
 __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
                                                             int N, const int* list) {
   const int r = list ? list[blockIdx.x] : (int)blockIdx.x;
   const ReplicaDev rp = reps[r];
   if (!rp.rep) return;
   __shared__ TypDev s_tp[kMaxTypical];
-  __shared__ __int128 s_w[kScanBlock / 64];
+  __shared__ __int128 s_w[kScanBlock / 64][kFields];
   __shared__ __int128 s_base[kFields];
   stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
   const int tid = (int)threadIdx.x;
@@ -183,28 +195,30 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
 #pragma unroll
       for (int k = 0; k < kFields; ++k) acc[k] += f[k];
     }
-#pragma unroll
-    for (int k = 0; k < kFields; ++k) {
-      __int128 tot;
-      (void)block_excl_scan128(acc[k], s_w, &tot);
-      if (tid == 0) s_base[k] = tot;
-    }
+    block_excl_scan_fields(acc, s_w, s_base);
   }
-  __syncthreads();
-  // contiguous chunk per thread: local total, block exclusive scan, then the running sum
+  // contiguous chunk per thread: local totals, block exclusive scan, then the running sums
   const int E = rp.n_events;
   const int per = (E + kScanBlock - 1) / kScanBlock;
   const int lo = min(E, tid * per), hi = min(E, lo + per);
-#pragma unroll 1
-  for (int k = 0; k < kFields; ++k) {
-    if (!rp.has_pw && power_field(k)) continue;  // stays 0 (k_report_delta wrote 0)
-    __int128 loc = 0;
-    for (int e = lo; e < hi; ++e) loc += rep_get(rp.rep + e, k);
-    __int128 tot;
-    __int128 run = s_base[k] + block_excl_scan128(loc, s_w, &tot);
-    for (int e = lo; e < hi; ++e) {
-      run += rep_get(rp.rep + e, k);
-      rep_set(rp.rep + e, k, run);
+  __int128 run[kFields];
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) run[k] = 0;
+  for (int e = lo; e < hi; ++e) {
+    const RepAcc* o = rp.rep + e;
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) run[k] += rep_get(o, k);
+  }
+  block_excl_scan_fields(run, s_w, nullptr);
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) run[k] += s_base[k];
+  for (int e = lo; e < hi; ++e) {
+    RepAcc* o = rp.rep + e;
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) {
+      run[k] += rep_get(o, k);
+      // the power fields stay 0 without an energy model (k_report_delta wrote 0; the sums are 0 too)
+      rep_set(o, k, run[k]);
     }
   }
 }

@@ -39,9 +39,53 @@ def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
     return [(t, p, s, tune) for t in traces for p in policies for s in seeds]
 
 
-def shard(items, rank, world):
-    """Replica-parallel split across ranks (no collective on the data path)."""
-    return items[rank::world]
+# Cost model of one experiment on one GPU (r04/r05 measurements, profiles/r04/hmemo/c4_fgd_traces.jsonl):
+# FGD replays on k_hmemo at ~4.1 us per event up to ~64 typical pods, growing with the typical table beyond
+# (gpuspec33, 127 typical pods: 9.1 us); the cheap policies on k_scan1 at ~3.3 us per event.
+FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
+
+
+def experiment_cost_us(policy_dir, events, n_typical):
+    """Estimated replay time of one experiment (us): its events x the policy's per-event latency."""
+    if policy_dir == "06-FGD":
+        return events * (FGD_US + FGD_US_PER_TYP * max(0, n_typical - 64))
+    return events * CHEAP_US
+
+
+_EVENTS = {}
+
+
+def plan_costs(items):
+    """Estimated cost of each (trace, policy, seed, tune) experiment: the replay's event count (the
+    reference's own stream, ksim.Trace.replay) x experiment_cost_us's latency."""
+    traces = {}
+    out = []
+    for (t, p, s, tune) in items:
+        if t not in traces:
+            traces[t] = ksim.Trace.openb(t[len("openb_pod_list_"):] if t.startswith("openb_pod_list_") else t)
+        tr = traces[t]
+        k = (t, s, tune)
+        if k not in _EVENTS:
+            _EVENTS[k] = tr.replay(seed=s, tune_ratio=tune, shuffle=True).n
+        out.append(experiment_cost_us(p, _EVENTS[k], tr.typical()[1]))
+    return out
+
+
+def shard(items, rank, world, costs=None):
+    """Replica-parallel split across ranks (no collective on the data path).  With `costs` (one per item,
+    plan_costs): longest processing time first -- items by falling cost, each to the rank with the least
+    cost so far (ties to the lower rank) -- so the long FGD replays spread over the ranks and the totals
+    balance; each rank keeps its items in plan order.  Without: round robin (items[rank::world])."""
+    if costs is None or world <= 1:
+        return items[rank::world]
+    load = [0.0] * world
+    mine = []
+    for i in sorted(range(len(items)), key=lambda i: (-costs[i], i)):
+        k = min(range(world), key=lambda j: (load[j], j))
+        load[k] += costs[i]
+        if k == rank:
+            mine.append(i)
+    return [items[i] for i in sorted(mine)]
 
 
 class Sweep:

@@ -46,7 +46,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     traces = SW.TRACES if args.traces == "all" else args.traces.split(",")
     policies = tuple(SW.ALL_POLICY_DIRS) if args.pwr else tuple(SW.POLICY_DIRS)
-    exps = SW.shard(SW.plan(traces=traces, policies=policies), rank, world)
+    items = SW.plan(traces=traces, policies=policies)
+    exps = SW.shard(items, rank, world, SW.plan_costs(items) if world > 1 else None)
     t0 = time.perf_counter()
     sw = SW.Sweep(exps, device=local, fgd_batch=args.fgd_batch)
     t_setup = time.perf_counter() - t0

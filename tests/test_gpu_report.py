@@ -121,7 +121,9 @@ def test_report_multi_replica_ragged(default_trace):
         eng.set_policy(r, name)
         eng.load_events(r, rp.events, n_ev)
     eng.run()
-    assert eng.last_report_ms() >= 0  # ~0 when the reports ran behind concurrent groups (run_persistent)
+    # the report kernels ran: after a sequential replay the report behind it, after concurrent groups the sum
+    # of each group's report timed on its own stream
+    assert eng.last_report_ms() > 0
     for r, (seed, name, pol, sel, n_ev) in enumerate(cfgs):
         onodes = helpers.oracle_subset(default_trace, rps[r], keep)
         _, _, want = O.run_events(onodes, helpers.oracle_typical(default_trace),
@@ -171,6 +173,11 @@ def test_report_concurrent_groups_side_streams(default_trace, monkeypatch, side)
             eng.set_policy(r, name, seed=seed)
             eng.load_events(r, rp.events, 700)
         eng.run()
+        # FGD on k_hmemo and the five cheap policies as one k_scan1_mix launch, concurrently; each group's
+        # report timed on its stream
+        launches, streams = eng.last_run_launches()
+        assert launches == 2 and streams == min(2, int(side))
+        assert eng.last_report_ms() > 0
         got = [(eng.results(r), eng.reports(r)) for r in range(len(cfgs))]
     finally:
         eng.close()
