@@ -1645,6 +1645,7 @@ struct ksim_engine {
   // k_memo (memoised FGD replay): per replica the distinct pod requests of its creation events
   // (PodDev.pad = class id) and how many events each has
   std::vector<std::vector<PodDev>> h_cls;
+  std::vector<std::vector<TypDev>> h_tp;  // each replica's typical table as uploaded (k_hmemo's per-model tables)
   std::vector<std::vector<int>> h_cls_n;
   std::vector<std::vector<int>> h_ev_cls;  // class of each event, -1 delete
   PodDev* d_m_pod = nullptr;
@@ -1672,6 +1673,9 @@ struct ksim_engine {
   PodDev* d_h_cls = nullptr;
   uint16_t* d_h_cgrp = nullptr;
   PodDev* d_h_gpod = nullptr;
+  int* d_h_mtoff = nullptr;      // k_hmemo's per-model tables (typed replicas)
+  uint8_t* d_h_mtab = nullptr;
+  double* d_h_na = nullptr;      // their NA bins per (model, total), k_hinit_na
   int* d_h_evc = nullptr;
   NodeRec* d_h_st = nullptr;
   int* d_h_ns = nullptr;
@@ -1683,7 +1687,7 @@ struct ksim_engine {
   int* d_h_cnt = nullptr;
   unsigned long long* d_h_prof = nullptr;
   uint8_t* d_h_hist = nullptr;  // wide k_hmemo with deletes: per-workgroup bind history
-  size_t h_cap[15] = {};
+  size_t h_cap[18] = {};
   int last_hmemo = 0;
   int last_rgo = 0;  // replicas the last run replayed on k_random_go
   int last_scan1 = 0;  // replicas the last run replayed on k_scan1
@@ -1986,6 +1990,11 @@ struct HPlan {
   std::vector<NodeRec> st;        // [Rg][Smax] distinct initial node states
   std::vector<int> ns;            // [Rg]
   std::vector<int> nstate;        // [Rg][Npad] state of each rank, -1 padding
+  // Typed replicas (a GPU typical pod names models): per GPU model of the cluster, the typical table cut to
+  // the CPU-only pods and the GPU pods that accept the model (ksim_hmemo.hpp, "per-model tables")
+  int Mtab = 0, Mslots = 0;       // longest replica's concatenated tables, most models of one replica
+  std::vector<int> mtoff;         // [Rg][KSIM_MAX_TYPES] kMtPresent | slot << 21 | entries << 12 | offset
+  std::vector<uint8_t> mtab;      // [Rg][Mtab] typical-table index of each entry
 };
 
 // Classes of each replica grouped by score request (cpu_nz, milli, num: the candidate states of
@@ -2068,9 +2077,39 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     // KSIM_HL2=0 never, =1 also for one workgroup per replica.
     const char* v = std::getenv("KSIM_HL2");
     const bool want = v ? v[0] == '1' : pl.K > 1;
-    pl.l2 = want && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true).total <= 160 * 1024;
+    pl.l2 = want && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true, 0).total <= 160 * 1024;
   }
-  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, pl.l2).total;
+  {  // per-model tables of the typed replicas (KSIM_HMODEL=0: the whole table for every model, as before r05)
+    const char* hm = std::getenv("KSIM_HMODEL");
+    const bool on = !(hm && hm[0] == '0');
+    pl.Mtab = pl.Mslots = 0;
+    pl.mtoff.assign((size_t)Rg * KSIM_MAX_TYPES, 0);
+    std::vector<std::vector<uint8_t>> mt(Rg);
+    for (int i = 0; on && i < Rg; ++i) {
+      const int r = reps[i];
+      if (!e->reps[r].typed || e->h_tp[r].size() != (size_t)e->reps[r].nt) continue;
+      const std::vector<TypDev>& tpv = e->h_tp[r];
+      const int ncpu = e->reps[r].ncpu, nt = e->reps[r].nt;
+      uint32_t models = 0u;
+      for (const NodeRec& n : e->h_rec[r]) models |= 1u << n.gpu_type;
+      int slot = 0;
+      for (int m = 0; m < KSIM_MAX_TYPES; ++m) {
+        if (!((models >> m) & 1u)) continue;
+        const int off = (int)mt[i].size();
+        for (int t = 0; t < nt; ++t)
+          if (t < ncpu || (tpv[t].tmask >> m) & 1u) mt[i].push_back((uint8_t)t);
+        const int len = (int)mt[i].size() - off;
+        pl.mtoff[(size_t)i * KSIM_MAX_TYPES + m] = (int)(ksim_hmemo::kMtPresent | (uint32_t)slot << 21 | (uint32_t)len << 12 | (uint32_t)off);
+        ++slot;
+      }
+      pl.Mtab = std::max(pl.Mtab, (int)mt[i].size());
+      pl.Mslots = std::max(pl.Mslots, slot);
+    }
+    if (pl.Mtab > 4095) return false;
+    pl.mtab.assign((size_t)Rg * std::max(pl.Mtab, 1), 0);
+    for (int i = 0; i < Rg; ++i) std::copy(mt[i].begin(), mt[i].end(), pl.mtab.begin() + (size_t)i * std::max(pl.Mtab, 1));
+  }
+  pl.lds = hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, pl.l2, pl.Mtab).total;
   if (pl.lds > 160 * 1024) return false;
   pl.cg.assign((size_t)Rg * 2, 0);
   pl.cls.assign((size_t)Rg * pl.Cmax, PodDev{});
@@ -2089,7 +2128,17 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
       pl.cls[(size_t)i * pl.Cmax + k] = cls[ord[i][k]];
       pl.cgrp[(size_t)i * pl.Cmax + k] = (uint16_t)gof[i][ord[i][k]];
     }
+    // a group's request: its first class's (the score part, fgd_score.go:99-149, is the group's), with the
+    // least demanding Filter part of every class of the group -- min CPU, min memory, every accepted GPU
+    // model -- so that Filter of it on a node fails only when every class of the group fails (the group
+    // pruning of k_hmemo's F list; nothing else reads these fields of a group's request)
     for (size_t g = 0; g < gfirst[i].size(); ++g) pl.gpod[(size_t)i * pl.Gmax + g] = cls[gfirst[i][g]];
+    for (size_t c = 0; c < cls.size(); ++c) {
+      PodDev& gp = pl.gpod[(size_t)i * pl.Gmax + gof[i][c]];
+      gp.cpu_req = std::min(gp.cpu_req, cls[c].cpu_req);
+      gp.mem = std::min(gp.mem, cls[c].mem);
+      gp.tmask |= cls[c].tmask;
+    }
     const std::vector<int>& ec = e->h_ev_cls[r];
     for (size_t k = 0; k < ec.size(); ++k) pl.evc[(size_t)i * stride + k] = ec[k] < 0 ? -1 : slot[i][ec[k]];
     std::copy(sts[i].begin(), sts[i].end(), pl.st.begin() + (size_t)i * pl.Smax);
@@ -2129,6 +2178,11 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   if ((rc = ensure_buf(e->d_h_l1, e->h_cap[10], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
   if (pl.l2 && (rc = ensure_buf(e->d_h_l2, e->h_cap[14], (size_t)Rg * pl.Cmax * pl.nb))) return rc;
   if ((rc = ensure_buf(e->d_h_cnt, e->h_cap[11], (size_t)Rg * pl.Cmax))) return rc;
+  if (pl.Mtab > 0) {
+    if ((rc = upload_vec(e->d_h_mtoff, e->h_cap[15], pl.mtoff, st))) return rc;
+    if ((rc = upload_vec(e->d_h_mtab, e->h_cap[16], pl.mtab, st))) return rc;
+    if ((rc = ensure_buf(e->d_h_na, e->h_cap[17], (size_t)Rg * pl.Mslots * ksim_hmemo::kNaStride))) return rc;
+  }
   if (!e->d_th) {
     KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
     KSIM_HIP(hipMemcpyAsync(e->d_th, score_table(), sizeof(double) * 102, hipMemcpyHostToDevice, st));
@@ -2393,6 +2447,14 @@ static int hmemo_init_keys(ksim_engine* e, int Rg, int first, hipStream_t st, in
   ia.l2 = pl.l2 ? e->d_h_l2 : nullptr;
   ia.cnt = e->d_h_cnt;
   ia.th = e->d_th;
+  ia.mtoff = pl.Mtab > 0 ? e->d_h_mtoff : nullptr;
+  ia.na = pl.Mtab > 0 ? e->d_h_na : nullptr;
+  ia.Mslots = pl.Mslots;
+  if (pl.Mtab > 0) {
+    hipLaunchKernelGGL(k_hinit_na, dim3((unsigned)((kNaStride + 255) / 256), (unsigned)pl.Mslots, (unsigned)Rg), dim3(256), 0,
+                       st, ia, (const TypDev*)e->d_tp);
+    KSIM_HIP(hipGetLastError());
+  }
   KSIM_HIP(hipMemsetAsync(e->d_h_cnt, 0, sizeof(int) * (size_t)Rg * pl.Cmax, st));
   hipLaunchKernelGGL(k_hinit_gk, dim3((unsigned)((pl.Smax + 255) / 256), (unsigned)pl.Gmax, (unsigned)Rg), dim3(256), 0,
                      st, ia, (const TypDev*)e->d_tp);
@@ -2413,6 +2475,11 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
   std::memset(&ma, 0, sizeof ma);  // every field a caller does not set (the gate, profile, exchange pointers) is null
   ma.reps = e->d_reps;
   ma.rep_list = e->d_replist + first;
+  ma.Mtab = pl.Mtab;
+  ma.Mslots = pl.Mslots;
+  ma.mtoff = pl.Mtab > 0 ? e->d_h_mtoff : nullptr;
+  ma.mtab = pl.Mtab > 0 ? e->d_h_mtab : nullptr;
+  ma.na = pl.Mtab > 0 ? e->d_h_na : nullptr;
   ma.N = e->N;
   ma.Npad = pl.Npad;
   ma.nb = pl.nb;
@@ -2457,6 +2524,11 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     const char* fw = std::getenv("KSIM_HFW");
     const int v = fw ? std::atoi(fw) : ksim_hmemo::kFW;
     ma.fw_big = v >= 1 && v <= 13 ? v : ksim_hmemo::kFW;
+  }
+  {  // KSIM_HPRUNE (A/B): the F list's group pruning for replicas with more than this many typical pods
+    // (-1: every replica; default 64: the large typed tables, where the F rounds bound the step)
+    const char* pr = std::getenv("KSIM_HPRUNE");
+    ma.prune_t = pr ? std::atoi(pr) : 64;
   }
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
@@ -2674,6 +2746,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->has_delete.assign(n_replicas, 0);
   e->go_state.assign(n_replicas, {});
   e->h_cls.resize(n_replicas);
+  e->h_tp.resize(n_replicas);
   e->h_cls_n.resize(n_replicas);
   e->h_ev_cls.resize(n_replicas);
   e->nt.assign(n_replicas, 0);
@@ -2727,7 +2800,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_cap, e->d_mcap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
-                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
+                  e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
                   e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
@@ -2875,6 +2948,8 @@ int ksim_engine_set_typical(ksim_engine* e, int replica, const ksim_typical* tp,
   e->reps[replica].nt = (int)h.size();
   e->reps[replica].ncpu = (int)cpu.size();
   e->reps[replica].typed = typed ? 1 : 0;
+  e->h_tp[replica] = h;
+  e->mplan_dirty = true;  // k_hmemo's plan holds per-model views of the table
   int rc = upload_reps(e);
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));

@@ -113,12 +113,25 @@ struct HMemoArgs {
                             // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
   int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
   int fw_big;               // F waves of a replica with more than 64 typical pods (KSIM_HFW; kFW by default)
+  int prune_t;              // list only the score groups some class of which may pass Filter on d (the group's
+                            // PodDev holds the least demanding request: min CPU / memory, every accepted GPU
+                            // model) for replicas with more than prune_t typical pods (KSIM_HPRUNE)
   // Residency gate (a concurrent run's FGD group): each workgroup stores `gate_epoch` into started[its
   // index] (host memory) as it starts, so the host launches the short groups only once every long replay
   // holds its CU.  Null: no gate.
   int* started;
   int gate_epoch;
+  // Per-model tables (typed replicas, null otherwise): mtoff[gi][model] = kMtPresent | slot << 21 | entries << 12 |
+  // offset into mtab[gi][.] (typical-table indices: the CPU-only pods, then the GPU pods accepting the model, in
+  // table order); na[gi][slot][total] = the NA bin of every state of that model with `total` milli-GPU left
+  // (k_hinit_na).  Mtab: mtab's stride; Mslots: na's.
+  const int* mtoff;
+  const uint8_t* mtab;
+  const double* na;
+  int Mtab, Mslots;
 };
+constexpr uint32_t kMtPresent = 1u << 31;
+constexpr int kNaStride = 8008;  // totals 0 .. 8 x 1000 (kMaxGpu x kMilli), padded
 constexpr int kHProf = 16;  // 0-6 phase sums, 7 items, 8 flagged classes, 9 refresh steps, 10 clock, 11 wall
 
 struct __align__(16) HShared {
@@ -150,10 +163,10 @@ static_assert(sizeof(HShared) % 16 == 0, "keep the dynamic regions 16-B aligned"
 
 // Dynamic LDS after HShared (16-B aligned regions).
 struct HLayout {
-  size_t cls, gpod, F, l1, l2, nodes, last, cnt, bx, bx2, cgrp, flist, code, igrp, fnew, fold, gbase, gkey, total;
+  size_t cls, gpod, F, l1, l2, nodes, last, cnt, bx, bx2, cgrp, flist, code, igrp, fnew, fold, gbase, gkey, ctp, mto, total;
 };
 KSIM_HD size_t halign(size_t x) { return (x + 15) & ~(size_t)15; }
-KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2) {
+KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2, int Mtab) {
   HLayout L;
   size_t o = sizeof(HShared);
   L.cls = o;   o = halign(o + (size_t)Cmax * sizeof(PodDev));
@@ -174,6 +187,8 @@ KSIM_HD HLayout hmemo_layout(int N, int Cmax, int Gmax, int nb, bool l2) {
   L.fold = o;  o = halign(o + (size_t)Cmax);
   L.gbase = o; o = halign(o + (size_t)Gmax * 2 * 2);
   L.gkey = o;  o = halign(o + (size_t)Gmax * 2 * 4);  // every score group's key on d, double-buffered like the list
+  L.ctp = o;   o = halign(o + (size_t)Mtab * sizeof(TypDev));  // the per-model tables (typed replicas)
+  L.mto = o;   o = halign(o + (Mtab > 0 ? (size_t)KSIM_MAX_TYPES * 4 : 0));
   L.total = o;
   return L;
 }
@@ -321,7 +336,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const int lo = w * a.S, ns = min(a.S, N - lo), b0 = lo / kFan;
   const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
   const bool use_l2 = a.l2 != nullptr;
-  const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb, use_l2);
+  const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb, use_l2, a.Mtab);
   PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
   double* s_F = reinterpret_cast<double*>(smem + L.F);
@@ -340,6 +355,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int16_t* const s_gbase_b = reinterpret_cast<int16_t*>(smem + L.gbase);
   unsigned* const s_gkey_b = reinterpret_cast<unsigned*>(smem + L.gkey);
   uint16_t* s_flist = reinterpret_cast<uint16_t*>(smem + L.flist);
+  TypDev* s_ctp = reinterpret_cast<TypDev*>(smem + L.ctp);
+  int* s_mto = reinterpret_cast<int*>(smem + L.mto);
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   unsigned* keys = a.keys + (size_t)gi * a.Cmax * a.Npad;
   const int* evc = a.evc + (size_t)gi * a.stride;
@@ -375,6 +392,11 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     if (use_l2) s_l2[i] = in ? a.l2[gix] : 0u;
   }
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
+  if (a.Mtab > 0) {  // the per-model tables: copies of the entries they name (the table in HBM, as above)
+    for (int i = tid; i < a.Mtab * 2; i += kHBlock)
+      reinterpret_cast<uint4*>(s_ctp)[i] = reinterpret_cast<const uint4*>(tp + a.mtab[(size_t)gi * a.Mtab + i / 2])[i & 1];
+    for (int m = tid; m < KSIM_MAX_TYPES; m += kHBlock) s_mto[m] = rp.typed ? a.mtoff[(size_t)gi * KSIM_MAX_TYPES + m] : 0;
+  }
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
   if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; sh.f0seq = 0; }
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
@@ -407,6 +429,25 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   // F waves (1..fw) and class waves (fw+1..15): kFW, or a.fw_big for a replica with more than 64 typical
   // pods (the F rounds grow with the table, the class pass does not)
   const int fw = rp.nt > 64 ? a.fw_big : kFW, cw = kHWaves - 1 - fw;
+  const bool prune = rp.nt > a.prune_t;
+  // F of a candidate state of node n (fgd_candidate's cpuL / gs / total) by the quad of lane q.  A typed replica
+  // with per-model tables evaluates only the CPU-only pods and the GPU pods that accept n's model: every other
+  // GPU pod adds its freq x total to the NA bin and nothing else (GetNodePodFrag, frag.go:460-493), so the NA
+  // bin -- added last in FragAmountSumExceptQ3 (frag.go:411-418) -- is the same sequential sum for every state
+  // of the model with that total: na[slot][total] (k_hinit_na).  Same bits as the whole table.
+  auto state_F = [&](const NodeV& n, int cpuL, const uint32_t (&gs)[4], int total, int q) -> double {
+    const uint32_t tb = 1u << n.gpu_type();
+    if (a.Mtab > 0) {
+      const unsigned mw = (unsigned)s_mto[n.gpu_type()];
+      if (mw & kMtPresent) {
+        const double nav = a.na[((size_t)gi * a.Mslots + ((mw >> 21) & 31u)) * kNaStride + total];
+        const double F = frag_F_quad<false>(cpuL, gs, total, tb, tp, s_ctp + (mw & 0xfffu), rp.ncpu, (int)((mw >> 12) & 0x1ffu), q);
+        return F + nav;
+      }
+    }
+    return typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
+                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+  };
   // wave 0 lists the next refresh's F evaluations (one workgroup per replica; the wide form too with bit 4)
   const bool w0list = (kSub == 0 || (a.pf & 4) != 0) && (a.pf & 1) != 0;
   const bool w0pf = kSub == 0 && (a.pf & 2) != 0;    // and touches its flagged key rows
@@ -506,6 +547,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         } else if (wv == 1) {
           if constexpr (kProf) hdelay(a.delay, 2, step, wv, wg);
           const unsigned dfirst = __builtin_amdgcn_readfirstlane(sh.dfirst[cur]);
+          const NodeSum sd = node_sum(dn);
           int base = 1;  // item 0: d's current state
           for (int g0 = 0; g0 < G; g0 += 64) {
             const int g = g0 + lane;
@@ -515,6 +557,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
               const PodDev gp = s_gpod[g];
               share = is_share_pod(gp);
               cm = share ? (dfirst & ksim_memo::ge_mask(dn, gp.milli)) : 0x100u;
+              if (prune && !filter_sum(sd, dn, gp)) cm = 0u;  // no class of the group passes Filter on d
             }
             const int nc = __popc(cm);
             int excl = 0, tot = 0;
@@ -560,9 +603,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           int cpuL, total;
           uint32_t gs[4];
           fgd_candidate(dn, code, gp, &cpuL, gs, &total);
-          const uint32_t tb = 1u << dn.gpu_type();
-          const double F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q)
-                                 : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, q);
+          const double F = state_F(dn, cpuL, gs, total, q);
           if (q == 0) s_F[j] = F;
         }
         // every listed candidate's key into its score group's max (LDS atomics), against item 0's F (d's
@@ -708,9 +749,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
           int cpuL, total;
           uint32_t gs[4];
           fgd_candidate(dn, code, gp, &cpuL, gs, &total);
-          const uint32_t tb = 1u << dn.gpu_type();
-          F = typed ? frag_F_quad<true>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, qq)
-                    : frag_F_quad<false>(cpuL, gs, total, tb, tp, sh.tp, rp.ncpu, rp.nt, qq);
+          F = state_F(dn, cpuL, gs, total, qq);
         }
         const long long fb = __builtin_bit_cast(long long, F);
         const double F0 = __builtin_bit_cast(double, ((long long)(unsigned)__builtin_amdgcn_readlane((int)(fb >> 32), 0) << 32) |
@@ -927,6 +966,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         if (lane == 0) sh.dfirst[cur ^ 1] = fm;
         if (w0list) {  // the next refresh's F list (wave 0 waits for the bulk at the end barrier anyway)
           const unsigned dfirst = (unsigned)__builtin_amdgcn_readfirstlane((int)fm);
+          const NodeSum sd = node_sum(after);
           uint8_t* const ncode = s_code_b + (cur ^ 1) * kMaxItems;
           uint8_t* const nigrp = s_igrp_b + (cur ^ 1) * kMaxItems;
           int16_t* const ngbase = s_gbase_b + (cur ^ 1) * a.Gmax;
@@ -940,6 +980,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
               const PodDev gp = s_gpod[g];
               share = is_share_pod(gp);
               cm = share ? (dfirst & ksim_memo::ge_mask(after, gp.milli)) : 0x100u;
+              if (prune && !filter_sum(sd, after, gp)) cm = 0u;  // no class of the group passes Filter on d
             }
             const int nc = __popc(cm);
             int excl = 0, tot = 0;
@@ -1041,7 +1082,36 @@ struct HInitArgs {
   unsigned* l2;            // [Rg][Cmax][nb] second maxima, or null
   int* cnt;                // [Rg][Cmax], zeroed before k_hinit_keys
   const double* th;
+  const int* mtoff;        // [Rg][KSIM_MAX_TYPES] the per-model tables (HMemoArgs), null: none
+  double* na;              // [Rg][Mslots][kNaStride]
+  int Mslots;
 };
+
+// grid (kNaStride / 256, Mslots, Rg): the NA bin of every (model, total) of a typed replica -- the sequential
+// sum, in table order, of freq x total over the GPU typical pods that do not accept the model (frag_F_quad's
+// bin 3: x = freq * dtot, then bin += x)
+__global__ __launch_bounds__(256) void k_hinit_na(HInitArgs a, const TypDev* __restrict__ tp_all) {
+  const int gi = (int)blockIdx.z, slot = (int)blockIdx.y;
+  const int total = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (total >= kNaStride) return;
+  const int r = a.rep_list[gi];
+  const ReplicaDev& rp = a.reps[r];
+  const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
+  int m = -1;
+  for (int k = 0; k < KSIM_MAX_TYPES; ++k) {
+    const unsigned w = (unsigned)a.mtoff[(size_t)gi * KSIM_MAX_TYPES + k];
+    if ((w & kMtPresent) && (int)((w >> 21) & 31u) == slot) m = k;
+  }
+  if (m < 0) return;
+  const double dtot = (double)total;
+  double na = 0.0;
+  for (int t = rp.ncpu; t < rp.nt; ++t) {
+    if ((tp[t].tmask >> m) & 1u) continue;
+    const double x = tp[t].freq * dtot;
+    na += x;
+  }
+  a.na[((size_t)gi * a.Mslots + slot) * kNaStride + total] = na;
+}
 
 __global__ __launch_bounds__(256) void k_hinit_gk(HInitArgs a, const TypDev* __restrict__ tp_all) {
   const int gi = (int)blockIdx.z, g = (int)blockIdx.y;
