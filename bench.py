@@ -35,7 +35,7 @@ BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # dispatch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section) and its
 # VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/<round>/prof/<profile_key(args)>/pmc.json, the
 # newest round that profiled the configuration first.
-PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r04", "r03", "r02")]
+PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r05", "r04", "r03", "r02")]
 PROF_DIR = PROF_DIRS[0]
 # MI355X_MICROARCH.md, persistent-kernel price list: handoff-1to1 = one producer -> one consumer
 # granule hand-off between CUs, idle chip, 8 B: 0.8 us.  A pod step whose decision crosses CUs
@@ -308,7 +308,10 @@ def main():
         # longest-processing-time split by the cost model (ksim.sweep.plan_costs): the long FGD replays spread
         # over the ranks, the totals balance
         exps = SW.shard(items, share_k, share_n, SW.plan_costs(items) if share_n > 1 else None)
-        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs, random_stream=args.random_stream)
+        # one workgroup per replica unless asked: every policy group then runs concurrently (FGD on k_hmemo, the
+        # cheap policies as one k_scan1_mix launch) whatever the share's size -- a share small enough for k_memo
+        # or k_replay at K > 1 would run its groups back to back (profiles/r05/c4_shares/)
+        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs or 1, random_stream=args.random_stream)
         eng = sweep.eng
         eng.total_events = sweep.total_events
         eng.memo_replicas = sweep.fgd_replicas()

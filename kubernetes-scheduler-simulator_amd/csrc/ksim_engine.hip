@@ -1710,11 +1710,9 @@ struct ksim_engine {
   // side streams for concurrent single-workgroup k_replay groups (created on first use)
   static constexpr int kSide = 6;
   hipStream_t side[kSide] = {};
-  int side_key[kSide] = {};
   int* h_started = nullptr;   // residency gate: host-mapped flags, one per FGD workgroup (hipHostMalloc)
   int* d_started = nullptr;   // its device address
   int started_cap = 0, gate_epoch = 0;   // how each side stream was created (plain 0, all-CU mask -1, CU range [0, k) k, complement -k)
-  int dev_cus = 256;          // the device's CUs (CU masks cover them all, whatever KSIM_CUS caps)
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
   bool report_done = false;
@@ -2085,7 +2083,7 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     pl.Mtab = pl.Mslots = 0;
     pl.mtoff.assign((size_t)Rg * KSIM_MAX_TYPES, 0);
     std::vector<std::vector<uint8_t>> mt(Rg);
-    for (int i = 0; on && i < Rg; ++i) {
+    for (int i = 0; on && pl.K == 1 && i < Rg; ++i) {  // (the wide form evaluates the whole table)
       const int r = reps[i];
       if (!e->reps[r].typed || e->h_tp[r].size() != (size_t)e->reps[r].nt) continue;
       const std::vector<TypDev>& tpv = e->h_tp[r];
@@ -2520,11 +2518,6 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     ma.pf = pf ? std::atoi(pf) & 7 : 1;  // (4: the wide form lists on wave 0 too)
   }
   ma.delay = hdelay_mask();
-  {  // F waves for the replicas with more than 64 typical pods (the rest of the 15 bulk waves run the class pass)
-    const char* fw = std::getenv("KSIM_HFW");
-    const int v = fw ? std::atoi(fw) : ksim_hmemo::kFW;
-    ma.fw_big = v >= 1 && v <= 13 ? v : ksim_hmemo::kFW;
-  }
   {  // KSIM_HPRUNE (A/B): the F list's group pruning for replicas with more than this many typical pods
     // (-1: every replica; default 64: the large typed tables, where the F rounds bound the step)
     const char* pr = std::getenv("KSIM_HPRUNE");
@@ -2563,7 +2556,10 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     ma.prof = e->d_h_prof;
   }
   const bool gen = profile || ma.delay != 0;  // the general instantiation: timers, stress delays
-  const void* f = pl.K == 1 ? (gen ? (const void*)k_hmemo<0, true> : (const void*)k_hmemo<0, false>)
+  // per-model tables (typed replicas at one workgroup per replica): the instantiations that read them
+  const bool model = pl.Mtab > 0;
+  const void* f = pl.K == 1 ? (gen ? (model ? (const void*)k_hmemo<0, true, true> : (const void*)k_hmemo<0, true>)
+                                   : (model ? (const void*)k_hmemo<0, false, true> : (const void*)k_hmemo<0, false>))
                   : pl.K <= 64 ? (gen ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
                                : (gen ? (const void*)k_hmemo<4, true> : (const void*)k_hmemo<4, false>);
   if (pl.K > 1 && Rg * pl.K > resident_cap(e, f, pl.lds)) {
@@ -2571,14 +2567,7 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     return KSIM_ERANGE;
   }
   const TypDev* tpp = e->d_tp;
-  // KSIM_HMEMO_EXCL=1 (K = 1): ask for a whole CU's LDS, so that no other group's workgroup shares a CU with a
-  // k_hmemo one (the paper sweep's concurrent groups)
-  size_t lds = pl.lds;
-  if (pl.K == 1) {
-    const char* ex = std::getenv("KSIM_HMEMO_EXCL");
-    if (ex && ex[0] == '1') lds = 160 * 1024;
-  }
-  const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, lds, st, e->coop && pl.K > 1, ma, tpp);
+  const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
   if (lrc) return lrc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
@@ -2682,7 +2671,6 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     hipDeviceProp_t prop;
     KSIM_HIP(hipGetDeviceProperties(&prop, dev));
     e->cus = prop.multiProcessorCount;
-    e->dev_cus = prop.multiProcessorCount;
     // KSIM_CUS: use at most this many CUs for co-resident persistent grids (a device shared with
     // another process; also the tests' way to exercise the residency checks)
     if (const char* c = std::getenv("KSIM_CUS")) e->cus = std::max(1, std::min(e->cus, std::atoi(c)));
@@ -3627,42 +3615,14 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipEventRecord(e->tev_fork, e->stream));
     }
   }
-  // KSIM_SIDE_CUMASK (A/B): 1 = every side stream with an all-CU mask (a hardware queue of its own);
-  // 2 = the first group (FGD on k_hmemo, one workgroup per replica) on CUs [0, Rg), the other groups on
-  // the rest, so the long FGD replays start at once instead of waiting for CUs the short groups hold.
-  // CU-masked streams are blocking streams (they order with the null stream; nothing here uses it).
-  int cm_mode = 0, cm_split = 0;
-  if (const char* cm = std::getenv("KSIM_SIDE_CUMASK")) cm_mode = std::atoi(cm);
-  if (concurrent && cm_mode == 2 && groups.size() >= 2 && groups[0].first == POL_FGD && e->hplan_ok && e->run_mode != 2)
-    cm_split = std::max(1, std::min(groups[0].second, e->dev_cus - 32));
   for (const auto& gp : groups) {
     const int Rg = gp.second;
     hipStream_t gs = e->stream;
     if (concurrent) {
       const int i = (gidx == 0 || nq == 1) ? 0 : 1 + (gidx - 1) % (nq - 1);
-      const int key = cm_split > 0 ? (i == 0 ? cm_split : -cm_split) : (cm_mode == 1 ? -1 : 0);
-      if (e->side[i] && e->side_key[i] != key) {  // created for another mask: recreate
-        KSIM_HIP(hipStreamSynchronize(e->side[i]));
-        KSIM_HIP(hipStreamDestroy(e->side[i]));
-        e->side[i] = nullptr;
-      }
       if (!e->side[i]) {
-        // KSIM_SIDE_PRIO=1: the first group's stream at the device's greatest priority, so that its workgroups
-        // are dispatched ahead of the short groups' (measured within C4's run-to-run spread: off by default)
-        const char* pr = std::getenv("KSIM_SIDE_PRIO");
-        int lo = 0, hi = 0;
-        if (key != 0) {
-          std::vector<uint32_t> mask((size_t)(e->dev_cus + 31) / 32, 0u);
-          for (int c = 0; c < e->dev_cus; ++c)
-            if (key == -1 || (key > 0 ? c < key : c >= -key)) mask[(size_t)c / 32] |= 1u << (c % 32);
-          KSIM_HIP(hipExtStreamCreateWithCUMask(&e->side[i], (uint32_t)mask.size(), mask.data()));
-        } else if (i == 0 && pr && pr[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
-          KSIM_HIP(hipStreamCreateWithPriority(&e->side[i], hipStreamNonBlocking, hi));
-        } else {
-          KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
-        }
-        e->side_key[i] = key;
-        if (!e->side_ev[i]) KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
+        KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
+        KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
       }
       gs = e->side[i];
       if (!(used & (1u << i))) KSIM_HIP(hipStreamWaitEvent(gs, e->ev_fork, 0));

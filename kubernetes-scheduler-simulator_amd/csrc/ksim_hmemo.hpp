@@ -112,7 +112,6 @@ struct HMemoArgs {
   int pf;                   // one workgroup per replica: 1 (default) = wave 0 lists the next refresh's F evaluations after its
                             // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
   int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
-  int fw_big;               // F waves of a replica with more than 64 typical pods (KSIM_HFW; kFW by default)
   int prune_t;              // list only the score groups some class of which may pass Filter on d (the group's
                             // PodDev holds the least demanding request: min CPU / memory, every accepted GPU
                             // model) for replicas with more than prune_t typical pods (KSIM_HPRUNE)
@@ -314,7 +313,7 @@ __device__ __forceinline__ void l12_update(unsigned& m1, unsigned& m2, unsigned 
 // workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the
 // KSIM_PROFILE phase timers and the KSIM_HDELAY stress delays (compiled out of the lean launches, as
 // k_memo's: the step loop's scalar registers are what it runs short of).
-template <int kSub, bool kProf>
+template <int kSub, bool kProf, bool kModel = false>
 __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __restrict__ tp_all, const int wg) {
   using namespace ksim_replay;
   using ksim_memo::gget;
@@ -392,7 +391,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
     if (use_l2) s_l2[i] = in ? a.l2[gix] : 0u;
   }
   for (int i = tid; i < rp.nt * 2; i += kHBlock) reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
-  if (a.Mtab > 0) {  // the per-model tables: copies of the entries they name (the table in HBM, as above)
+  if (kModel && a.Mtab > 0) {  // the per-model tables: copies of the entries they name (the table in HBM, as above)
     for (int i = tid; i < a.Mtab * 2; i += kHBlock)
       reinterpret_cast<uint4*>(s_ctp)[i] = reinterpret_cast<const uint4*>(tp + a.mtab[(size_t)gi * a.Mtab + i / 2])[i & 1];
     for (int m = tid; m < KSIM_MAX_TYPES; m += kHBlock) s_mto[m] = rp.typed ? a.mtoff[(size_t)gi * KSIM_MAX_TYPES + m] : 0;
@@ -426,10 +425,10 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   int bar_target = 0;  // the bulk barrier's count so far (waves 1-15)
   int cbar_target = 0; // the class waves' barrier count so far
   int list_seq = 0;    // refreshes whose F list wave 1 handed over (waves 1..fw)
-  // F waves (1..fw) and class waves (fw+1..15): kFW, or a.fw_big for a replica with more than 64 typical
-  // pods (the F rounds grow with the table, the class pass does not)
-  const int fw = rp.nt > 64 ? a.fw_big : kFW, cw = kHWaves - 1 - fw;
-  const bool prune = rp.nt > a.prune_t;
+  // F waves (1..fw) and class waves (fw+1..15); r04 measured 8-10 F waves for the large tables (KSIM_HFW, removed
+  // in r05) within C4's spread
+  const int fw = kFW, cw = kHWaves - 1 - fw;
+  const bool prune = kSub == 0 && rp.nt > a.prune_t;  // (one workgroup per replica only: the wide form keeps r04's list)
   // F of a candidate state of node n (fgd_candidate's cpuL / gs / total) by the quad of lane q.  A typed replica
   // with per-model tables evaluates only the CPU-only pods and the GPU pods that accept n's model: every other
   // GPU pod adds its freq x total to the NA bin and nothing else (GetNodePodFrag, frag.go:460-493), so the NA
@@ -437,7 +436,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   // of the model with that total: na[slot][total] (k_hinit_na).  Same bits as the whole table.
   auto state_F = [&](const NodeV& n, int cpuL, const uint32_t (&gs)[4], int total, int q) -> double {
     const uint32_t tb = 1u << n.gpu_type();
-    if (a.Mtab > 0) {
+    if constexpr (kModel) {  // (the instantiations without it -- the wide form, C5 -- keep r04's registers)
       const unsigned mw = (unsigned)s_mto[n.gpu_type()];
       if (mw & kMtPresent) {
         const double nav = a.na[((size_t)gi * a.Mslots + ((mw >> 21) & 31u)) * kNaStride + total];
@@ -1043,11 +1042,11 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   for (int i = tid; i < ns; i += kHBlock) store_node(rp.nodes + rank2idx[lo + i], load_node(&s_nodes[i]));
 }
 
-template <int kSub, bool kProf>
+template <int kSub, bool kProf, bool kModel = false>
 __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
   if (a.started != nullptr && threadIdx.x == 0)  // a vector store to host memory, system scope
     __hip_atomic_store(a.started + blockIdx.x, a.gate_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  hmemo_body<kSub, kProf>(a, tp_all, (int)blockIdx.x);
+  hmemo_body<kSub, kProf, kModel>(a, tp_all, (int)blockIdx.x);
 }
 
 // One launch over the shards of a node-sharded cluster on one device (ksim_shard_group_run): workgroup

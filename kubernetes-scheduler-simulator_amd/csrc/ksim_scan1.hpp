@@ -265,8 +265,10 @@ __global__ __launch_bounds__(kBlock) void k_scan1(Scan1Args a) {
 // Every cheap policy in one launch: workgroup b replays replica rep_list[b] under that replica's policy
 // (a uniform branch per workgroup).  The host lists the replicas longest stream first, so the launch
 // dispatches the long replays before the short ones fill in behind them.
+// Six waves per SIMD (80 VGPRs, no spills; the default register budget gave 91 and five): six replicas per CU
+// instead of five while the FGD group holds the rest of the CUs
 template <bool kReport, bool kReg>
-__global__ __launch_bounds__(kBlock) void k_scan1_mix(Scan1Args a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_scan1_mix(Scan1Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ReplicaDev rp = a.reps[a.rep_list[blockIdx.x]];
   switch (rp.policy) {

@@ -272,6 +272,8 @@ def lib():
             C.CDLL(rt, mode=C.RTLD_GLOBAL)  # the process's HIP runtime, before the library binds one
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("KSIM_LIB_PATH") and not hasattr(L, name):
+                continue  # an older library loaded for an A/B run: its missing entry points fail when called
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
