@@ -615,15 +615,30 @@ KSIM_HD int pwr_score(const NodeV& n, const PodDev& p, int cap, int cm, const Po
 // PWRScorePlugin.NormalizeScore (pwr_score.go:104-141)
 KSIM_HD int pwr_normalize(int s, int lo, int hi) { return lo == hi ? 100 : (int)((long long)(s - lo) * 100 / (hi - lo)); }
 
+// x / 125 correctly rounded for every integer-valued x with |x| < 2^31, without a division: the product
+// with RN(1/125), its exact remainder by an fma, one fma correction.  Checked against IEEE division for
+// every x in [0, 2^31) (tests/native/div125_check.c; the formula is odd in x); 3 fp64 operations instead
+// of the ~11 of a division.  kMaxSpecCpu = 125 x 2^10 and kMaxSpecGpu = 125 x 2^6, and scaling by a power
+// of two is exact, so x / kMaxSpec* = div125(x) x 2^-k bit for bit (const.go:16-18).
+KSIM_HD double div125(double x) {
+  const double r = 1.0 / 125.0;
+  const double q = x * r;
+  const double e = __builtin_fma(-q, 125.0, x);
+  return __builtin_fma(e, r, q);
+}
+KSIM_HD double div_spec_cpu(double x) { return div125(x) * 0x1p-10; }  // x / kMaxSpecCpu, |x| < 2^31 integer
+KSIM_HD double div_spec_gpu(double x) { return div125(x) * 0x1p-6; }   // x / kMaxSpecGpu, |x| < 2^31 integer
+static_assert(kMaxSpecCpu == 125 * 1024 && kMaxSpecGpu == 125 * 64, "div_spec_* assume these");
+
 // getBestFitScore (best_fit_score.go:66-97); -1 = error
 KSIM_HD int bestfit_score(const NodeV& n, const PodDev& p, int total) {
   const double f0 = (double)n.cpu_left, r0 = (double)p.cpu_nz;
   const double f1 = (double)total, r1 = (double)((int)p.milli * (int)p.num);
   double s = 0;
   if (f0 < r0) return -1;
-  s += (f0 - r0) / (double)kMaxSpecCpu * 0.5;
+  s += div_spec_cpu(f0 - r0) * 0.5;  // (f0 - r0) / MaxSpecCpu: an integer in [0, 2^31)
   if (f1 < r1) return -1;
-  s += (f1 - r1) / (double)kMaxSpecGpu * 0.5;
+  s += div_spec_gpu(f1 - r1) * 0.5;
   s = (1.0 - s) * (double)100;
   return (int)s;
 }
@@ -727,10 +742,11 @@ KSIM_HD int dotprod_cfg_score(const NodeV& n, const PodDev& p, int cap, int cfg,
 // dotprod_cfg_score's (the fast path of the scanning kernels; tests check the two agree).
 KSIM_HD int dotprod_merge_max(const NodeV& n, const PodDev& p) {
   if (n.cpu_left < p.cpu_nz) return 0;
-  const double a0 = (double)n.cpu_left / (double)kMaxSpecCpu;
-  const double a1 = (double)n.total() / (double)kMaxSpecGpu;
-  const double c0 = (double)p.cpu_nz / (double)kMaxSpecCpu;
-  const double c1 = (double)((int)p.milli * (int)p.num) / (double)kMaxSpecGpu;
+  // the quotients by div_spec_* (integers below 2^31: the same bits as the divisions)
+  const double a0 = div_spec_cpu((double)n.cpu_left);
+  const double a1 = div_spec_gpu((double)n.total());
+  const double c0 = div_spec_cpu((double)p.cpu_nz);
+  const double c1 = div_spec_gpu((double)((int)p.milli * (int)p.num));
   double cur = 0;
   cur += a0 * c0;
   cur += a1 * c1;
