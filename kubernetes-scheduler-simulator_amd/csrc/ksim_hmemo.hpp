@@ -428,7 +428,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   // F waves (1..fw) and class waves (fw+1..15); r04 measured 8-10 F waves for the large tables (KSIM_HFW, removed
   // in r05) within C4's spread
   const int fw = kFW, cw = kHWaves - 1 - fw;
-  const bool prune = kSub == 0 && rp.nt > a.prune_t;  // (one workgroup per replica only: the wide form keeps r04's list)
+  const bool prune = kSub == 0 && rp.nt > a.prune_t;  // (one workgroup per replica only: at C5 the pruned list measured slower)
   // F of a candidate state of node n (fgd_candidate's cpuL / gs / total) by the quad of lane q.  A typed replica
   // with per-model tables evaluates only the CPU-only pods and the GPU pods that accept n's model: every other
   // GPU pod adds its freq x total to the NA bin and nothing else (GetNodePodFrag, frag.go:460-493), so the NA
