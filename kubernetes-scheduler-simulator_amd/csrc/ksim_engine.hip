@@ -2556,8 +2556,10 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     ma.prof = e->d_h_prof;
   }
   const bool gen = profile || ma.delay != 0;  // the general instantiation: timers, stress delays
-  // per-model tables (typed replicas at one workgroup per replica): the instantiations that read them
-  const bool model = pl.Mtab > 0;
+  // the large-table instantiations (per-model tables of typed replicas, the F-list pruning) when a replica of
+  // the launch has use for them
+  bool model = pl.Mtab > 0;
+  for (const int r : e->mplan_reps) model = model || e->reps[r].nt > ma.prune_t;  // the FGD replicas
   const void* f = pl.K == 1 ? (gen ? (model ? (const void*)k_hmemo<0, true, true> : (const void*)k_hmemo<0, true>)
                                    : (model ? (const void*)k_hmemo<0, false, true> : (const void*)k_hmemo<0, false>))
                   : pl.K <= 64 ? (gen ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)

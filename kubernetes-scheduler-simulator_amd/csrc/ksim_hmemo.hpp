@@ -313,6 +313,8 @@ __device__ __forceinline__ void l12_update(unsigned& m1, unsigned& m2, unsigned 
 // workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the
 // KSIM_PROFILE phase timers and the KSIM_HDELAY stress delays (compiled out of the lean launches, as
 // k_memo's: the step loop's scalar registers are what it runs short of).
+// kModel: the instantiation for large typical tables -- the per-model tables (typed replicas) and the F-list
+// pruning (one workgroup per replica)
 template <int kSub, bool kProf, bool kModel = false>
 __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __restrict__ tp_all, const int wg) {
   using namespace ksim_replay;
@@ -428,7 +430,9 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   // F waves (1..fw) and class waves (fw+1..15); r04 measured 8-10 F waves for the large tables (KSIM_HFW, removed
   // in r05) within C4's spread
   const int fw = kFW, cw = kHWaves - 1 - fw;
-  const bool prune = kSub == 0 && rp.nt > a.prune_t;  // (one workgroup per replica only: at C5 the pruned list measured slower)
+  // (the instantiations for large tables only: compiled into the wide form it measured slower at C5, and into
+  // the lean untyped one it cost C2 run_mode 5 registers)
+  const bool prune = kModel && rp.nt > a.prune_t;
   // F of a candidate state of node n (fgd_candidate's cpuL / gs / total) by the quad of lane q.  A typed replica
   // with per-model tables evaluates only the CPU-only pods and the GPU pods that accept n's model: every other
   // GPU pod adds its freq x total to the NA bin and nothing else (GetNodePodFrag, frag.go:460-493), so the NA
