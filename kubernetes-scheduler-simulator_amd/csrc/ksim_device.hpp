@@ -465,6 +465,33 @@ KSIM_HD bool filter_node(const NodeV& n, const PodDev& p) {
   return slots >= p.num;
 }
 
+// filter_node's decisions without its early returns (k_scan1's per-slot scan: there the return chain diverged per
+// lane, each exit an exec-mask branch).  The pod's fields are uniform in a scan, so only its branches remain.
+KSIM_HD bool filter_scan(const NodeV& n, const PodDev& p) {
+  bool ok = n.pods_left() >= 1;
+  const bool zero = p.cpu_req == 0 && p.mem == 0;
+  ok = ok & (zero | ((n.cpu_left >= p.cpu_req) & (n.mem_left >= p.mem)));
+  if (p.milli > 0) {
+    const int cnt = n.gpu_cnt();
+    bool dev = (cnt != 0) & (((p.tmask >> n.gpu_type()) & 1u) != 0u) & (p.num > 0);
+    if (p.num == 1) {
+      bool any = false;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g) any = any | ((g < cnt) & (n.gl(g) >= p.milli));
+      dev = dev & any;
+    } else if (p.milli == kMilli) {
+      int slots = 0;
+#pragma unroll
+      for (int g = 0; g < kMaxGpu; ++g) slots += ((g < cnt) & (n.gl(g) == kMilli)) ? 1 : 0;
+      dev = dev & (slots >= p.num);
+    } else {
+      dev = dev & filter_node(n, p);  // a partial multi-GPU request (no trace has one)
+    }
+    ok = ok & dev;
+  }
+  return ok;
+}
+
 KSIM_HD bool is_share_pod(const PodDev& p) { return p.num == 1 && p.milli < kMilli; }
 
 // GPUs selected by NodeResource.Sub (resource.go:454-480): ascending stable
@@ -842,6 +869,11 @@ KSIM_HD uint32_t key_rank(unsigned long long k) { return 0xFFFFFFu - (uint32_t)(
 KSIM_HD int key_gpu(unsigned long long k) { return (int)((k >> 12) & 0xFu) - 1; }
 KSIM_HD int key_loc(unsigned long long k) { return (int)(k & 0xFFFu); }
 constexpr int kMaxRank = 0xFFFFFF;  // name ranks must stay below (N < 2^24)
+// BestFit's raw score leaves [0, 100] downwards on a node with more CPU left than MaxSpecCpu, and only -1 is a
+// Score error (best_fit_score.go:48-51,76-96).  Its raw scores travel biased by kBfKeyBias (> -2^23 for CPU below
+// 2^31), so the key field and the min / max accumulators see non-negative values.  NormalizeScore maps only the
+// max raw score to 100 whatever the range (plugin_utils.go:48-74), so the raw argmax is the normalized one.
+constexpr int kBfKeyBias = 1 << 23;
 constexpr int kMaxSlice = 0xFFF;    // slots per k_replay workgroup
 
 }  // namespace ksim

@@ -225,12 +225,14 @@ __device__ __forceinline__ int cheap_score(const NodeV& n, const PodDev& p, uint
   *err = false;
   if constexpr (kPol == POL_BESTFIT) {
     const int r = bestfit_score(n, p, n.total());
-    if (r < 0) { *err = true; return 0; }
-    return r;
+    if (r == -1) { *err = true; return kBfKeyBias; }
+    return r + kBfKeyBias;  // biased (kBfKeyBias)
   } else if constexpr (kPol == POL_DOTPROD) {
-    if (dpcfg == (DIM_MERGE | NORM_MAX << 4)) return dotprod_merge_max(n, p);  // uniform per replica
     int gid = 0;
-    return dotprod_cfg_score(n, p, cap, dpcfg, &gid);
+    // uniform per replica
+    const int r = dpcfg == (DIM_MERGE | NORM_MAX << 4) ? dotprod_merge_max(n, p) : dotprod_cfg_score(n, p, cap, dpcfg, &gid);
+    *err = r < 0 || r > 100;  // no NormalizeScore: the framework's range check (framework.go:686-704)
+    return r;
   } else if constexpr (kPol == POL_PACKING) {
     bool perr = false;
     const int r = p.milli <= 0 ? 0 : packing_score(n, p, &perr);
@@ -263,11 +265,13 @@ __device__ __forceinline__ bool node_phase1(const NodeV& n, const PodDev& p, con
       break;
     case POL_BESTFIT:
       *raw = bestfit_score(n, p, total);
-      if (*raw < 0) { *err = true; *raw = 0; }
+      *err = *raw == -1;
+      *raw = (*err ? 0 : *raw) + kBfKeyBias;  // biased (kBfKeyBias)
       break;
     case POL_DOTPROD: {  // any dimExtMethod / normMethod; *pgpu: the best group's GPU mask
       int gid = 0;
       *raw = dotprod_cfg_score(n, p, rp.cap[node], rp.dpcfg, &gid);
+      *err = *raw < 0 || *raw > 100;  // no NormalizeScore: the framework's range check
       if (pgpu) *pgpu = gid;
       break;
     }
@@ -705,7 +709,7 @@ void k_replay(ksim_replay::ReplayArgs a,
   constexpr bool kPF = kPol == POL_PWR_FGD;
   constexpr bool kFgd = kPol == POL_FGD || kPF;  // the FGD candidate evaluation
   constexpr bool kMinMax = kPol == POL_BESTFIT;  // NormalizeScore needs the raw min / max
-  constexpr bool kErr = kPol == POL_BESTFIT || kPol == POL_PACKING || kPol == POL_CLUSTERING || kPwr || kPF;
+  constexpr bool kErr = kPol == POL_BESTFIT || kPol == POL_DOTPROD || kPol == POL_PACKING || kPol == POL_CLUSTERING || kPwr || kPF;
   // all LDS is dynamic (no static __shared__ in front of it), carved 16-byte aligned
   extern __shared__ __attribute__((aligned(16))) char smem[];
   ReplayShared& sh = *reinterpret_cast<ReplayShared*>(smem);
@@ -933,11 +937,14 @@ void k_replay(ksim_replay::ReplayArgs a,
       const int cj = (int)(st & 0x1ffff);
       c += cj;
       e1 = e1 || (st >> 31) != 0u;
-      if (kMinMax && cj > 0) {
-        lo = min(lo, (int)((st >> 17) & 0x7f));
-        hi = max(hi, (int)((st >> 24) & 0x7f));
-      }
       const unsigned long long kj = in ? ((g.g1[j] & 0xffffffffull) << 32) | (g.g0[j] & 0xffffffffull) : 0ull;
+      if (kMinMax && cj > 0) {
+        // BestFit: a slice's max raw score is its key's score field; its bit 17 says whether its scores differ.
+        // NormalizeScore needs only whether any two feasible scores differ (result_score: hi > lo).
+        const int sj = key_score(kj);
+        lo = min(lo, sj - (int)((st >> 17) & 1u));
+        hi = max(hi, sj);
+      }
       best = kj > best ? kj : best;
     }
     *gc = wave_sum_dpp(c);
@@ -1435,8 +1442,8 @@ void k_replay(ksim_replay::ReplayArgs a,
           if (a.K > 1) {
             unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
             const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-            const unsigned stat = ((unsigned)e << 31) | ((unsigned)(h < 0 ? 0 : h) & 0x7f) << 24 |
-                                  ((unsigned)(l > 127 ? 127 : l) & 0x7f) << 17 | ((unsigned)c & 0x1ffff);
+            // bit 17 (BestFit): the slice's feasible raw scores are not all equal (its max is mk's score)
+            const unsigned stat = ((unsigned)e << 31) | (l < h ? 1u << 17 : 0u) | ((unsigned)c & 0x1ffff);
             gstore(slot + (size_t)w * kGranW + 0, tag | (mk & 0xffffffffull));
             gstore(slot + (size_t)w * kGranW + 1, tag | (mk >> 32));
             gstore(slot + (size_t)w * kGranW + 2, tag | stat);
@@ -3649,8 +3656,9 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       continue;
     }
     if (gp.first == ksim_scan1::kPolMix) {
-      const void* f = e->report ? (reg1 ? (const void*)ksim_scan1::k_scan1_mix<true, true> : (const void*)ksim_scan1::k_scan1_mix<true, false>)
-                                : (reg1 ? (const void*)ksim_scan1::k_scan1_mix<false, true> : (const void*)ksim_scan1::k_scan1_mix<false, false>);
+      using namespace ksim_scan1;
+      const void* f = e->report ? (reg1 ? (const void*)k_scan1_mix<true, true> : (const void*)k_scan1_mix<true, false>)
+                                : (reg1 ? (const void*)k_scan1_mix<false, true> : (const void*)k_scan1_mix<false, false>);
       const size_t lds = ksim_scan1::scan1_lds(e->N, ksim_scan1::kPolMix, e->report, reg1);
       ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N,
                                dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0};

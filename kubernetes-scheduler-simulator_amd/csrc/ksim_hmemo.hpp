@@ -441,7 +441,8 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   auto state_F = [&](const NodeV& n, int cpuL, const uint32_t (&gs)[4], int total, int q) -> double {
     const uint32_t tb = 1u << n.gpu_type();
     if constexpr (kModel) {  // (the instantiations without it -- the wide form, C5 -- keep r04's registers)
-      const unsigned mw = (unsigned)s_mto[n.gpu_type()];
+      // (a launch of this instantiation for the pruning alone has no tables: s_mto is then not allocated)
+      const unsigned mw = a.Mtab > 0 ? (unsigned)s_mto[n.gpu_type()] : 0u;
       if (mw & kMtPresent) {
         const double nav = a.na[((size_t)gi * a.Mslots + ((mw >> 21) & 31u)) * kNaStride + total];
         const double F = frag_F_quad<false>(cpuL, gs, total, tb, tp, s_ctp + (mw & 0xfffu), rp.ncpu, (int)((mw >> 12) & 0x1ffu), q);
@@ -600,7 +601,11 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         }
         const int nit = __builtin_amdgcn_readfirstlane(sh.nitems[cur]);
         const int q = bt & 3;
-        for (int j = bt >> 2; j < nit; j += fw * 16) {
+        // (r05 tried the items round robin over the F waves, so that a short list keeps every SIMD busy: C5
+        // 4.25 -> 4.57 s, C2 run_mode 5 48.7 -> 52.6 ms -- the class waves beside the idle F waves lost their
+        // issue slots; profiles/r05/hmemo/ab_r05c18_round_robin.txt)
+        const int j0 = bt >> 2;
+        for (int j = j0; j < nit; j += fw * 16) {
           const int code = s_code[j];
           const PodDev gp = s_gpod[s_igrp[j]];
           int cpuL, total;
@@ -622,7 +627,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (q == 0) {
           const double F0k = s_F[0];
-          for (int j = bt >> 2; j < nit; j += fw * 16) {
+          for (int j = j0; j < nit; j += fw * 16) {  // (the items this quad evaluated)
             if (j == 0) continue;
             const int code = s_code[j];
             const unsigned x =

@@ -141,7 +141,7 @@ __device__ __forceinline__ void scan1_body(const Scan1Args& a, const ReplicaDev&
     int cnt = 0, lo = 0x7fffffff, hi = -1;
     bool err = false;
     auto visit = [&](const NodeV& n, int i) {
-      if (filter_node(n, p)) {
+      if (filter_scan(n, p)) {
         bool e1 = false;
         int raw;
         if constexpr (kTags) {
@@ -149,6 +149,7 @@ __device__ __forceinline__ void scan1_body(const Scan1Args& a, const ReplicaDev&
           raw = e1 ? 0 : clustering_score_mask(s_tm[i], p.tag, n.total());
         } else if constexpr (kPol == POL_DOTPROD && kDpMM) {
           raw = dotprod_merge_max(n, p);
+          e1 = raw < 0;  // the framework's range check (<= 100 always)
         } else {
           const int cap = (kPol == POL_DOTPROD && dp_norm(rp.dpcfg) == NORM_NODE) ? rp.cap[i] : 0;
           raw = cheap_score<kPol>(n, p, rp.seed, nullptr, step, &e1, rp.dpcfg, cap);

@@ -143,6 +143,13 @@ int dm_filter(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_
   p.mem = mem;
   return filter_node(mk(cpu_left, mem_left, gl8, gpu_cnt, type_id, pods_left), p) ? 1 : 0;
 }
+// k_scan1's branch-free form of the same Filter
+int dm_filter_scan(int cpu_left, int mem_left, const int* gl8, int gpu_cnt, int type_id, int pods_left, int cpu, int mem,
+                   int milli, int num, unsigned mask) {
+  PodDev p = pod(cpu, milli, num, mask);
+  p.mem = mem;
+  return filter_scan(mk(cpu_left, mem_left, gl8, gpu_cnt, type_id, pods_left), p) ? 1 : 0;
+}
 
 int dm_bestfit(int cpu_left, const int* gl8, int gpu_cnt, int cpu, int milli, int num) {
   const NodeV n = mk(cpu_left, 0, gl8, gpu_cnt, 0, 1);

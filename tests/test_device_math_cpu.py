@@ -31,6 +31,7 @@ def dm():
                                C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int)]
     L.dm_filter.argtypes = [C.c_int, C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                             C.c_uint]
+    L.dm_filter_scan.argtypes = L.dm_filter.argtypes
     L.dm_bestfit.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
     L.dm_dotprod.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
     L.dm_dotprod_mm.argtypes = [C.c_int, I8, C.c_int, C.c_int, C.c_int, C.c_int]
@@ -241,3 +242,35 @@ def test_go_tanh_host_equals_oracle(dm):
         assert a == b or (a != a and b != b), x
     # Go's tanh: exact at 0 and saturated beyond 0.5 * log(2**127)
     assert O.go_tanh(50.0) == 1.0 and O.go_tanh(-50.0) == -1.0
+
+
+def test_filter_scan_equals_filter_node(dm):
+    # k_scan1's branch-free Filter (filter_scan) against filter_node, which every other path and the GPU parity
+    # tests check against the oracle: every corner -- no pod slot left, zero requests, CPU / memory at and past
+    # the boundary, GPU-less nodes, a model the pod does not accept, share / whole / partial multi-GPU requests
+    rnd = random.Random(11)
+    n = 0
+    for _ in range(40000):
+        cnt = rnd.choice([0, 1, 2, 4, 8])
+        gl = rand_gl(rnd, cnt) if cnt else [0] * 8
+        cpu_left = rnd.choice([0, 50, 100, 1000, 4000, 32000, 96000, -5])
+        mem_left = rnd.choice([0, 100, 1024, 10 ** 6])
+        pods_left = rnd.choice([0, 1, 5])
+        ty = rnd.randrange(len(TYPES))
+        cpu = rnd.choice([0, 100, 1000, 4000, 32000, 96000])
+        mem = rnd.choice([0, 100, 1024])
+        k = rnd.random()
+        if k < 0.2:
+            milli, num = 0, 0
+        elif k < 0.6:
+            milli, num = rnd.choice([100, 250, 500, 999, 1000]), 1
+        elif k < 0.85:
+            milli, num = 1000, rnd.choice([2, 4, 8])
+        else:
+            milli, num = rnd.choice([300, 500]), rnd.choice([0, 2, 3])
+        mask = rnd.choice([0xFFFFFFFF, 1 << ty, 1 << ((ty + 1) % len(TYPES)), 0])
+        args = (cpu_left, mem_left, (C.c_int * 8)(*gl), cnt, ty, pods_left, cpu, mem, milli, num, mask)
+        a, b = dm.dm_filter(*args), dm.dm_filter_scan(*args)
+        assert a == b, args
+        n += a
+    assert 1000 < n < 39000  # both outcomes well represented

@@ -138,3 +138,56 @@ def test_clustering_resumes_from_a_state_with_tags(trace, monkeypatch):
     tail, _ = run(mid, tail_events, rp.n - k)
     assert head == full[:k]
     assert [r[1:] for r in tail] == [r[1:] for r in full[k:]] and [r[0] for r in tail] == [r[0] for r in full[k:]]
+
+
+@pytest.mark.parametrize("path", ["mix", "scan1", "replay", "replay-k4", "step"])
+def test_nodes_beyond_max_spec_cpu(trace, path, monkeypatch):
+    # nodes with more CPU than MaxSpecCpu (128 cores): BestFit's raw scores go below 0 (only -1 is a Score error,
+    # best_fit_score.go:48-51; NormalizeScore spans any range) and DotProduct's can too (no NormalizeScore: the
+    # framework's [0, 100] range check fails the cycle).  Every path -- k_scan1_mix, k_scan1 per policy, k_replay at one and four workgroups per replica (the
+    # slices' exchange), k_step -- equals the oracle event by event.
+    monkeypatch.setenv("KSIM_SCAN1_MIX", "1" if path == "mix" else "0")
+    monkeypatch.setenv("KSIM_SCAN1", "0" if path.startswith("replay") else "2")
+    rp = trace.replay(seed=47)
+    arr, n = trace.typical()
+    n_ev = 1500
+    big = {i: (400000 if i % 6 == 0 else 150000) for i in range(0, trace.num_nodes, 3)}
+    nodes = helpers.subset_nodes(rp, list(range(trace.num_nodes)))
+    onodes = helpers.oracle_nodes(trace, rp)
+    for i, c in big.items():
+        nodes[i].cpu_alloc_milli = c
+        onodes[i] = dict(onodes[i], cpu=c)
+    names = [("BestFit", O.POL_BESTFIT), ("DotProd", O.POL_DOTPROD), ("GpuPacking", O.POL_PACKING)]
+    got = []
+    if path == "step":  # plugin-level calls: one replica per engine
+        for name, _ in names:
+            eng = ksim.Engine(trace.num_nodes, 1, run_mode=1)
+            try:
+                eng.set_nodes(0, nodes)
+                eng.set_typical(0, arr, n)
+                eng.set_policy(0, name, seed=SEED)
+                eng.load_events(0, rp.events, n_ev)
+                eng.run()
+                got.append(eng.results(0))
+            finally:
+                eng.close()
+    else:
+        eng = ksim.Engine(trace.num_nodes, len(names), wgs_per_replica=4 if path == "replay-k4" else 1)
+        try:
+            for r, (name, _) in enumerate(names):
+                eng.set_nodes(r, nodes)
+                eng.set_typical(r, arr, n)
+                eng.set_policy(r, name, seed=SEED)
+                eng.load_events(r, rp.events, n_ev)
+            eng.run()
+            if path == "mix":
+                assert eng.last_run_launches() == (1, 1)
+            got = [eng.results(r) for r in range(len(names))]
+        finally:
+            eng.close()
+    for r, (name, pol) in enumerate(names):
+        want, _, _ = O.run_events(onodes, helpers.oracle_typical(trace), helpers.oracle_events(trace, rp, n_ev),
+                                  policy=pol, gpu_sel=O.SEL_BEST, seed=SEED, threads=16)
+        bad = [i for i, (a, b) in enumerate(zip(got[r], want)) if a != b]
+        assert len(got[r]) == len(want) and not bad, (name, bad[:1], got[r][bad[0]] if bad else None,
+                                                      want[bad[0]] if bad else None)
