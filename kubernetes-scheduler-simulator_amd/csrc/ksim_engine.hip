@@ -736,6 +736,9 @@ void k_replay(ksim_replay::ReplayArgs a,
   int* s_last = reinterpret_cast<int*>(smem + L.last);
   int* s_praw = reinterpret_cast<int*>(smem + L.praw);  // PWR+FGD per-slot scratch of the current step
   int* s_pinf = reinterpret_cast<int*>(smem + L.pinf);
+  // PWR+FGD: each class's two most recent cluster-wide raw PWR ranges {lo0, hi0, lo1, hi1} (most recent first;
+  // classes alias mod kPfGuess -- a guess only ever saves a round, the decision checks it)
+  int4* s_gtab = reinterpret_cast<int4*>(smem + L.gtab);
   // PWR+FGD memo (a.pm_c > 0): every class's Filter + Score of every real slot, kept while the slot's
   // record is unchanged (s_pver), so a step evaluates only the slots changed since its class last came
   // and the virtual slot
@@ -767,6 +770,8 @@ void k_replay(ksim_replay::ReplayArgs a,
     for (int i = tid; i < ns; i += kRBlock) s_pe[i] = energy_static(rp.cap[n_lo + i], rp.cpum[n_lo + i], *rp.pw);
     for (int i = tid; i <= ns; i += kRBlock) s_E0[i] = kEnergyStale;
   }
+  if (kPF)
+    for (int i = tid; i < kPfGuess; i += kRBlock) s_gtab[i] = make_int4(1, 0, 1, 0);  // lo > hi: never a range
   if (pmon) {
     for (int i = tid; i <= ns; i += kRBlock) s_pver[i] = a.pm_ver0;
     for (int i = tid; i < a.pm_c * a.S; i += kRBlock) s_pm[i] = make_uint2(0u, kPmInvalid << 18);
@@ -778,6 +783,7 @@ void k_replay(ksim_replay::ReplayArgs a,
   }
   auto reset_agg = [&]() {
     sh.agg_key = 0ull;
+    sh.agg_key1 = 0ull;
     sh.agg_cnt = 0;
     sh.agg_err = 0;
     sh.agg_lo = 0x7fffffff;
@@ -819,45 +825,25 @@ void k_replay(ksim_replay::ReplayArgs a,
       }
     }
   };
-  // Wave 0, PWR+FGD: the A round of the current step (seq), published BEFORE the pending key round
-  // completes, so that its hand-off overlaps that one.  This slice's aggregate without the pending best
-  // node b -- min / max raw PWR score, feasible count, Score error -- and b's raw score both as it is
-  // (pre) and as the pending Bind leaves it (post, the virtual slot): granules 4-6 and 3, 7.  Once the key
-  // round names its winner every workgroup reduces all K, taking post for the winner's slice when the
-  // pending step binds, pre for every other (collect_a).  The slots are safe to reuse two steps later for
-  // the same reason as the key round's.
-  struct AVar { int c0, e0, l0, h0, fpre, epre, rpre, fpost, epost, rpost; };
-  auto a_total = [](const AVar& v, bool post, int* c, int* e, int* l, int* h) {
-    const int f = post ? v.fpost : v.fpre, ev = post ? v.epost : v.epre, rv = post ? v.rpost : v.rpre;
-    *c = v.c0 + f;
-    *e = v.e0 | (f & ev);
-    *l = f ? min(v.l0, rv) : v.l0;
-    *h = f ? max(v.h0, rv) : v.h0;
-  };
-  auto publish_a = [&](const AVar& v) {
-    unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW + (size_t)w * kGranW;
-    const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-    gstore(slot + 4, tag | (unsigned)v.l0);
-    gstore(slot + 5, tag | (unsigned)v.h0);
-    gstore(slot + 6, tag | ((unsigned)v.e0 << 31) | ((unsigned)v.fpre << 30) | ((unsigned)v.epre << 29) |
-                         ((unsigned)v.fpost << 28) | ((unsigned)v.epost << 27) | ((unsigned)v.c0 & 0x7ffffffu));
-    gstore(slot + 3, tag | (unsigned)v.rpre);
-    gstore(slot + 7, tag | (unsigned)v.rpost);
-  };
-  auto collect_a = [&](int kstar, bool bind, int* gc, int* ge, int* gl, int* gh) -> bool {
-    const unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
-    const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-    unsigned long long x[kS][5];
+  // Wave 0, PWR+FGD: ONE round per pod step.  NormalizeScore needs the cluster-wide min / max raw PWR score
+  // before any node's weighted total exists; instead of a round for it and then a key round, every slice
+  // publishes its A totals (min, max, feasible count | Score error: words 4-6) together with its best key under
+  // each of the two ranges last seen for the pod's class (words 0-1, 2-3).  When the true range is one of them
+  // (or at most one node is feasible: no normalisation), that key column decides; else every slice re-keys
+  // the step under the true range from its scratch (kept two steps) and a miss round (words 7-8) decides.
+  // The round overlaps the next pod's evaluation like every policy's key round.
+  // (x: an earlier poll when `have`, issued before the evaluation's last barrier so its latency overlaps the wait)
+  auto pf_collect = [&](unsigned long long (&x)[kS][7], bool have, int* gc, int* ge, int* gl, int* gh,
+                        unsigned long long* W0, unsigned long long* W1) -> bool {
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
     auto load = [&]() {
 #pragma unroll
       for (int j = 0; j < kS; ++j) {
         const int k = lane + 64 * j;
         if (k < a.K) {
-          x[j][0] = gload(slot + (size_t)k * kGranW + 4);
-          x[j][1] = gload(slot + (size_t)k * kGranW + 5);
-          x[j][2] = gload(slot + (size_t)k * kGranW + 6);
-          x[j][3] = gload(slot + (size_t)k * kGranW + 3);
-          x[j][4] = gload(slot + (size_t)k * kGranW + 7);
+#pragma unroll
+          for (int q = 0; q < 7; ++q) x[j][q] = gload(slot + (size_t)k * kGranW + q);
         }
       }
     };
@@ -867,9 +853,70 @@ void k_replay(ksim_replay::ReplayArgs a,
       for (int j = 0; j < kS; ++j) {
         bool t = true;
 #pragma unroll
-        for (int q = 0; q < 5; ++q) t = t && (x[j][q] & ~0xffffffffull) == tag;
+        for (int q = 0; q < 7; ++q) t = t && (x[j][q] & ~0xffffffffull) == tag;
         r = r && (lane + 64 * j >= a.K || t);
       }
+      return r;
+    };
+    if (!have) load();
+    unsigned spins = 0;
+    bool ok = true;
+    while (!__all(ready())) {
+      if (++spins > kSpinLimit) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+      load();
+    }
+    if (prof && lane == 0) sh.prof[8] += spins;
+    int cs = 0, lo = INT_MAX, hi = INT_MIN, e1 = 0;
+    unsigned long long b0 = 0ull, b1 = 0ull;
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+      if (lane + 64 * j < a.K) {
+        const unsigned long long k0 = ((x[j][1] & 0xffffffffull) << 32) | (x[j][0] & 0xffffffffull);
+        const unsigned long long k1 = ((x[j][3] & 0xffffffffull) << 32) | (x[j][2] & 0xffffffffull);
+        const unsigned st = (unsigned)x[j][6];
+        const int c = (int)(st & 0x7fffffffu);
+        cs += c;
+        e1 |= (int)(st >> 31);
+        if (c > 0) {
+          lo = min(lo, (int)(unsigned)x[j][4]);
+          hi = max(hi, (int)(unsigned)x[j][5]);
+        }
+        b0 = k0 > b0 ? k0 : b0;
+        b1 = k1 > b1 ? k1 : b1;
+      }
+    }
+    *gc = wave_sum_dpp(cs);
+    *ge = __any(e1 != 0) ? 1 : 0;
+    *gl = wave_min_dpp(lo);
+    *gh = wave_max_dpp(hi);
+    *W0 = wave_max_u64_dpp(b0);
+    *W1 = wave_max_u64_dpp(b1);
+    return ok;
+  };
+  auto pf_miss_round = [&](unsigned long long mine, unsigned long long* W) -> bool {
+    unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
+    if (lane == 0) {
+      gstore(slot + (size_t)w * kGranW + 7, tag | (mine & 0xffffffffull));
+      gstore(slot + (size_t)w * kGranW + 8, tag | (mine >> 32));
+    }
+    unsigned long long x0[kS], x1[kS];
+    auto load = [&]() {
+#pragma unroll
+      for (int j = 0; j < kS; ++j) {
+        const int k = lane + 64 * j;
+        if (k < a.K) {
+          x0[j] = gload(slot + (size_t)k * kGranW + 7);
+          x1[j] = gload(slot + (size_t)k * kGranW + 8);
+        }
+      }
+    };
+    auto ready = [&]() {
+      bool r = true;
+#pragma unroll
+      for (int j = 0; j < kS; ++j)
+        r = r && (lane + 64 * j >= a.K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
       return r;
     };
     load();
@@ -880,27 +927,14 @@ void k_replay(ksim_replay::ReplayArgs a,
       __builtin_amdgcn_s_sleep(1);
       load();
     }
-    int cs = 0, lo = INT_MAX, hi = INT_MIN, e1 = 0;
+    unsigned long long b = 0ull;
 #pragma unroll
-    for (int j = 0; j < kS; ++j) {
-      const int k = lane + 64 * j;
-      if (k < a.K) {
-        const unsigned st = (unsigned)x[j][2];
-        const AVar v{(int)(st & 0x7ffffffu), (int)(st >> 31), (int)(unsigned)x[j][0], (int)(unsigned)x[j][1],
-                     (int)((st >> 30) & 1u), (int)((st >> 29) & 1u), (int)(unsigned)x[j][3],
-                     (int)((st >> 28) & 1u), (int)((st >> 27) & 1u), (int)(unsigned)x[j][4]};
-        int c, e, l, h;
-        a_total(v, bind && k == kstar, &c, &e, &l, &h);
-        cs += c;
-        e1 |= e;
-        lo = min(lo, l);
-        hi = max(hi, h);
+    for (int j = 0; j < kS; ++j)
+      if (lane + 64 * j < a.K) {
+        const unsigned long long k = ((x1[j] & 0xffffffffull) << 32) | (x0[j] & 0xffffffffull);
+        b = k > b ? k : b;
       }
-    }
-    *gc = wave_sum_dpp(cs);
-    *ge = __any(e1 != 0) ? 1 : 0;
-    *gl = wave_min_dpp(lo);
-    *gh = wave_max_dpp(hi);
+    *W = wave_max_u64_dpp(b);
     return ok;
   };
   // Wave 0: the pending step's exchange result -- every workgroup's granules (K > 1) or
@@ -1006,16 +1040,135 @@ void k_replay(ksim_replay::ReplayArgs a,
     }
   };
 
+  // PWR+FGD: a feasible slot's packed key under the range [lo, hi]: w_pwr * NormalizeScore(PWR) + w_fgd * FGD
+  // (framework.go:686-704; unsigned arithmetic: a guessed range that is not the step's may give any value, and
+  // is then never used)
+  auto pf_key = [&](int praw, int inf, int lo, int hi, int i) -> unsigned long long {
+    // pwr_normalize in 32 bits: on the step's true range 0 <= praw - lo <= hi - lo < 2^24, so (praw - lo) * 100 < 2^31
+    const unsigned norm = lo == hi ? 100u : (unsigned)(praw - lo) * 100u / (unsigned)(hi - lo);
+    const unsigned total = (unsigned)rp.w_pwr * norm + (unsigned)rp.w_fgd * (unsigned)(inf & 0xff);
+    const int kg = rp.gpusel == SEL_PWR ? ((inf >> 8) & 0xf) - 1 : ((inf >> 12) & 0xf) - 1;
+    return pack_key(total, load_node(&s_nodes[i]).name_rank, kg, i);
+  };
+  // Wave 0: the pending step's best key of this slice under the true range, from its scratch
+  auto pf_rekey = [&](int lo, int hi) -> unsigned long long {
+    const int* q_praw = s_praw + (p_step & 1) * (a.S + 1);
+    const int* q_pinf = s_pinf + (p_step & 1) * (a.S + 1);
+    unsigned long long b = 0ull;
+    for (int i = lane; i < ns; i += 64) {
+      const int inf = q_pinf[i];
+      if (inf & kPfFeas) {
+        const unsigned long long k = pf_key(q_praw[i], inf, lo, hi, i);
+        b = k > b ? k : b;
+      }
+    }
+    return wave_max_u64_dpp(b);
+  };
+  // Wave 0: decide and commit the pending step.  The owner of the winner applies the virtual node when the winner
+  // is the node it prepared (guess 0's local best), else Reserve + Bind on the winner's slot itself; `overlapped`:
+  // this step's evaluation already ran, and *redo asks for it again (one of its slots changed under it).
+  auto pf_resolve = [&](unsigned long long (&x)[kS][7], bool have, bool overlapped, bool* redo) -> bool {
+    *redo = false;
+    int gc = p_st0, ge = p_st1, gl = p_st2, gh = p_st3;
+    const unsigned long long p_key1 = sh.pf_key1;
+    const int4 p_g = sh.pf_g;
+    unsigned long long W0 = p_key, W1 = p_key1;
+    if (a.K > 1 && !pf_collect(x, have, &gc, &ge, &gl, &gh, &W0, &W1)) return false;
+    const bool m0 = gc <= 1 || (gl == p_g.x && gh == p_g.y);  // at most one feasible node: no normalisation
+    const bool m1 = !m0 && gl == p_g.z && gh == p_g.w;
+    unsigned long long W = m0 ? W0 : W1, mine = m0 ? p_key : p_key1;
+    if (!m0 && !m1 && !ge) {  // (a Score error aborts the cycle: no winner needed)
+      if (prof && lane == 0) sh.prof[9] += 1ull;  // KSIM_PROFILE: misses (low half), re-evaluations (high)
+      mine = pf_rekey(gl, gh);
+      W = mine;
+      if (a.K > 1 && !pf_miss_round(mine, &W)) return false;
+    }
+    if (gc > 1 && lane == 0) {  // the class's most recent ranges (every workgroup updates alike)
+      int4& t = s_gtab[p_cls & (kPfGuess - 1)];
+      if (!(t.x == gl && t.y == gh)) t = make_int4(gl, gh, t.x, t.y);
+    }
+    // commit
+    const bool owner = W != 0ull && W == mine;
+    if (a.skip && gc == 0 && lane == 0) sh.dead[p_cls >> 5] |= 1u << (p_cls & 31);
+    ResultDev out{-1, 0, 0, gc, ST_UNSCHED};
+    int2 hrec = make_int2(-1, 0);
+    bool writer = w == 0;
+    if (gc > 0) {
+      out.status = (gc > 1 && ge) ? ST_ERROR : ST_OK;  // framework.go:650-656: a Score error aborts
+      if (out.status == ST_OK) {
+        out.score = result_score(rp, gc, key_score(W), gl, gh);
+        writer = owner;
+        hrec.x = -2;
+        if (owner) {
+          const int x = key_loc(W);
+          int mask = p_mask;
+          const bool virt = x == p_b;
+          NodeV bn{};
+          const PodDev p_pod = sh.pf_pod;
+          if (!virt) {  // Reserve + Bind on the winner's slot (the virtual node holds another)
+            bn = load_node(&s_nodes[x]);
+            mask = select_gpus(bn, p_pod, rp.gpusel, sel_arg<false>(rp, bn, p_pod, n_lo + x, key_gpu(W)), rp.seed, p_step);
+            if (mask >= 0) bind_node(bn, p_pod, mask, +1);
+          }
+          if (mask < 0) {  // Reserve failed: allocateGpuId returned "" / panicked
+            out.status = ST_ERROR;
+            out.score = 0;
+            hrec.x = -3;
+          } else {
+            const int tg = (int)p_pod.tag;
+            if (virt) {
+              if (lane < 2) reinterpret_cast<uint4*>(&s_nodes[x])[lane] = reinterpret_cast<const uint4*>(&s_nodes[ns])[lane];
+              else if (lane == 6) s_F0[x] = s_F0[ns];
+              else if (lane == 9) s_E0[x] = s_E0[ns];
+              else if (lane == 8 && overlapped) {  // this step's scratch: the post-Bind node (the virtual slot's)
+                int* c_pr = s_praw + (p_step + 1 & 1) * (a.S + 1);
+                int* c_pi = s_pinf + (p_step + 1 & 1) * (a.S + 1);
+                c_pr[x] = c_pr[ns];
+                c_pi[x] = c_pi[ns];
+              }
+            } else {
+              if (lane == 0) store_node(&s_nodes[x], bn);
+              else if (lane == 6) s_F0[x] = -1.0;
+              else if (lane == 9) s_E0[x] = kEnergyStale;
+              *redo = overlapped;
+              if (prof && lane == 0 && overlapped) sh.prof[9] += 1ull << 32;
+            }
+            if (lane == 2 && tg >= 0) tag_add(g_tags + (size_t)x * kTagStride, tg, +1);
+            else if (lane == 10 && pmon) pm_bump(x);
+            else if (lane == 7 && snap) {  // cluster report: the post-Bind record
+              store_node(snap + p_step, virt ? load_node(&s_nodes[ns]) : bn);
+              rp.prev[p_step] = s_last[x];
+              s_last[x] = p_step;
+            }
+            out.node = n_lo + x;
+            out.gpu_mask = mask;
+            hrec = make_int2(n_lo + x, mask + 1);
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      if (hist) hist[p_step] = hrec;
+      if (writer) rp.res[p_step] = out;
+    }
+    return true;
+  };
+
   // Finish the pending step with nothing to overlap (before a delete / at the end).
   auto finish_pending = [&]() {
     if (wv == 0) {
-      GranV<kS> g{};
-      if (a.K > 1) poll_once(g);
-      int gc, ge, gl, gh;
-      bool ok;
-      const unsigned long long W = exchange(g, &gc, &ge, &gl, &gh, &ok);
-      if (kPF) { gc = p_st0; ge = p_st1; gl = p_st2; gh = p_st3; }  // the step's A round
-      if (ok) commit(W, gc, ge, gl, gh);
+      bool ok = true;
+      if constexpr (kPF) {
+        bool redo;
+        unsigned long long x[kS][7];
+        ok = pf_resolve(x, false, false, &redo);
+      } else {
+        GranV<kS> g{};
+        if (a.K > 1) poll_once(g);
+        int gc, ge, gl, gh;
+        const unsigned long long W = exchange(g, &gc, &ge, &gl, &gh, &ok);
+        if (ok) commit(W, gc, ge, gl, gh);
+      }
       if (lane == 0) {
         if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
         sh.pend_valid = 0;
@@ -1086,6 +1239,10 @@ void k_replay(ksim_replay::ReplayArgs a,
     const bool share = is_share_pod(p);
     const int vb = pend ? __builtin_amdgcn_readfirstlane(pvb.y) : -1;
     const int nsv = ns + (vb >= 0 ? 1 : 0);
+    // PWR+FGD: this step's per-slot scratch (by step parity: the pending step's stays intact for a miss round)
+    int* const c_praw = s_praw + (step & 1) * (a.S + 1);
+    int* const c_pinf = s_pinf + (step & 1) * (a.S + 1);
+    unsigned long long px[kS][7];  // PWR+FGD: wave 0's early poll of the pending round
     // early poll of the pending exchange by wave 0 (consumed after the evaluation)
     GranV<kS> pg{};
     // one node's packed key into the workgroup aggregate (LDS atomics), or the excluded pair
@@ -1107,17 +1264,6 @@ void k_replay(ksim_replay::ReplayArgs a,
         if (kErr) {
           if (__any(agg && e1) && lane == 0) atomicOr(&sh.agg_err, 1);
         }
-      }
-    };
-    // PWR+FGD: a feasible node's raw PWR score into the slice's A-round aggregate (the pending best
-    // node and the virtual slot join after the commit, from their per-slot scratch)
-    auto route_a = [&](bool leader, int i, bool feas, bool e1, int praw) {
-      const bool agg = leader && feas && i != vb && i != ns;
-      const unsigned long long am = __ballot(agg);
-      if (am) {
-        if (agg) { atomicMin(&sh.agg_lo, praw); atomicMax(&sh.agg_hi, praw); }
-        if (lane == 0) atomicAdd(&sh.agg_cnt, (int)__popcll(am));
-        if (__any(agg && e1) && lane == 0) atomicOr(&sh.agg_err, 1);
       }
     };
     if constexpr (kFgd) {
@@ -1188,7 +1334,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         }
         __syncthreads();
         mark(2);
-        if (pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(pg);
+        if (!kPF && pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(pg);
         if (tid == 0) sh.nitems = 0;  // every thread has read tot; the next writer is past a barrier
         // fgd_score.go:100-141: every candidate lane scores itself; the node keeps the max,
         // ties to the lowest GPU index (fgd_score.go:128 keeps the first max)
@@ -1229,11 +1375,10 @@ void k_replay(ksim_replay::ReplayArgs a,
             perr = (pinf & kPfErr) != 0;
           }
           if (valid && g == 0) {
-            s_praw[i] = praw;
-            s_pinf[i] = pinf;
+            c_praw[i] = praw;
+            c_pinf[i] = pinf;
             if (pmon && !hit && i < ns) s_pm[(size_t)p.pad * a.S + i] = pf_memo_pack(praw, pinf, s_pver[i]);
           }
-          route_a(valid && g == 0, i, feas, perr, praw);
         } else {
           const unsigned long long k = feas ? pack_key((unsigned)raw, n.name_rank, gpu, i == ns ? vb : i) : 0ull;
           route(valid && g == 0, i, feas, false, raw, k);
@@ -1294,90 +1439,90 @@ void k_replay(ksim_replay::ReplayArgs a,
         route(tid < cn, i, feas, e1, raw, k);
       }
     }
+    if (kPF && pend && a.K > 1 && wv == 0) {  // the pending round's granules: loads in flight over the barrier
+      const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+#pragma unroll
+      for (int j = 0; j < kS; ++j)
+        if (lane + 64 * j < a.K) {
+#pragma unroll
+          for (int q = 0; q < 7; ++q) px[j][q] = gload(slot + (size_t)(lane + 64 * j) * kGranW + q);
+        }
+    }
     __syncthreads();
     mark(4);
     if constexpr (kPF) {
-      if (wv == 0) {
-        // 1. this step's A round out first (publish_a): the slice without b, and b pre / post
-        AVar v{sh.agg_cnt, sh.agg_err, sh.agg_lo, sh.agg_hi, 0, 0, 0, 0, 0, 0};
-        if (vb >= 0) {
-          const int ip = s_pinf[vb], iq = s_pinf[ns];
-          v.fpre = (ip & kPfFeas) ? 1 : 0;
-          v.epre = (ip & kPfErr) ? 1 : 0;
-          v.rpre = s_praw[vb];
-          v.fpost = (iq & kPfFeas) ? 1 : 0;
-          v.epost = (iq & kPfErr) ? 1 : 0;
-          v.rpost = s_praw[ns];
-        }
-        if (a.K > 1 && lane == 0) publish_a(v);
-        // 2. finish the pending key round (its latency overlapped the evaluation above) and commit it with
-        //    its own A round's totals; the column holding its winner
-        bool ok = true;
-        unsigned long long W = 0ull;
-        int kstar = -1;
-        if (pend) {
-          int gc_, ge_, gl_, gh_;
-          W = exchange(pg, &gc_, &ge_, &gl_, &gh_, &ok);
-          if (a.K == 1) {
-            kstar = W != 0ull && W == p_key ? 0 : -1;
-          } else {
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-              const unsigned long long kj = lane + 64 * j < a.K ? ((pg.g1[j] & 0xffffffffull) << 32) | (pg.g0[j] & 0xffffffffull)
-                                                                : 0ull;
-              const unsigned long long bm = __ballot(W != 0ull && kj == W);
-              if (bm && kstar < 0) kstar = 64 * j + (int)__builtin_ctzll(bm);
-            }
+      // 1. the pending step (its round overlapped the evaluation above): decide and commit.  The owner of a winner
+      //    other than its virtual node re-evaluates this step: that slot changed under the evaluation.
+      if (pend) {
+        if (wv == 0) {
+          bool redo = false;
+          const bool ok = pf_resolve(px, a.K > 1, true, &redo);
+          if (lane == 0) {
+            sh.pf_redo = redo ? 1 : 0;
+            sh.pend_valid = 0;
+            sh.pend_b = -1;
+            if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
           }
-          if (ok) commit(W, p_st0, p_st1, p_st2, p_st3);
         }
-        // the pending step binds its winner (a Score error aborts the cycle, framework.go:650-656): post for
-        // the winner's slice
-        const bool bind = pend && W != 0ull && !(p_st0 > 1 && p_st1);
-        // 3. this step's A round totals
-        int gc = 0, ge = 0, gl = 0, gh = 0;
-        if (a.K > 1) {
-          ok = ok && collect_a(kstar, bind, &gc, &ge, &gl, &gh);
-        } else {
-          a_total(v, bind && kstar == 0, &gc, &ge, &gl, &gh);
-        }
-        p_st0 = gc; p_st1 = ge; p_st2 = gl; p_st3 = gh;
-        if (lane == 0) {
-          sh.a_lo = gl;
-          sh.a_hi = gh;
-          reset_agg();
-          if (!ok) { sh.stop = 1; atomicOr(a.fail, 1); }
+        __syncthreads();
+        if (sh.stop) break;
+        if (sh.pf_redo) {  // the same step again, nothing pending
+          --step;
+          continue;
         }
       }
-      __syncthreads();
-      if (sh.stop) break;
       mark(5);
-      // 3. the slice's weighted totals w_pwr * NormalizeScore(PWR) + w_fgd * FGD (framework.go:686-704)
-      {
-        const int glo = sh.a_lo, ghi = sh.a_hi;
+      // 2. the slice's A totals and its best key under each of the class's two guessed ranges
+      const int4 gs = s_gtab[p.pad & (kPfGuess - 1)];
+      if (wv * 64 < ns) {
+        int c = 0, e = 0, lo = INT_MAX, hi = INT_MIN;
+        unsigned long long k0 = 0ull, k1 = 0ull;
         for (int i = tid; i < ns; i += kRBlock) {
-          const int inf = s_pinf[i];
+          const int inf = c_pinf[i];
           if (inf & kPfFeas) {
-            const int norm = pwr_normalize(s_praw[i], glo, ghi);
-            const int total = rp.w_pwr * norm + rp.w_fgd * (inf & 0xff);
-            const int kg = rp.gpusel == SEL_PWR ? ((inf >> 8) & 0xf) - 1 : ((inf >> 12) & 0xf) - 1;
-            atomicMax(&sh.agg_key, pack_key((unsigned)total, load_node(&s_nodes[i]).name_rank, kg, i));
+            const int pr = c_praw[i];
+            ++c;
+            e |= (inf & kPfErr) ? 1 : 0;
+            lo = min(lo, pr);
+            hi = max(hi, pr);
+            const unsigned long long q0 = pf_key(pr, inf, gs.x, gs.y, i), q1 = pf_key(pr, inf, gs.z, gs.w, i);
+            k0 = q0 > k0 ? q0 : k0;
+            k1 = q1 > k1 ? q1 : k1;
           }
+        }
+        c = wave_sum_dpp(c);
+        e = __any(e != 0) ? 1 : 0;
+        lo = wave_min_dpp(lo);
+        hi = wave_max_dpp(hi);
+        k0 = wave_max_u64_dpp(k0);
+        k1 = wave_max_u64_dpp(k1);
+        if (lane == 0 && c > 0) {
+          atomicAdd(&sh.agg_cnt, c);
+          if (e) atomicOr(&sh.agg_err, 1);
+          atomicMin(&sh.agg_lo, lo);
+          atomicMax(&sh.agg_hi, hi);
+          atomicMax(&sh.agg_key, k0);
+          atomicMax(&sh.agg_key1, k1);
         }
       }
       __syncthreads();
-      // 4. publish the key round, then prepare the virtual node as below
+      // 3. publish the round, then prepare the virtual node: guess 0's local best with this step's Reserve + Bind
       if (wv == 0) {
-        const unsigned long long mk = sh.agg_key;
+        const unsigned long long mk = sh.agg_key, mk1 = sh.agg_key1;
+        const int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
         if (lane == 0) {
           if (a.K > 1) {
-            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW + (size_t)w * kGranW;
             const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
-            gstore(slot + (size_t)w * kGranW + 0, tag | (mk & 0xffffffffull));
-            gstore(slot + (size_t)w * kGranW + 1, tag | (mk >> 32));
-            gstore(slot + (size_t)w * kGranW + 2, tag);
+            gstore(slot + 0, tag | (mk & 0xffffffffull));
+            gstore(slot + 1, tag | (mk >> 32));
+            gstore(slot + 2, tag | (mk1 & 0xffffffffull));
+            gstore(slot + 3, tag | (mk1 >> 32));
+            gstore(slot + 4, tag | (unsigned)l);
+            gstore(slot + 5, tag | (unsigned)h);
+            gstore(slot + 6, tag | ((unsigned)e << 31) | ((unsigned)c & 0x7fffffffu));
           }
-          sh.agg_key = 0ull;
+          reset_agg();
         }
         const int mloc = key_loc(mk);
         int mask = -1;
@@ -1406,6 +1551,12 @@ void k_replay(ksim_replay::ReplayArgs a,
         p_seq = seq;
         p_b = mk != 0ull ? mloc : -1;
         p_key = mk;
+        if (lane == 0) {
+          sh.pf_key1 = mk1;
+          sh.pf_g = gs;
+          sh.pf_pod = p;
+        }
+        p_st0 = c; p_st1 = e; p_st2 = l; p_st3 = h;
         p_mask = mask;
         p_tag = mask >= 0 ? (int)p.tag : -1;
         ++seq;
@@ -3452,6 +3603,12 @@ static void print_replay_profile(ksim_engine* e, int R, int K, int steps) {
   double spins = 0;
   for (int b = 0; b < nb; ++b) spins += (double)h[(size_t)b * P + 8];
   std::fprintf(stderr, " poll spins/step %.2f", spins / nb / steps);
+  double miss = 0, redo = 0;  // PWR+FGD: guessed-range misses (every workgroup alike), re-evaluations
+  for (int b = 0; b < nb; ++b) {
+    miss += (double)(h[(size_t)b * P + 9] & 0xffffffffull);
+    redo += (double)(h[(size_t)b * P + 9] >> 32);
+  }
+  if (miss + redo > 0) std::fprintf(stderr, " pf misses/step %.4f re-evaluations/step %.4f", miss / nb / steps, redo / nb / steps * K);
   double cyc = 0, tick = 0;
   for (int b = 0; b < nb; ++b) { cyc += (double)h[(size_t)b * P + 10]; tick += (double)h[(size_t)b * P + 11]; }
   if (tick > 0) std::fprintf(stderr, " shader clock %.0f MHz", cyc / tick * 100.0);

@@ -46,7 +46,8 @@ constexpr int kFChunk = kRBlock / 8; // nodes per chunk, 8 lanes per node -- lan
 constexpr int kRMaxCand = 9;         // FGD items per node: stale current state + up to 8 candidates
 constexpr int kMaxK = 256;         // workgroups per replica (<= 64: one granule column per polling lane)
 constexpr int kGran = 3;           // granules per workgroup per step (the key exchange)
-constexpr int kGranW = 8;          // granule words per workgroup per parity: key round 0-2, PWR+FGD's A round 4-6
+constexpr int kGranW = 10;         // granule words per workgroup per parity: key round 0-2; PWR+FGD's round 0-6, its miss round 7-8
+constexpr int kPfGuess = 256;      // PWR+FGD: entries of the guessed-range table (class id mod 256)
 constexpr unsigned kSpinLimit = 1u << 22;  // ~seconds: only a non-resident workgroup can stall a poll
 constexpr int kEvBuf = 128;        // events staged in LDS per refill (4 KB)
 
@@ -72,7 +73,8 @@ constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11
 // tags[S+1][16] (GpuClustering; the other policies keep the tag counts in HBM), double F0[S+1]
 // (FGD: cached F of the current state, < 0 = stale), double E0[S+1] + int2 pe[S+1] (PWR: cached
 // energy, static energy terms), i32 last[S+1] (cluster report), i32 praw[S+1] + i32 pinf[S+1]
-// (PWR+FGD: the step's raw PWR score and packed FGD score / GPU choices of every slot).  A lean
+// (PWR+FGD: the raw PWR score and packed FGD score / GPU choices of every slot, two steps' worth) + int4
+// gtab[kPfGuess] (PWR+FGD: each class's two most recent cluster-wide raw PWR ranges).  A lean
 // BestFit / DotProd / GpuPacking / Random workgroup of C2 / C4 is about 44 KB, so several share a
 // CU.  Slot ns (one past the slice) is the VIRTUAL node: the pending step's local best node with
 // that step's Bind already applied (see the pipelining note).
@@ -80,6 +82,7 @@ struct __align__(16) ReplayShared {
   PodDev ev[kEvBuf];
   // the step's local aggregate (LDS atomics), the pending best node b and the virtual node excluded
   unsigned long long agg_key;
+  unsigned long long agg_key1, agg_pad;  // PWR+FGD: the slice's key under the class's second guessed range
   int agg_cnt, agg_err, agg_lo, agg_hi;
   // the excluded real node (pre-Bind) and the virtual node (post-Bind) of the current step
   unsigned long long pre_key, post_key;
@@ -88,10 +91,15 @@ struct __align__(16) ReplayShared {
   int pend_valid, pend_b;
   int stop;
   int nitems;                   // FGD work-list length of the current chunk
-  int a_lo, a_hi;               // PWR+FGD: the step's cluster-wide min / max raw PWR score (A round)
-  int pad0;
+  int pf_redo;                  // PWR+FGD: this workgroup re-evaluates the step (its winner was not the virtual node)
+  int pad0, pad1;
   unsigned long long prof[kProfPhases];  // KSIM_PROFILE phase sums (thread 0)
   unsigned long long prof_pad[4];
+  // PWR+FGD, the pending step (kept here, not in wave 0's registers): its pod, the class's guessed ranges
+  // {lo0, hi0, lo1, hi1} and this slice's key under the second one
+  PodDev pf_pod;
+  int4 pf_g;
+  unsigned long long pf_key1, pf_pad2;
   PowerDev pw;                  // PWR policies: the replica's energy model
   unsigned dead[32];            // classes with no feasible node (create-only streams: for good)
 };
@@ -109,7 +117,7 @@ static_assert(sizeof(ReplayFgd) % 16 == 0, "keep the node records 16-B aligned")
 
 // The dynamic LDS layout of one k_replay workgroup (host and device).
 struct RLayout {
-  size_t fgd, nodes, tags, F0, E0, pe, last, praw, pinf, pver, pm, total;
+  size_t fgd, nodes, tags, F0, E0, pe, last, praw, pinf, gtab, pver, pm, total;
 };
 // pm_c > 0 (PWR+FGD): u32 pver[S+1] (each slot's state version) and uint2 pm[pm_c][S] (every class's
 // memoised Filter + Score of every real slot, valid while its version matches; pf_memo_* below)
@@ -126,8 +134,10 @@ __host__ __device__ inline RLayout replay_layout(int S, int pol, bool general, i
   L.E0 = o;    o += pwr ? S1 * sizeof(double) : 0;
   L.pe = o;    o += pwr ? S1 * sizeof(int2) : 0;
   L.last = o;  o += general ? S1 * sizeof(int) : 0;
-  L.praw = o;  o += pf ? S1 * sizeof(int) : 0;
-  L.pinf = o;  o += pf ? S1 * sizeof(int) : 0;
+  L.praw = o;  o += pf ? 2 * S1 * sizeof(int) : 0;  // by step parity: the pending step's stays intact
+  L.pinf = o;  o += pf ? 2 * S1 * sizeof(int) : 0;
+  o = (o + 15) / 16 * 16;
+  L.gtab = o;  o += pf ? kPfGuess * sizeof(int4) : 0;
   L.pver = o;  o += (pf && pm_c > 0) ? (S1 * sizeof(unsigned) + 15) / 16 * 16 : 0;
   L.pm = o;    o += (pf && pm_c > 0) ? (size_t)pm_c * S * sizeof(uint2) : 0;
   L.total = o;

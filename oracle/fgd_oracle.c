@@ -133,6 +133,15 @@ static long long g_census_n;
 static int g_census_cur_step = -1;
 static __thread int tl_census_node = -1;
 
+/* Diagnostics: the raw PWR min / max of every PWR / PWR+FGD cycle scored (step -> {lo, hi}; the step's entry stays
+ * {1, 0} when no normalisation ran).  Used to size a speculative NormalizeScore range. */
+static int64_t* g_pwr_lohi = NULL;
+static int g_pwr_lohi_cap = 0;
+void orc_pwr_lohi_trace(int64_t* buf, int cap) {
+    g_pwr_lohi = buf;
+    g_pwr_lohi_cap = cap;
+}
+
 int orc_census_begin(void) {
     if (orc_score_thresholds(g_th)) return -1;
     g_census_min = HUGE_VAL;
@@ -1286,7 +1295,15 @@ int orc_run_events_state(const orc_node_spec* nodes, int n_nodes, const orc_targ
                     R->status = 2; /* framework.go:656-667: a Score error aborts the cycle */
                 } else {
                     if (pol.policy == ORC_POL_BESTFIT) orc_normalize_score(fs, nf);
-                    if (pol.policy == ORC_POL_PWR || pol.policy == ORC_POL_PWR_FGD) orc_normalize_score_pwr(fs, nf);
+                    if (pol.policy == ORC_POL_PWR || pol.policy == ORC_POL_PWR_FGD) {
+                        if (g_pwr_lohi && s < g_pwr_lohi_cap) {
+                            int64_t lo = fs[0], hi = fs[0];
+                            for (int k = 1; k < nf; k++) { lo = fs[k] < lo ? fs[k] : lo; hi = fs[k] > hi ? fs[k] : hi; }
+                            g_pwr_lohi[2 * s] = lo;
+                            g_pwr_lohi[2 * s + 1] = hi;
+                        }
+                        orc_normalize_score_pwr(fs, nf);
+                    }
                     /* framework.go:686-704: range check, then x plugin weight; prioritizeNodes sums the
                      * plugins (generic_scheduler.go:511-519) */
                     const int64_t w1 = pol.policy == ORC_POL_PWR_FGD ? pol.w_pwr : 1000;

@@ -94,6 +94,7 @@ int     orc_score_thresholds(double* th /* [102] */);
  * end returns the smallest distance |delta - th[k]|, where it happened (event, node, k) and the
  * number of deltas seen. */
 typedef struct { double delta; int event, node, score, score_nudged, ulps; } orc_census_case;
+void    orc_pwr_lohi_trace(int64_t* buf, int cap); /* diagnostics: per-step raw PWR min / max */
 int     orc_census_begin(void);
 /* deltas within 1e-10 of a step; of those, the ones whose score differs from the one a correctly
  * rounded exp gives (crdiff) and, of the rest, the ones whose score changes when exp's result moves

@@ -2,8 +2,8 @@
 (pkg/simulator/plugin/pwr_score.go; generate_run_scripts.py:31-42 "PWR", "PWR 500 FGD 500", ...).
 
 The engine replays PWR replicas with the persistent k_replay (PWR: one key round per pod, the raw
-score decides; PWR + FGD: an A round for the cluster's min / max raw PWR score, then the normalized
-weighted key round) and, with run_mode 1, on the per-pod path: k_step (Filter, raw PWR score, FGD
+score decides; PWR + FGD: one round carrying the cluster's min / max raw PWR score and each slice's
+normalized weighted keys under two guessed ranges, a miss round when neither is the step's) and, with run_mode 1, on the per-pod path: k_step (Filter, raw PWR score, FGD
 candidates) then k_step_pwr (NormalizeScore, weighted sum, selectHost, Reserve, Bind) in a hipGraph.
 Bar: bit-exact against the oracle, event by event, and the same final cluster state, on every path.
 Every test needs a gfx950 device.
