@@ -74,8 +74,12 @@ def profile_rooflines(args, kernel):
         pmc = json.load(f)
     dom = pmc.get("dominant") or {}
     fam = dom.get("kernel", "")
-    # the run's path names the kernels it launched ("memo+k_replay": k_memo or k_hmemo beside k_replay)
-    if not any(t and (t in fam if t != "memo" else fam in ("k_memo", "k_hmemo")) for t in kernel.split("+")):
+    # the run's path names the kernels it launched ("memo+k_replay": k_memo or k_hmemo for the FGD replicas beside
+    # the other policies' kernels -- k_replay, k_scan1 / k_scan1_mix or k_random_go)
+    toks = kernel.split("+")
+    if "memo" in toks and "k_replay" in toks:
+        toks += ["k_scan1", "k_random_go"]
+    if not any(t and (t in fam if t != "memo" else fam in ("k_memo", "k_hmemo")) for t in toks):
         return None, None, None
     src = os.path.relpath(pf, ROOT)
     valu = None

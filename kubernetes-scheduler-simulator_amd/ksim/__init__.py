@@ -654,7 +654,8 @@ class Engine:
     def last_run_path(self):
         """'k_replay' | 'k_memo' | 'memo+k_replay' | 'k_step' | 'sharded' | 'k_hmemo' | 'k_random_go' | 'k_scan1': the kernels
         the last run()
-        used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay for the others)."""
+        used ('memo+k_replay': a memoised kernel for the FGD replicas, k_replay / k_scan1 / k_random_go for the
+        others)."""
         k = C.c_int(0)
         check(lib().ksim_engine_last_run_path(self.h, C.byref(k)), "last_run_path")
         return ["k_replay", "k_memo", "memo+k_replay", "k_step", "sharded", "k_hmemo", "k_random_go", "k_scan1"][k.value]
