@@ -2230,9 +2230,10 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     // L2 spares the flagged blocks' key reloads.  They bound the wide form's class waves (C5: 100k nodes, the
     // keys far beyond L2, 55 flagged rows per refresh from HBM), while one workgroup over an openb cluster
     // keeps its keys in L2 and is bound by F: there L2 only adds update work (profiles/r04/hmemo/).
-    // KSIM_HL2=0 never, =1 also for one workgroup per replica.
+    // Off by default since r05: in the wide form its code alone cost C5 4.09 -> 4.22 s, and it is compiled only into
+    // the one-workgroup instantiations; KSIM_HL2=1 turns it on there.
     const char* v = std::getenv("KSIM_HL2");
-    const bool want = v ? v[0] == '1' : pl.K > 1;
+    const bool want = v && v[0] == '1' && pl.K == 1;
     pl.l2 = want && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true, 0).total <= 160 * 1024;
   }
   {  // per-model tables of the typed replicas (KSIM_HMODEL=0: the whole table for every model, as before r05)

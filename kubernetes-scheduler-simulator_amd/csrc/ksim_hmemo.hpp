@@ -336,7 +336,10 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const int N = a.N, nb = a.nbw;  // nb: L1 blocks of this workgroup's slice
   const int lo = w * a.S, ns = min(a.S, N - lo), b0 = lo / kFan;
   const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
-  const bool use_l2 = a.l2 != nullptr;
+  // L2 is compiled into the one-workgroup instantiations only (KSIM_HL2=1): in the wide form its code alone cost C5
+  // 4.09 -> 4.22 s (r04 bisect, profiles/r05/hmemo/c5_bisect_r05c26.txt), on or off
+  constexpr bool kL2Code = kSub == 0;
+  const bool use_l2 = kL2Code && a.l2 != nullptr;
   const HLayout L = hmemo_layout(a.S, a.Cmax, a.Gmax, nb, use_l2, a.Mtab);
   PodDev* s_cls = reinterpret_cast<PodDev*>(smem + L.cls);
   PodDev* s_gpod = reinterpret_cast<PodDev*>(smem + L.gpod);
