@@ -235,14 +235,16 @@ def test_hmemo_cluster_report(default_trace, wgs):
     assert reps[HMEMO] == reps[SCAN]
 
 
-@pytest.mark.parametrize("knobs", [{"KSIM_HPRUNE": "-1"}, {"KSIM_HMODEL": "0"}, {"KSIM_HMODEL": "0", "KSIM_HPRUNE": "100000"}],
-                         ids=["prune-all", "whole-table", "r04-form"])
+@pytest.mark.parametrize("knobs", [{"KSIM_HPRUNE": "-1"}, {"KSIM_HMODEL": "0"}, {"KSIM_HMODEL": "0", "KSIM_HPRUNE": "100000"},
+                                   {"KSIM_HL2": "1"}],
+                         ids=["prune-all", "whole-table", "r04-form", "l2"])
 @pytest.mark.parametrize("trace_name", ["gpuspec33", "gpuspec10", "default"])
 def test_hmemo_list_and_table_forms(trace_name, knobs, monkeypatch):
     # r05: k_hmemo's F list without the groups no class of which passes Filter on d (by default for tables of
     # more than 64 typical pods; -1: every replica), and per GPU model the typical table cut to the pods that
-    # accept the model plus the precomputed NA bin (typed replicas; KSIM_HMODEL=0 the whole table): every form
-    # decides as the oracle does, one workgroup per replica and the wide form
+    # accept the model plus the precomputed NA bin (typed replicas; KSIM_HMODEL=0 the whole table), and the
+    # per-(class, block) second maxima (KSIM_HL2=1: one workgroup per replica only, compiled out of the wide form):
+    # every form decides as the oracle does, one workgroup per replica and the wide form
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     t = ksim.Trace.openb(trace_name)
