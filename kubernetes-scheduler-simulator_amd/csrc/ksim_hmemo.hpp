@@ -403,6 +403,12 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   }
   for (int i = tid; i < 102; i += kHBlock) sh.th[i] = a.th[i];
   if (tid == 0) { sh.d[0] = sh.d[1] = -1; sh.nitems[0] = sh.nitems[1] = 0; sh.nflag = 0; sh.dfirst[0] = sh.dfirst[1] = 0u; sh.stop = 0; sh.bar = 0; sh.cbar = 0; sh.lseq = 0; sh.pdead[0] = sh.pdead[1] = -1; sh.f0seq = 0; }
+  // the residency gate (C4): this workgroup has started -- a vector store to host memory, system scope.  In the
+  // one-workgroup instantiations it is stored here, not at the kernel's entry: there it took them from 8 to 57
+  // VGPR spills (C2 run_mode 5 48.7 -> 47.2 ms here); the wide form keeps it at the entry (C5 measured no better
+  // with it here, profiles/r05/hmemo/ab_r05c30_gate_store.txt)
+  if (kSub == 0 && a.started != nullptr && tid == 0)
+    __hip_atomic_store(a.started + blockIdx.x, a.gate_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (int i = tid; i < 32; i += kHBlock) sh.dead[i] = 0u;
   const bool prof = kProf && a.prof != nullptr;
   if (prof && tid < kHProf) sh.prof[tid] = 0ull;
@@ -1056,7 +1062,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
 
 template <int kSub, bool kProf, bool kModel = false>
 __global__ __launch_bounds__(kHBlock) void k_hmemo(HMemoArgs a, const TypDev* __restrict__ tp_all) {
-  if (a.started != nullptr && threadIdx.x == 0)  // a vector store to host memory, system scope
+  if (kSub != 0 && a.started != nullptr && threadIdx.x == 0)  // (the one-workgroup forms store it in the body)
     __hip_atomic_store(a.started + blockIdx.x, a.gate_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   hmemo_body<kSub, kProf, kModel>(a, tp_all, (int)blockIdx.x);
 }
