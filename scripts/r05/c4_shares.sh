@@ -3,7 +3,7 @@
 # N = 2, 4, 8 timed alone on this GPU (bench.py --rank-share k/N); the max over k predicts the N-GPU time
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r05c6; mkdir -p $OUT
+OUT=gpurun_out/${RUN:-r05c6}; mkdir -p $OUT
 for N in 2 4 8; do
   for k in $(seq 0 $((N-1))); do
     KSIM_GROUP_TIMES=1 timeout -k 10 240 python -u bench.py --config c4 --rank-share $k/$N --no-cpu-baseline --steps 5 --warmup 1 \
