@@ -1121,8 +1121,8 @@ void k_replay(ksim_replay::ReplayArgs a,
               else if (lane == 6) s_F0[x] = s_F0[ns];
               else if (lane == 9) s_E0[x] = s_E0[ns];
               else if (lane == 8 && overlapped) {  // this step's scratch: the post-Bind node (the virtual slot's)
-                int* c_pr = s_praw + (p_step + 1 & 1) * (a.S + 1);
-                int* c_pi = s_pinf + (p_step + 1 & 1) * (a.S + 1);
+                int* c_pr = s_praw + ((p_step + 1) & 1) * (a.S + 1);
+                int* c_pi = s_pinf + ((p_step + 1) & 1) * (a.S + 1);
                 c_pr[x] = c_pr[ns];
                 c_pi[x] = c_pi[ns];
               }
