@@ -1083,7 +1083,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       W = mine;
       if (a.K > 1 && !pf_miss_round(mine, &W)) return false;
     }
-    if (gc > 1 && lane == 0) {  // the class's most recent ranges (every workgroup updates alike)
+    if (gc > 1 && lane == 0 && a.pf_guess) {  // the class's most recent ranges (every workgroup updates alike)
       int4& t = s_gtab[p_cls & (kPfGuess - 1)];
       if (!(t.x == gl && t.y == gh)) t = make_int4(gl, gh, t.x, t.y);
     }
@@ -3945,6 +3945,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       const char* v0 = std::getenv("KSIM_PF_MEMO_VER0");
       const long v = v0 ? std::atol(v0) : 0;
       ra.pm_ver0 = v > 0 && v < (long)ksim_replay::kPmInvalid ? (unsigned)v : 0u;
+      const char* pg = std::getenv("KSIM_PF_GUESS");
+      ra.pf_guess = pg && pg[0] == '0' ? 0 : 1;
     }
     ra.reps = e->d_reps;
     ra.rep_list = e->d_replist + first;
