@@ -35,7 +35,7 @@ BYTES_PER_POD = 56        # 16 B request + 8 B winner + 32 B scatter
 # dispatch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE; MI355X_MICROARCH.md HBM section) and its
 # VALU issue (SQ_INSTS_VALU with the fp64 split).  profiles/<round>/prof/<profile_key(args)>/pmc.json, the
 # newest round that profiled the configuration first.
-PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r05", "r04", "r03", "r02")]
+PROF_DIRS = [os.path.join(ROOT, "profiles", r, "prof") for r in ("r06", "r05", "r04", "r03", "r02")]
 PROF_DIR = PROF_DIRS[0]
 # MI355X_MICROARCH.md, persistent-kernel price list: handoff-1to1 = one producer -> one consumer
 # granule hand-off between CUs, idle chip, 8 B: 0.8 us.  A pod step whose decision crosses CUs
@@ -56,6 +56,8 @@ def profile_key(args):
         k += "-sharded"
     if getattr(args, "random_stream", "hash") == "go":
         k += "-go"
+    if getattr(args, "rank_share", ""):
+        k += "-share%s" % args.rank_share.replace("/", "of")  # a share's own launches (no profile: traffic null)
     return k
 
 
@@ -64,22 +66,18 @@ def profile_file(key):
     return next((f for f in (os.path.join(d, key, "pmc.json") for d in PROF_DIRS) if os.path.exists(f)), None)
 
 
-def profile_rooflines(args, kernel):
+def profile_rooflines(args, kernels):
     """(traffic, traffic_source, valu) from this configuration's counter passes, if it was profiled and
-    the profiled dominant kernel is the one this run launched."""
+    the profiled dominant kernel is one this run launched (`kernels`: Engine.last_run_kernels())."""
     pf = profile_file(profile_key(args))
     if pf is None:
         return None, None, None
     with open(pf) as f:
         pmc = json.load(f)
     dom = pmc.get("dominant") or {}
-    fam = dom.get("kernel", "")
-    # the run's path names the kernels it launched ("memo+k_replay": k_memo or k_hmemo for the FGD replicas beside
-    # the other policies' kernels -- k_replay, k_scan1 / k_scan1_mix or k_random_go)
-    toks = kernel.split("+")
-    if "memo" in toks and "k_replay" in toks:
-        toks += ["k_scan1", "k_random_go"]
-    if not any(t and (t in fam if t != "memo" else fam in ("k_memo", "k_hmemo")) for t in toks):
+    fam = dom.get("kernel", "")  # scripts/pmc_summary.py kernel_of: k_memo, k_hmemo, k_scan1_mix, k_replay<1>, ...
+    names = {"k_hmemo" if k == "k_hmemo_wide" else k for k in kernels}
+    if fam.split("<")[0] not in names:
         return None, None, None
     src = os.path.relpath(pf, ROOT)
     valu = None
@@ -205,6 +203,26 @@ def cpu_baseline_sweep(workers=16, per_worker=2, prefix=None):
                        % (len(jobs), step, "the first %d events of each" % prefix if prefix else "replayed to completion", workers, full, os.cpu_count(), cpu_model()))
 
 
+def cpu_baseline_c5(trace, rp, threads, prefix=400):
+    """C5's CPU baseline: the oracle's FGD cycle over the 100 000-node cluster with `threads` workers per cycle
+    (parallelize.Until's fan-out, generic_scheduler.go:274-346), on the first `prefix` events of the bench's own
+    1M-event stream (a full replay would take days on the host)."""
+    os.environ["KSIM_ORACLE_CACHE"] = "0"
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    import helpers
+    import pyoracle as O
+    nodes, tp = helpers.oracle_nodes(trace, rp), helpers.oracle_typical(trace)
+    ev = helpers.oracle_events(trace, rp, prefix)
+    t0 = time.perf_counter()
+    O.run_events(nodes, tp, ev, policy=O.POL_FGD, gpu_sel=O.SEL_FGD, threads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=len(ev) / dt, unit="pods/s", cores=threads, kind="port",
+                node_evals_per_s=len(ev) * trace.num_nodes / dt,
+                sample="C5's own stream (synthetic 100000 nodes, seed 1 draw), its first %d events, FGD, %d worker "
+                       "threads per cycle (parallelize.Until fan-out); host nproc=%d, cpu %s"
+                       % (len(ev), threads, os.cpu_count(), cpu_model()))
+
+
 def cpu_model():
     """Host CPU model name (SURVEY §8(d) asks for it beside the thread count)."""
     try:
@@ -302,6 +320,7 @@ def main():
             dist.init_process_group("nccl")
 
     trace = ksim.Trace.openb("default")
+    c5_rp = None
     if args.config == "c4":
         import ksim.sweep as SW
         items = SW.plan()
@@ -333,6 +352,7 @@ def main():
         seeds = [2 * rank + 1]
         eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
                          tune=0.0, shuffle=False, report=args.report, random_stream=args.random_stream)
+        c5_rp = trace.replay(seed=seeds[0], tune_ratio=0.0, shuffle=False)
     else:
         seeds = seeds_for_rank(rank, args.replicas)
         eng = _engine_on(local, trace, seeds, args.nodes_per_block, args.policy, args.wgs, args.run_mode,
@@ -361,6 +381,8 @@ def main():
 
     steps_per_run = eng.last_run_steps()
     kernel = eng.last_run_path()
+    kernels = eng.last_run_kernels()  # what the run launched, in launch order
+    gate, gate_timeouts = eng.last_run_gate()
     # roofline: the dominant kernel (k_memo / k_replay) is one launch per replay of all replicas; its
     # duration is the hipEvent pair around the launch on the engine stream (mean over the timed runs)
     kern_us = dev_ms / args.steps * 1000.0
@@ -370,7 +392,7 @@ def main():
     value = job_events / dt
     # HBM traffic and the VALU issue fraction (FGD is fp64 VALU work) of the dominant kernel
     # from this configuration's counter passes (scripts/profile_config.sh -> profiles/r02/prof/)
-    traffic, traffic_src, valu = profile_rooflines(args, kernel)
+    traffic, traffic_src, valu = profile_rooflines(args, kernels)
     # executed work (the memoised paths skip most node evaluations): feasible (pod, node) score evaluations
     # of the reference's Score phase, and the (class, node) keys the memoised FGD replicas recomputed
     score_evals, key_refreshes = eng.work(getattr(eng, "memo_replicas", None))
@@ -405,13 +427,18 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      # what the counters saw the kernel move, as a fraction of peak over the same time
                      "traffic_frac": (traffic / (kern_us * 1e-6) / (HBM_PEAK_GBS * 1e9)) if traffic else None,
-                     "kernel": kernel, "kernel_us": kern_us, "bytes_per_launch": bytes_per_launch,
-                     "wgs_per_replica": eng.last_run_wgs()},
+                     "kernel": "+".join(kernels), "path": kernel, "kernel_us": kern_us,
+                     "bytes_per_launch": bytes_per_launch, "wgs_per_replica": eng.last_run_wgs()},
         # the bound that binds: every replica is a chain of dependent pod steps
         "latency": latency_block(kern_us, steps_per_run, eng.last_run_wgs()),
         "valu_roofline": valu,
     }
+    if gate:
+        line["residency_gate"] = {"opened": gate == 1, "timeouts": gate_timeouts}
     if args.config == "c4":
+        # SURVEY's 32 B per node-evaluation prices node reads the LDS / VGPR-resident kernels never make (the
+        # counters' traffic is ~0.2 % of it): the byte roofline is nominal here, the latency block binds
+        line["roofline"]["nominal"] = True
         line["data"] = "Alibaba openb traces (data/openb: 17 pod lists), the reference's own event order (Go math/rand replay)"
         line["config"] = {"workload": "C4: paper sweep, 17 traces x 6 policies x seeds 42-51, tune 1.3, "
                                       "per-event cluster report", "replicas_per_gpu": args.replicas,
@@ -456,6 +483,8 @@ def main():
         line["cpu_baseline"]["single_thread"] = one["single_thread"]
     if sweep_cpu is not None:
         line["cpu_baseline"] = sweep_cpu
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and c5_rp is not None and args.policy == "FGD":
+        line["cpu_baseline"] = cpu_baseline_c5(trace, c5_rp, args.cpu_threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if os.environ.get("KSIM_MAPS_OUT"):  # the process's mappings, to symbolise an exit-path fault

@@ -353,6 +353,13 @@ int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
  * policies' k_scan1_mix or one k_scan1 / k_replay per policy, k_random_go) and the side streams they ran
  * on concurrently (0: back to back on the engine stream).  Introspection for the tests and the bench. */
 int  ksim_engine_last_run_launches(ksim_engine* e, int* launches, int* side_streams);
+/* The replay kernels the last run launched, '+'-joined in launch order ("k_hmemo+k_scan1_mix", "k_memo",
+ * "k_step+k_step_pwr", ...), NUL-terminated into out[cap]: KSIM_ERANGE when cap is too small. */
+int  ksim_engine_last_run_kernels(ksim_engine* e, char* out, int cap);
+/* The residency gate of the last run (a paper-sweep run: the concurrent groups launch once every FGD workgroup
+ * has started): *gate 0 = no gate, 1 = opened, -1 = given up at its 2 s bound (the groups then
+ * launch unordered, and a note goes to stderr); *timeouts = gates given up over the engine's life. */
+int  ksim_engine_last_run_gate(ksim_engine* e, int* gate, long long* timeouts);
 /* Workgroups per replica used by the last run. */
 int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 /* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),

@@ -1853,9 +1853,9 @@ struct ksim_engine {
   std::vector<hipEvent_t> grp_rev;  // concurrent groups' report kernels: a timing event pair per group
   int grp_rev_used = 0;             // pairs recorded by the last run
   int scan1 = 2;       // single-workgroup cheap-policy groups on k_scan1, node records in VGPRs where they fit
-                       // (KSIM_SCAN1=1: records in LDS; 0: k_replay)
+                       // (KSIM_VARIANT scan1=1: records in LDS; 0: k_replay)
   std::vector<std::vector<NodeRec>> h_rec;  // the records set_nodes gave each replica (k_hmemo's initial states)
-  bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)  // replicas of the last run replayed by k_memo
+  bool last_step_path = false;  // the last run went through k_step (run_mode 1 or a PWR replica)
   std::vector<int> nt;
   hipGraphExec_t graph = nullptr;
   int graph_R = -1;
@@ -1870,7 +1870,10 @@ struct ksim_engine {
   hipStream_t side[kSide] = {};
   int* h_started = nullptr;   // residency gate: host-mapped flags, one per FGD workgroup (hipHostMalloc)
   int* d_started = nullptr;   // its device address
-  int started_cap = 0, gate_epoch = 0;   // how each side stream was created (plain 0, all-CU mask -1, CU range [0, k) k, complement -k)
+  int started_cap = 0, gate_epoch = 0;
+  int last_gate = 0;          // the last run's residency gate: 0 none, 1 opened, -1 given up at its bound (stderr note)
+  long long gate_timeouts = 0;  // gates given up at their bound, over the engine's life
+  std::string last_kernels;    // the replay kernels the last run launched, '+'-joined in launch order
   hipEvent_t side_ev[kSide] = {};
   hipEvent_t ev_fork = nullptr;
   bool report_done = false;
@@ -1879,7 +1882,7 @@ struct ksim_engine {
   hipEvent_t tev_fork = nullptr;
   hipEvent_t tev_side[kSide] = {};
   unsigned tev_used = 0u;
-  int last_pf_memo = 0;      // PWR+FGD memo class stride of the last k_replay<PWR+FGD> launch (0: none)  // run_persistent ran the report behind each concurrent group (last run)
+  int last_pf_memo = 0;      // PWR+FGD memo class stride of the last k_replay<PWR+FGD> launch (0: none)
   double last_ms = 0, last_report_ms = 0;
   // cluster report (ksim_engine_set_report)
   bool report = false;
@@ -1916,6 +1919,26 @@ struct ksim_engine {
   size_t go_cap = 0;
   int64_t last_steps = 0;
 };
+
+// Environment knobs.  Besides the five plain ones (KSIM_PROFILE, KSIM_COOP, KSIM_CUS,
+// KSIM_SIDE_STREAMS, KSIM_GROUP_TIMES), two comma-separated key=value lists: KSIM_VARIANT selects the measured
+// alternative forms of the kernels and plans (A/B runs; the defaults are what the bench and the tests measure),
+// KSIM_TEST the test-only settings (wrap points, stress delays, forced misses).
+static long knob(const char* var, const char* key, long dflt) {
+  const char* v = std::getenv(var);
+  if (!v) return dflt;
+  const size_t kl = std::strlen(key);
+  for (const char* p = v; *p;) {
+    const char* q = std::strchr(p, ',');
+    const size_t len = q ? (size_t)(q - p) : std::strlen(p);
+    if (len > kl && std::strncmp(p, key, kl) == 0 && p[kl] == '=') return std::strtol(p + kl + 1, nullptr, 0);
+    if (!q) break;
+    p = q + 1;
+  }
+  return dflt;
+}
+static long variant(const char* key, long dflt) { return knob("KSIM_VARIANT", key, dflt); }
+static long test_knob(const char* key, long dflt) { return knob("KSIM_TEST", key, dflt); }
 
 static int check_gfx950(int dev) {
   int n = 0;
@@ -2137,7 +2160,7 @@ static const double* score_table() {
 struct HPlan {
   int Cmax = 1, Gmax = 1, Smax = 1, Npad = 0, nb = 0;
   int K = 1, S = 0, nbw = 0;      // workgroups per replica, ranks per workgroup, L1 blocks per workgroup
-  bool l2 = false;                // the second maxima beside L1 (the wide form, when they fit in LDS; KSIM_HL2)
+  bool l2 = false;                // the second maxima beside L1 (the wide form, when they fit in LDS; KSIM_VARIANT hl2)
   size_t lds = 0;
   std::vector<int> cg;            // [Rg][2] classes, groups
   std::vector<PodDev> cls, gpod;  // [Rg][Cmax] (sorted by group), [Rg][Gmax]
@@ -2231,14 +2254,12 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
     // keys far beyond L2, 55 flagged rows per refresh from HBM), while one workgroup over an openb cluster
     // keeps its keys in L2 and is bound by F: there L2 only adds update work (profiles/r04/hmemo/).
     // Off by default since r05: in the wide form its code alone cost C5 4.09 -> 4.22 s, and it is compiled only into
-    // the one-workgroup instantiations; KSIM_HL2=1 turns it on there.
-    const char* v = std::getenv("KSIM_HL2");
-    const bool want = v && v[0] == '1' && pl.K == 1;
+    // the one-workgroup instantiations; KSIM_VARIANT=hl2=1 turns it on there.
+    const bool want = variant("hl2", 0) == 1 && pl.K == 1;
     pl.l2 = want && hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, true, 0).total <= 160 * 1024;
   }
-  {  // per-model tables of the typed replicas (KSIM_HMODEL=0: the whole table for every model, as before r05)
-    const char* hm = std::getenv("KSIM_HMODEL");
-    const bool on = !(hm && hm[0] == '0');
+  {  // per-model tables of the typed replicas (KSIM_VARIANT=hmodel=0: the whole table for every model, as before r05)
+    const bool on = variant("hmodel", 1) != 0;
     pl.Mtab = pl.Mslots = 0;
     pl.mtoff.assign((size_t)Rg * KSIM_MAX_TYPES, 0);
     std::vector<std::vector<uint8_t>> mt(Rg);
@@ -2262,7 +2283,13 @@ static bool hmemo_plan(const ksim_engine* e, const std::vector<int>& reps, int s
       pl.Mtab = std::max(pl.Mtab, (int)mt[i].size());
       pl.Mslots = std::max(pl.Mslots, slot);
     }
-    if (pl.Mtab > 4095) return false;
+    // tables that do not fit (a 12-bit offset, or the LDS beside the keys' L1 level): the whole-table form
+    // (KSIM_VARIANT hmodel=0), which evaluates the same bits, rather than no k_hmemo at all
+    if (pl.Mtab > 4095 || hmemo_layout(pl.S, pl.Cmax, pl.Gmax, pl.nbw, pl.l2, pl.Mtab).total > 160 * 1024) {
+      pl.Mtab = pl.Mslots = 0;
+      std::fill(pl.mtoff.begin(), pl.mtoff.end(), 0);
+      for (auto& v : mt) v.clear();
+    }
     pl.mtab.assign((size_t)Rg * std::max(pl.Mtab, 1), 0);
     for (int i = 0; i < Rg; ++i) std::copy(mt[i].begin(), mt[i].end(), pl.mtab.begin() + (size_t)i * std::max(pl.Mtab, 1));
   }
@@ -2366,9 +2393,8 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   if (e->run_mode == 5) return prepare_hmemo(e, reps, max_ev);  // k_hmemo required
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
-  // run_mode 4 (or KSIM_MEMO_DECIDER=1 with run_mode 0): the decider variant of k_memo
-  const char* dv = std::getenv("KSIM_MEMO_DECIDER");
-  pl.decider = e->run_mode == 4 || (e->run_mode == 0 && dv && dv[0] == '1');
+  // run_mode 4 (or KSIM_VARIANT=memo_decider=1 with run_mode 0): the decider variant of k_memo
+  pl.decider = e->run_mode == 4 || (e->run_mode == 0 && variant("memo_decider", 0) == 1);
   if (!memo_plan(e, reps, pl)) return e->run_mode == 0 ? prepare_hmemo(e, reps, max_ev) : KSIM_OK;
   const int Rg = (int)reps.size();
   int rc;
@@ -2417,12 +2443,9 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   return KSIM_OK;
 }
 
-// KSIM_HDELAY=<mask>: the memoised kernels' hand-over stress delays (ksim_memo.hpp hdelay; the bits are
+// KSIM_TEST=hdelay=<mask>: the memoised kernels' hand-over stress delays (ksim_memo.hpp hdelay; the bits are
 // per kernel); a nonzero mask selects the general (non-lean) instantiation, which alone carries them.
-static int hdelay_mask() {
-  const char* v = std::getenv("KSIM_HDELAY");
-  return v ? (int)(std::strtol(v, nullptr, 0) & 0xff) : 0;
-}
+static int hdelay_mask() { return (int)(test_knob("hdelay", 0) & 0xff); }
 
 static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, int max_ev) {
   int rc;
@@ -2455,10 +2478,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ma.decider = pl.decider ? 1 : 0;
   ma.ev_cls = e->d_m_evcls;
   ma.topg = e->d_topg;
-  {
-    const char* sk = std::getenv("KSIM_SKIP");
-    ma.skip = !(sk && sk[0] == '0');
-  }
+  ma.skip = variant("skip", 1) != 0;
   ma.delay = hdelay_mask();
   const char* pe = std::getenv("KSIM_PROFILE");
   const bool profile = pe && pe[0] == '1';
@@ -2480,7 +2500,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   // the general instantiation for the profile / trace / report / deletes / no score table, else the lean one
   const bool general = profile || tracing || e->report || !e->d_th ||
                        std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; });
-  // KSIM_HDELAY: the lean kernel with the stress delays compiled in (or the general one, which has them)
+  // the hdelay test knob: the lean kernel with the stress delays compiled in (or the general one, which has them)
   const void* f = pl.decider ? (const void*)ksim_memo::k_memo<true, true>
                   : general ? (const void*)ksim_memo::k_memo<false, true>
                   : ma.delay ? (const void*)ksim_memo::k_memo<false, false, true> : (const void*)ksim_memo::k_memo<false, false>;
@@ -2671,23 +2691,23 @@ static ksim_hmemo::HMemoArgs hmemo_args(ksim_engine* e, int first, int stride) {
     std::iota(all.begin(), all.end(), 0);
     ma.skip = dead_skip(e, all) ? 1 : 0;
   }
-  {  // KSIM_HPF (one workgroup per replica): 1 = wave 0 lists the next refresh (the default since r04: C4 190.7 ->
+  {  // KSIM_VARIANT hpf (one workgroup per replica): 1 = wave 0 lists the next refresh (the default since r04: C4 190.7 ->
      // 178-185 ms, C2 run_mode 5 50.3 -> 47.7 ms, profiles/r04/memo/ab_runs.txt), 2 = touches its flagged rows, 0 = off
-    const char* pf = std::getenv("KSIM_HPF");
-    ma.pf = pf ? std::atoi(pf) & 7 : 1;  // (4: the wide form lists on wave 0 too)
+    ma.pf = (int)variant("hpf", 1) & 7;  // (4: the wide form lists on wave 0 too)
   }
   ma.delay = hdelay_mask();
-  {  // KSIM_HPRUNE (A/B): the F list's group pruning for replicas with more than this many typical pods
+  {  // KSIM_VARIANT hprune (A/B): the F list's group pruning for replicas with more than this many typical pods
     // (-1: every replica; default 64: the large typed tables, where the F rounds bound the step)
-    const char* pr = std::getenv("KSIM_HPRUNE");
-    ma.prune_t = pr ? std::atoi(pr) : 64;
+    ma.prune_t = (int)variant("hprune", 64);
   }
   for (int q = 0; q < kMaxPeers; ++q) ma.peer[q] = nullptr;
   return ma;
 }
 
+// started: the residency gate's flags (K = 1 only); *gated tells the caller whether the launch carries them --
+// not when its Rg workgroups cannot all be resident at once (a gate that could never open)
 static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream_t st, int* started = nullptr,
-                        int gate_epoch = 0) {
+                        int gate_epoch = 0, bool* gated = nullptr) {
   using namespace ksim_hmemo;
   const HPlan& pl = *e->hplan;
   const int stride = std::max(max_ev, 1);
@@ -2696,6 +2716,7 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   HMemoArgs ma = hmemo_args(e, first, stride);
   ma.started = pl.K == 1 ? started : nullptr;
   ma.gate_epoch = gate_epoch;
+  if (gated) *gated = false;
   bool any_delete = false;
   for (const int r : e->mplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
   if (pl.K > 1) {
@@ -2727,6 +2748,8 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
     std::fprintf(stderr, "ksim: k_hmemo needs %d co-resident workgroups\n", Rg * pl.K);
     return KSIM_ERANGE;
   }
+  if (ma.started && Rg > resident_cap(e, f, pl.lds)) ma.started = nullptr;
+  if (gated) *gated = ma.started != nullptr;
   const TypDev* tpp = e->d_tp;
   const int lrc = launch_persistent(f, Rg * pl.K, kHBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
   if (lrc) return lrc;
@@ -2839,9 +2862,9 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     // the profiler passes of scripts/profile_config.sh use it -- rocprofv3 7.2 faults at process exit
     // after a cooperative launch
     if (const char* c = std::getenv("KSIM_COOP")) e->coop = std::atoi(c) != 0;
-    // KSIM_SCAN1: single-workgroup cheap-policy groups on k_scan1 with the records in VGPRs (2, default),
+    // KSIM_VARIANT scan1: single-workgroup cheap-policy groups on k_scan1 with the records in VGPRs (2, default),
     // in LDS (1), or on k_replay (0) -- A/B switches
-    if (const char* c = std::getenv("KSIM_SCAN1")) e->scan1 = std::atoi(c);
+    e->scan1 = (int)variant("scan1", 2);
   }
   e->bpr = (n_nodes + e->NB - 1) / e->NB;
   e->tags_stride = (size_t)n_nodes * kTagStride + (size_t)n_nodes * 2;  // + int rank2idx[N]
@@ -3651,10 +3674,9 @@ static size_t replay_lds(int S, int pol, bool general) {  // S real slots + the 
 // The dead-class skip (k_memo, k_hmemo, k_scan1): on create-only streams a class that once found no
 // feasible node never finds one again (Filter is monotone in the resources a creation takes), so its
 // later events are decided without a scan.  Needs every replica create-only with class ids < 1024;
-// KSIM_SKIP=0 turns it off (A/B runs).
+// KSIM_VARIANT=skip=0 turns it off (A/B runs).
 static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps) {
-  const char* sk = std::getenv("KSIM_SKIP");
-  if (sk && sk[0] == '0') return false;
+  if (variant("skip", 1) == 0) return false;
   for (int r : reps)
     if (e->has_delete[r] || e->h_cls[r].size() > 1024) return false;
   return true;
@@ -3663,6 +3685,17 @@ static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps) {
 // One k_replay launch per policy present (the kernel is specialised on the policy);
 // launches of different policies run back to back on the engine stream.
 constexpr int kPolRandomGo = 64;  // run_persistent's group id of the k_random_go replicas
+
+static void note_kernel(ksim_engine* e, const char* name) {
+  for (size_t p = 0; p < e->last_kernels.size();) {  // each name once
+    size_t q = e->last_kernels.find('+', p);
+    if (q == std::string::npos) q = e->last_kernels.size();
+    if (e->last_kernels.compare(p, q - p, name) == 0) return;
+    p = q + 1;
+  }
+  if (!e->last_kernels.empty()) e->last_kernels += '+';
+  e->last_kernels += name;
+}
 
 static int run_persistent(ksim_engine* e, int max_ev) {
   std::vector<int> order;
@@ -3730,8 +3763,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   // launch (policy per workgroup), its replicas longest stream first: the run then needs one side stream
   // beside the FGD group's, whatever the hardware-queue mapping of the process.
   const bool reg1 = e->scan1 == 2 && e->N <= ksim_scan1::kBlock * ksim_scan1::kRegSlots;
-  const char* mixe = std::getenv("KSIM_SCAN1_MIX");
-  if (concurrent && !any_delete && e->scan1 && e->N <= kMaxSlice && !(mixe && mixe[0] == '0') &&
+  if (concurrent && !any_delete && e->scan1 && e->N <= kMaxSlice && variant("scan1_mix", 1) != 0 &&
       ksim_scan1::scan1_lds(e->N, ksim_scan1::kPolMix, e->report, reg1) <= 160 * 1024) {
     std::vector<int> mix, norder;
     std::vector<std::pair<int, int>> ngroups;
@@ -3808,6 +3840,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         hipLaunchKernelGGL(ksim_random_go::k_random_go<false>, dim3(Rg), dim3(ksim_random_go::kBlock), lds, gs, ga);
       }
       KSIM_HIP(hipGetLastError());
+      note_kernel(e, "k_random_go");
       e->last_groups = (int)groups.size();
       e->last_rgo += Rg;
       first += Rg;
@@ -3823,6 +3856,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       void* params[] = {(void*)&sa};
       KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
+      note_kernel(e, "k_scan1_mix");
       e->last_K = 1;
       e->last_groups = (int)groups.size();
       e->last_scan1 += Rg;
@@ -3835,6 +3869,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         const MemoPlan& pl = *e->mplan;
         const int rc = launch_memo(e, pl, Rg, first, max_ev);
         if (rc) return rc;
+        note_kernel(e, "k_memo");
         e->last_K = pl.K;
         e->last_groups = (int)groups.size();
         e->last_memo += Rg;
@@ -3844,12 +3879,11 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         continue;
       }
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
-        // The residency gate (concurrent groups behind a K = 1 FGD group; KSIM_C4_GATE=0 off): the long FGD
+        // The residency gate (concurrent groups behind a K = 1 FGD group; KSIM_VARIANT gate=0 off): the long FGD
         // replays take their CUs before any short group's workgroup is dispatched, so none of them waits
         // for a CU that short replays hold.  The host waits for every workgroup's start flag (bounded: a
         // gate that does not open in 2 s lets the launches go on, it orders work, it decides nothing).
-        const char* ge = std::getenv("KSIM_C4_GATE");
-        const bool gate = concurrent && gidx == 1 && groups.size() >= 2 && e->hplan->K == 1 && !(ge && ge[0] == '0');
+        const bool gate = concurrent && gidx == 1 && groups.size() >= 2 && e->hplan->K == 1 && variant("gate", 1) != 0;
         if (gate && Rg > e->started_cap) {
           if (e->h_started) KSIM_HIP(hipHostFree(e->h_started));
           e->h_started = nullptr;
@@ -3859,17 +3893,26 @@ static int run_persistent(ksim_engine* e, int max_ev) {
           e->started_cap = Rg;
         }
         const int epoch = gate ? (e->gate_epoch = (e->gate_epoch % 0x3fffffff) + 1) : 0;
-        const int rc = launch_hmemo(e, Rg, first, max_ev, gs, gate ? e->d_started : nullptr, epoch);
+        bool gated = false;
+        const int rc = launch_hmemo(e, Rg, first, max_ev, gs, gate ? e->d_started : nullptr, epoch, &gated);
         if (rc) return rc;
-        if (gate) {
+        if (gated) {
           const auto t0 = std::chrono::steady_clock::now();
           volatile int* fl = e->h_started;
+          e->last_gate = 1;
           for (int w = 0; w < Rg;) {
             if (fl[w] == epoch) { ++w; continue; }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+              e->last_gate = -1;
+              ++e->gate_timeouts;
+              std::fprintf(stderr, "ksim: residency gate given up after 2 s (%d of %d FGD workgroups started); the "
+                           "concurrent groups launch unordered\n", w, Rg);
+              break;
+            }
             std::this_thread::yield();
           }
         }
+        note_kernel(e, e->hplan->K == 1 ? "k_hmemo" : "k_hmemo_wide");
         e->last_K = e->hplan->K;
         e->last_groups = (int)groups.size();
         e->last_hmemo += Rg;
@@ -3892,6 +3935,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       void* params[] = {(void*)&sa};
       KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
+      note_kernel(e, "k_scan1");
       e->last_K = 1;
       e->last_groups = (int)groups.size();
       e->last_scan1 += Rg;
@@ -3924,11 +3968,10 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     size_t lds = replay_lds(S, gp.first, general);
     // PWR+FGD: the per-(class, slot) memo when every class of the group fits beside the slice
-    // (KSIM_PF_MEMO=0: evaluate every slot every step, as before r04)
+    // (KSIM_VARIANT pf_memo=0: evaluate every slot every step, as before r04)
     int pm_c = 0;
     if (gp.first == POL_PWR_FGD) {
-      const char* pm = std::getenv("KSIM_PF_MEMO");
-      if (!(pm && pm[0] == '0')) {
+      if (variant("pf_memo", 1) != 0) {
         for (int j = first; j < first + Rg; ++j) pm_c = std::max(pm_c, (int)e->h_cls[order[j]].size());
         const size_t lm = ksim_replay::replay_layout(S, gp.first, general, pm_c).total;
         if (pm_c > 0 && lm <= 160 * 1024 &&
@@ -3942,11 +3985,9 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     ksim_replay::ReplayArgs ra;
     ra.pm_c = pm_c;
     {
-      const char* v0 = std::getenv("KSIM_PF_MEMO_VER0");
-      const long v = v0 ? std::atol(v0) : 0;
+      const long v = test_knob("pf_memo_ver0", 0);
       ra.pm_ver0 = v > 0 && v < (long)ksim_replay::kPmInvalid ? (unsigned)v : 0u;
-      const char* pg = std::getenv("KSIM_PF_GUESS");
-      ra.pf_guess = pg && pg[0] == '0' ? 0 : 1;
+      ra.pf_guess = test_knob("pf_guess", 1) != 0 ? 1 : 0;
     }
     ra.reps = e->d_reps;
     ra.rep_list = e->d_replist + first;
@@ -3978,6 +4019,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     const TypDev* tp = e->d_tp;
     const int lrc = launch_persistent(replay_kernel(gp.first, K, general), grid, ksim_replay::kRBlock, lds, gs, e->coop && K > 1, ra, tp);
     if (lrc) return lrc;
+    note_kernel(e, "k_replay");
     e->last_K = K;
     e->last_groups = (int)groups.size();
     first += Rg;
@@ -4053,6 +4095,8 @@ int ksim_engine_run(ksim_engine* e) {
   e->tev_used = 0u;  // KSIM_GROUP_TIMES: only run_persistent's concurrent groups record side-stream ends
   e->last_launches = 0;
   e->last_streams = 0;
+  e->last_gate = 0;
+  e->last_kernels.clear();
   int rc = prepare_memo(e, max_ev);
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev0, e->stream));
@@ -4070,6 +4114,8 @@ int ksim_engine_run(ksim_engine* e) {
   if (e->shard_world > 0 && !e->peers.empty()) rc = run_hmemo_peer(e, max_ev);
   else if (e->shard_world > 0) rc = any_pwr(e) ? KSIM_ENOTSUP : run_sharded(e, max_ev);
   else rc = step_path ? run_graph(e, max_ev) : run_persistent(e, max_ev);
+  if (!rc && e->shard_world > 0) note_kernel(e, !e->peers.empty() ? "k_hmemo_wide" : "k_step");
+  if (!rc && step_path) note_kernel(e, any_pwr(e) ? "k_step+k_step_pwr" : "k_step");
   if (rc) return rc;
   KSIM_HIP(hipEventRecord(e->ev_mid, e->stream));
   if (e->report && !e->report_done) {
@@ -4217,8 +4263,8 @@ int ksim_engine_set_shard_peers(ksim_engine* e, const uint8_t* handles) {
   if (e->shard_world < 1 || !e->d_pgran || e->pgran_handle.empty() || !e->peers.empty()) return KSIM_ESTATE;
   KSIM_HIP(hipSetDevice(e->device));
   const int world = e->shard_world;
-  if (const char* ep = std::getenv("KSIM_PEER_EPOCH0"))  // tests: start the run epoch near its wrap
-    e->peer_epoch = (int)(std::strtol(ep, nullptr, 0) & 0xffffff);
+  if (const long ep = test_knob("peer_epoch0", 0))  // tests: start the run epoch near its wrap
+    e->peer_epoch = (int)(ep & 0xffffff);
   e->peers.assign(world, nullptr);
   e->peer_opened.assign(world, 0);
   if (e->pgran_handle.empty() ||
@@ -4344,8 +4390,7 @@ static int run_hmemo_peer(ksim_engine* e, int max_ev) {
 // world x K granule columns: selectHost over the union (generic_scheduler.go:187-212), the owner of the
 // winner binds.  Results carry global ranks as the k_step shards' do (ksim/shard.py merge_results).
 static bool hmemo_group_eligible(ksim_engine* const* engines, int world) {
-  const char* v = std::getenv("KSIM_SHARD_HMEMO");
-  if (v && v[0] == '0') return false;
+  if (variant("shard_hmemo", 1) == 0) return false;
   if (!score_table()) return false;
   for (int k = 0; k < world; ++k) {
     const ksim_engine* e = engines[k];
@@ -4382,7 +4427,7 @@ static int run_hmemo_group(ksim_engine* const* engines, int world, int max_ev, b
     e->mplan_dirty = true;  // the unsharded plan is not this one
     lds = std::max(lds, e->hplan->lds);
   }
-  const bool gen = hdelay_mask() != 0;  // KSIM_HDELAY: the general instantiation
+  const bool gen = hdelay_mask() != 0;  // the hdelay test knob: the general instantiation
   const void* f = Kt <= 64 ? (gen ? (const void*)k_hmemo_group<1, true> : (const void*)k_hmemo_group<1, false>)
                            : (gen ? (const void*)k_hmemo_group<4, true> : (const void*)k_hmemo_group<4, false>);
   if (Kt > resident_cap(e0, f, lds)) return KSIM_OK;
@@ -4460,8 +4505,11 @@ int ksim_shard_group_run(ksim_engine* const* engines, int world) {
   if (hmemo_group_eligible(engines, world)) {
     bool done = false;
     const int rc = run_hmemo_group(engines, world, max_ev, &done);
+    if (!rc && done)
+      for (int k = 0; k < world; ++k) engines[k]->last_kernels = "k_hmemo_group";
     if (rc || done) return rc;
   }
+  for (int k = 0; k < world; ++k) engines[k]->last_kernels = "k_step";
   if (!e0->d_ptrs) KSIM_HIP(hipMalloc(&e0->d_ptrs, sizeof(unsigned long long*) * 32));
   std::vector<unsigned long long*> ptrs(32, nullptr);
   for (int k = 0; k < world; ++k) {
@@ -4567,6 +4615,20 @@ int ksim_engine_last_run_launches(ksim_engine* e, int* launches, int* side_strea
   if (!e || !launches || !side_streams) return KSIM_EINVAL;
   *launches = e->last_launches;
   *side_streams = e->last_streams;
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_kernels(ksim_engine* e, char* out, int cap) {
+  if (!e || !out || cap <= 0) return KSIM_EINVAL;
+  if ((int)e->last_kernels.size() >= cap) return KSIM_ERANGE;
+  std::memcpy(out, e->last_kernels.c_str(), e->last_kernels.size() + 1);
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_gate(ksim_engine* e, int* gate, long long* timeouts) {
+  if (!e || !gate || !timeouts) return KSIM_EINVAL;
+  *gate = e->last_gate;
+  *timeouts = e->gate_timeouts;
   return KSIM_OK;
 }
 

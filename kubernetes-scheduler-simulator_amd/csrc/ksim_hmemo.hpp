@@ -110,11 +110,11 @@ struct HMemoArgs {
   unsigned long long* peer[kMaxPeers];
   int skip;                 // the dead-class skip (create-only streams; class slots < 1024)
   int pf;                   // one workgroup per replica: 1 (default) = wave 0 lists the next refresh's F evaluations after its
-                            // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_HPF)
-  int delay;                // KSIM_HDELAY (general instantiation only): hand-over stress delays, hdelay() below
+                            // Bind, 2 = it also touches the next refresh's flagged key rows (KSIM_VARIANT hpf)
+  int delay;                // the hdelay test knob (general instantiation only): hand-over stress delays, hdelay() below
   int prune_t;              // list only the score groups some class of which may pass Filter on d (the group's
                             // PodDev holds the least demanding request: min CPU / memory, every accepted GPU
-                            // model) for replicas with more than prune_t typical pods (KSIM_HPRUNE)
+                            // model) for replicas with more than prune_t typical pods (KSIM_VARIANT hprune)
   // Residency gate (a concurrent run's FGD group): each workgroup stores `gate_epoch` into started[its
   // index] (host memory) as it starts, so the host launches the short groups only once every long replay
   // holds its CU.  Null: no gate.
@@ -261,7 +261,7 @@ __device__ __forceinline__ unsigned block_max_excl(const uint4& v, int base, int
   return (unsigned)row_max16((int)m);
 }
 
-// KSIM_HDELAY stress delays (ksim_memo::hdelay).  Bits here: 1 waves 1-15 before reading the step's
+// the hdelay test knob stress delays (ksim_memo::hdelay).  Bits here: 1 waves 1-15 before reading the step's
 // skip condition (the r03 dead-set race: wave 0 decides and marks the class dead first), 2 wave 1 before
 // its F list (the F waves wait on the list hand-over), 4 wave 0 before its decision (the bulk finishes the
 // step first), 8 the class waves before the class pass.  Results must not change (tests/test_gpu_hdelay.py).
@@ -311,7 +311,7 @@ __device__ __forceinline__ void l12_update(unsigned& m1, unsigned& m2, unsigned 
 
 // kSub = ceil(K / 64): the granule columns one polling lane reads (K > 1); kSub = 0: the lean one-
 // workgroup form (K = 1, the exchange compiled out).  kProf: the general instantiation -- the
-// KSIM_PROFILE phase timers and the KSIM_HDELAY stress delays (compiled out of the lean launches, as
+// KSIM_PROFILE phase timers and the the hdelay test knob stress delays (compiled out of the lean launches, as
 // k_memo's: the step loop's scalar registers are what it runs short of).
 // kModel: the instantiation for large typical tables -- the per-model tables (typed replicas) and the F-list
 // pruning (one workgroup per replica)
@@ -336,7 +336,7 @@ __device__ __forceinline__ void hmemo_body(const HMemoArgs& a, const TypDev* __r
   const int N = a.N, nb = a.nbw;  // nb: L1 blocks of this workgroup's slice
   const int lo = w * a.S, ns = min(a.S, N - lo), b0 = lo / kFan;
   const int C = a.cg[2 * gi], G = a.cg[2 * gi + 1];
-  // L2 is compiled into the one-workgroup instantiations only (KSIM_HL2=1): in the wide form its code alone cost C5
+  // L2 is compiled into the one-workgroup instantiations only (KSIM_VARIANT hl2=1): in the wide form its code alone cost C5
   // 4.09 -> 4.22 s (r04 bisect, profiles/r05/hmemo/c5_bisect_r05c26.txt), on or off
   constexpr bool kL2Code = kSub == 0;
   const bool use_l2 = kL2Code && a.l2 != nullptr;

@@ -79,8 +79,8 @@ struct MemoArgs {
   int decider;
   const int* ev_cls;         // [launch replica][win_stride] class of each event, -1 delete
   unsigned* topg;            // [launch replica][win_stride][kTopWords] top granules, zeroed before launch
-  int skip;                  // lean launches: the dead-class skip (KSIM_SKIP=0: off)
-  int delay;                 // KSIM_HDELAY (general and stress instantiations): 1 every wave before the end-of-step
+  int skip;                  // lean launches: the dead-class skip (KSIM_VARIANT skip=0: off)
+  int delay;                 // the hdelay test knob (general and stress instantiations): 1 every wave before the end-of-step
                              // barrier (wave 0 before it receives the step's granule), 2 the owner's critical waves
                              // before their F, 4 every wave at the step start
 };
@@ -342,7 +342,7 @@ __device__ __forceinline__ double wave_F(int cpuL, const uint32_t (&g)[4], int t
   return out;
 }
 
-// KSIM_HDELAY stress delays at the hand-over points of a step (the memoised kernels' general
+// the hdelay test knob stress delays at the hand-over points of a step (the memoised kernels' general
 // instantiations and k_memo's stress instantiation only): a wave about to read something another wave of
 // the same step may be writing sleeps 0-3 x ~3.4 us on about half the steps (a hash of step, wave and
 // workgroup), so the late-reader orders that are rare on an idle chip happen thousands of times per run.
@@ -740,7 +740,7 @@ __device__ void memo_decider(const MemoArgs& a, const ReplicaDev& rp, MemoShared
 // the bench and the paper sweeps)
 // compiles them out of the step loop: this kernel's critical path is sensitive to code size and
 // scalar-register pressure (39.1 -> 35.8 ms per C2 launch for the profile hooks alone).
-// kStress: the lean instantiation plus the KSIM_HDELAY delays (tests only: the dead-class skip is lean-only).
+// kStress: the lean instantiation plus the the hdelay test knob delays (tests only: the dead-class skip is lean-only).
 template <bool kDecider, bool kGeneral, bool kStress = false>
 __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __restrict__ tp_all) {
   constexpr bool kDelays = kGeneral || kStress;

@@ -64,8 +64,8 @@ struct ReplayArgs {
   unsigned long long* prof;  // optional [R*K][8] s_memrealtime phase sums (KSIM_PROFILE=1), else null
   int skip;                  // the dead-class skip (create-only streams; class ids < 1024)
   int pm_c;                  // PWR+FGD: class stride of the per-(class, slot) memo in LDS, 0 = no memo
-  unsigned pm_ver0;          // the slots' first version (KSIM_PF_MEMO_VER0: tests start near the wrap)
-  int pf_guess;              // PWR+FGD: learn each class's ranges (KSIM_PF_GUESS=0: never -- every scored step misses)
+  unsigned pm_ver0;          // the slots' first version (KSIM_TEST pf_memo_ver0: tests start near the wrap)
+  int pf_guess;              // PWR+FGD: learn each class's ranges (KSIM_TEST pf_guess=0: never -- every scored step misses)
 };
 constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 

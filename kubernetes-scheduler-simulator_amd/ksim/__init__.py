@@ -164,6 +164,8 @@ SIGNATURES = {
     "ksim_engine_last_run_steps": (C.c_int, [_VP, _P(C.c_int64)]),
     "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_last_run_launches": (C.c_int, [_VP, _P(C.c_int), _P(C.c_int)]),
+    "ksim_engine_last_run_gate": (C.c_int, [_VP, _P(C.c_int), _P(C.c_longlong)]),
+    "ksim_engine_last_run_kernels": (C.c_int, [_VP, C.c_char_p, C.c_int]),
     "ksim_engine_last_run_path": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
     "ksim_engine_get_reports": (C.c_int, [_VP, C.c_int, _P(Report), C.c_int]),
@@ -665,6 +667,19 @@ class Engine:
         n, s = C.c_int(0), C.c_int(0)
         check(lib().ksim_engine_last_run_launches(self.h, C.byref(n), C.byref(s)), "last_run_launches")
         return n.value, s.value
+
+    def last_run_kernels(self):
+        """The replay kernels the last run() launched, in launch order (e.g. ['k_hmemo', 'k_scan1_mix'])."""
+        buf = C.create_string_buffer(256)
+        check(lib().ksim_engine_last_run_kernels(self.h, buf, 256), "last_run_kernels")
+        return [k for k in buf.value.decode().split("+") if k]
+
+    def last_run_gate(self):
+        """(gate, timeouts): the last run()'s residency gate (0 none, 1 opened, -1 given up at its bound) and the
+        gates this engine gave up so far."""
+        g, t = C.c_int(0), C.c_longlong(0)
+        check(lib().ksim_engine_last_run_gate(self.h, C.byref(g), C.byref(t)), "last_run_gate")
+        return g.value, t.value
 
     def last_run_wgs(self):
         k = C.c_int(0)

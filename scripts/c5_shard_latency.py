@@ -37,8 +37,8 @@ def main():
     for w in a.worlds:
         for mode in ("hmemo", "step"):
             # hmemo: one k_hmemo launch over every shard's slices, one granule exchange per pod (the default);
-            # step: KSIM_SHARD_HMEMO=0, the per-pod k_step + gather + commit launches (round 2's path)
-            os.environ["KSIM_SHARD_HMEMO"] = "1" if mode == "hmemo" else "0"
+            # step: KSIM_VARIANT=shard_hmemo=0, the per-pod k_step + gather + commit launches (round 2's path)
+            os.environ["KSIM_VARIANT"] = "shard_hmemo=%d" % (mode == "hmemo")
             g = SH.ShardGroup(rp.nodes, (arr, n), w)
             g.load_events(rp.events, a.events)
             g.run()
@@ -53,7 +53,7 @@ def main():
                                   "results_equal_unsharded": same})
             print("world %d %s: %.2f us/pod, equal %s" % (w, mode, ms * 1e3 / a.events, same), file=sys.stderr,
                   flush=True)
-    os.environ.pop("KSIM_SHARD_HMEMO", None)
+    os.environ.pop("KSIM_VARIANT", None)
     out["note"] = ("in-process shard group on one device. hmemo: every shard's k_hmemo slices in one launch, the "
                    "pod step's slice maxima exchanged as world x K granules (no host, no collective per pod); "
                    "step: per pod every shard's Filter+Score (k_step mode 2), a gather kernel and the commit. The "

@@ -34,6 +34,8 @@ def kernel_of(name):
               "k_step_pwr", "k_step", "k_shard_commit", "k_shard_gather", "k_reserve", "k_advance"):
         if k in name:
             return k
+    if "k_scan1_mix" in name:
+        return "k_scan1_mix"
     if "k_scan1" in name:
         m = re.search(r"k_scan1<(\d+)", name) or re.search(r"k_scan1ILi(\d+)E", name)
         return "k_scan1<%s>" % (m.group(1) if m else "?")

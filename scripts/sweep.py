@@ -4,8 +4,11 @@ write its curves in the format of the reference's experiments/analysis/expected_
   <out>/compare.json   per (trace, policy): max |ours - reference| of the 10-seed mean curves
                        over arrived-GPU % 0..130; per policy: how many experiments reproduce
                        the reference's row exactly; the sweep's timing
-Multi-GPU: torchrun --nproc-per-node N scripts/sweep.py; rank k replays experiments k::N (no
-collective on the data path); each rank writes its own CSV files (suffix .rank<k>).
+Multi-GPU: torchrun --nproc-per-node N scripts/sweep.py; rank k replays its share of a longest-processing-time
+split by ksim.sweep's cost model (ksim.sweep.shard with plan_costs: experiments by falling estimated replay time,
+each to the least loaded rank; no collective on the data path); each rank writes its own CSV files (suffix
+.rank<k>).  The cost model counts each experiment's events from the Go math/rand replay on the host (cached
+per process).
 """
 import argparse
 import json

@@ -28,9 +28,17 @@ def test_profile_keys():
     assert bench.profile_key(_args(config="c5", sharded=True)) == "c5-sharded"
 
 
-@pytest.mark.parametrize("key,path", [("c2", "k_memo"), ("c4", "memo+k_replay"), ("c5", "k_hmemo"),
-                                      ("c2-rm5", "k_hmemo"), ("c2-BestFit", "k_replay"), ("c2-DotProd", "k_replay"),
-                                      ("c2-PWR", "k_replay"), ("c2-PWR_500_FGD_500", "k_replay")])
+def test_rank_share_lines_do_not_borrow_the_whole_sweep_profile():
+    # a --rank-share line times one share's launches: the whole C4 profile's traffic is not its traffic
+    import bench
+    ns = _args(config="c4", report=True, rank_share="3/8")
+    assert bench.profile_key(ns) == "c4-share3of8"
+    assert bench.profile_rooflines(ns, ["k_hmemo", "k_scan1_mix"]) == (None, None, None)
+
+
+@pytest.mark.parametrize("key,path", [("c2", ["k_memo"]), ("c4", ["k_hmemo", "k_scan1_mix"]), ("c5", ["k_hmemo_wide"]),
+                                      ("c2-rm5", ["k_hmemo"]), ("c2-BestFit", ["k_replay"]), ("c2-DotProd", ["k_replay"]),
+                                      ("c2-PWR", ["k_replay"]), ("c2-PWR_500_FGD_500", ["k_replay"])])
 def test_committed_profiles_feed_the_bench_line(key, path):
     import bench
     pf = bench.profile_file(key)
@@ -52,4 +60,4 @@ def test_committed_profiles_feed_the_bench_line(key, path):
     assert traffic == dom["hbm_bytes_per_dispatch"] and src.endswith(key + "/pmc.json")
     assert valu["frac"] == dom["valu_frac"] and valu["f64_frac"] == dom["f64_frac"]
     # a run that launched another kernel does not borrow this profile
-    assert bench.profile_rooflines(ns, "k_step") == (None, None, None)
+    assert bench.profile_rooflines(ns, ["k_step"]) == (None, None, None)

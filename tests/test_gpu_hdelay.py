@@ -1,16 +1,16 @@
-"""Hand-over stress for the memoised FGD kernels (KSIM_HDELAY, round-3 verdict item 1).
+"""Hand-over stress for the memoised FGD kernels (KSIM_TEST=hdelay=<mask>, round-3 verdict item 1).
 
 k_memo hands its critical F over through an LDS counter (the owner's waves 1-9 to wave 0) and otherwise
 joins on barriers; its delay points: 1 every wave before the end-of-step barrier (wave 0 before it receives
 the granule), 2 the owner's critical waves before their F, 4 every wave at the step start.  The lean kernel
-with them compiled in (KSIM_HDELAY selects it) runs the dead-class skip too.
+with them compiled in (a hdelay mask selects it) runs the dead-class skip too.
 
 k_hmemo has no workgroup barrier inside a step: wave 0 (the event's own class, the decision, the Bind) and
 waves 1-15 (every other class's refresh) hand work over through LDS counters and double-buffered state,
 and join once, at the end-of-step barrier.  A wave that reads something late -- after another wave of the
 same step already wrote the next step's value -- is the failure this design must exclude; r03 shipped one
 (the dead-class set: a late bulk wave read the skip condition after wave 0 had marked the class dead,
-skipped the step and stalled the bulk).  KSIM_HDELAY makes the late orders the common ones:
+skipped the step and stalled the bulk).  The delays make the late orders the common ones:
 the general instantiation sleeps 0-3 x ~3.4 us at the hand-over points on about half the steps (a hash of
 step, wave and workgroup; ksim_hmemo.hpp hdelay).  Every run here must finish without a bounded-wait
 failure (run() raises KSIM_ESTATE on one) and give the decisions k_replay / the oracle give.
@@ -59,9 +59,9 @@ def c2_replay(default_trace):
 @pytest.mark.parametrize("hpf", ["0", "1", "3"])
 def test_hmemo_c2_delays(default_trace, c2_replay, monkeypatch, hpf):
     # the C2 job on k_hmemo at one workgroup per replica (run_mode 5), every delay point on, with wave 0
-    # listing the next refresh (KSIM_HPF=1) and also touching its flagged rows (=3) or not (0)
-    monkeypatch.setenv("KSIM_HDELAY", ALL)
-    monkeypatch.setenv("KSIM_HPF", hpf)
+    # listing the next refresh (hpf=1) and also touching its flagged rows (=3) or not (0)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % ALL)
+    monkeypatch.setenv("KSIM_VARIANT", "hpf=%s" % hpf)
     eng = c2_engine(default_trace, SEEDS, 5)
     try:
         eng.run()
@@ -75,7 +75,7 @@ def test_hmemo_c2_delays(default_trace, c2_replay, monkeypatch, hpf):
 
 def test_hmemo_c2_seed_vs_oracle_with_delays(default_trace, monkeypatch):
     # one full seed against the oracle itself (k_replay is pinned the same way, tests/test_gpu_parity.py)
-    monkeypatch.setenv("KSIM_HDELAY", ALL)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % ALL)
     rp = default_trace.replay(seed=42, tune_ratio=1.3, shuffle=True)
     eng = c2_engine(default_trace, [42], 5)
     try:
@@ -92,9 +92,9 @@ def test_hmemo_c2_seed_vs_oracle_with_delays(default_trace, monkeypatch):
 @pytest.mark.parametrize("hpf", ["1", "5"])
 def test_hmemo_wide_delays(default_trace, c2_replay, monkeypatch, hpf):
     # the wide form (K = 7 co-resident workgroups per replica, the granule exchange per pod) on four C2 seeds;
-    # KSIM_HPF=5: the workgroup that binds lists the next refresh on its wave 0 (bit 4: the wide form too)
-    monkeypatch.setenv("KSIM_HDELAY", ALL)
-    monkeypatch.setenv("KSIM_HPF", hpf)
+    # hpf=5: the workgroup that binds lists the next refresh on its wave 0 (bit 4: the wide form too)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % ALL)
+    monkeypatch.setenv("KSIM_VARIANT", "hpf=%s" % hpf)
     eng = c2_engine(default_trace, SEEDS[:4], 5, wgs=7)
     try:
         eng.run()
@@ -132,7 +132,7 @@ def test_hmemo_c5_prefix_delays(c5, monkeypatch):
     t, rp = c5
     n_ev = 4000
     want, _, _ = _c5_run(t, rp, n_ev, 2)
-    monkeypatch.setenv("KSIM_HDELAY", ALL)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % ALL)
     got, path, k = _c5_run(t, rp, n_ev, 0)
     assert path == "k_hmemo" and k == 63
     assert got == want
@@ -144,7 +144,7 @@ def test_hmemo_shard_group_delays(c5, monkeypatch):
     t, rp = c5
     n_ev = 3000
     want, _, _ = _c5_run(t, rp, n_ev, 2)
-    monkeypatch.setenv("KSIM_HDELAY", ALL)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % ALL)
     g = SH.ShardGroup(rp.nodes, t.typical(), 3)
     try:
         g.load_events(rp.events, n_ev)
@@ -158,7 +158,7 @@ def test_hmemo_shard_group_delays(c5, monkeypatch):
 @pytest.mark.parametrize("mask", ["0x7", "0x1", "0x6"])
 def test_memo_c2_delays(default_trace, c2_replay, monkeypatch, mask):
     # the C2 job on k_memo (run_mode 3: 25 co-resident workgroups per replica), the lean kernel with the delays
-    monkeypatch.setenv("KSIM_HDELAY", mask)
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % mask)
     eng = c2_engine(default_trace, SEEDS, 3)
     try:
         eng.run()
@@ -172,7 +172,7 @@ def test_memo_c2_delays(default_trace, c2_replay, monkeypatch, mask):
 
 def test_memo_deletes_report_delays(default_trace, monkeypatch):
     # the general k_memo (a create / delete stream with the per-event report) with every delay point on
-    monkeypatch.setenv("KSIM_HDELAY", "0x7")
+    monkeypatch.setenv("KSIM_TEST", "hdelay=%s" % "0x7")
     rp = default_trace.replay(seed=44, tune_ratio=1.3, shuffle=True)
     keep = list(range(0, default_trace.num_nodes, 3))
     evs, oev = helpers.delete_stream(default_trace, rp, 1500, p_delete=0.3, seed=5)

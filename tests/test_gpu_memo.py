@@ -8,6 +8,7 @@ event changed; in decider mode (run_mode 4) workgroup 0 decides every event from
 top lists, kLag events old, plus the fresh keys of the nodes changed since; the bar is the same as every other path: bit-exact (node, GPU set, score, feasible
 count, status) per event and the same final cluster state.  Every test needs a gfx950 device.
 """
+import numpy as np
 import pytest
 
 import helpers
@@ -235,15 +236,42 @@ def test_hmemo_cluster_report(default_trace, wgs):
     assert reps[HMEMO] == reps[SCAN]
 
 
-@pytest.mark.parametrize("knobs", [{"KSIM_HPRUNE": "-1"}, {"KSIM_HMODEL": "0"}, {"KSIM_HMODEL": "0", "KSIM_HPRUNE": "100000"},
-                                   {"KSIM_HL2": "1"}],
+def test_hmemo_per_model_tables_that_do_not_fit():
+    # r05 advisor: a typed replica whose per-model tables exceed their 12-bit offsets (25 GPU models x 200 GPU typical
+    # pods accepting every model = 5 000 entries) runs k_hmemo on the whole table, bit-exact, instead of refusing it
+    from fuzz_cases import _mask, make_case
+    from test_gpu_fuzz import check_state, run_engine
+    models = [chr(ord("a") + i) for i in range(25)]  # one-letter names: the oracle keeps a spec in 64 bytes
+    case = make_case(11, 400, 1500, models=models)
+    vocab = models + ["H100"]
+    assert len({n["model"] for n in case["onodes"] if n["gpu"]}) == 25
+    spec = "|".join(models)
+    rnd = np.random.default_rng(3)
+    otyp = [(int(c), 0, 0, "", 0.002) for c in (500, 1000, 4000, 8000)]
+    for k in range(200):
+        milli, num = (int(rnd.choice([100, 250, 500, 700])), 1) if k % 2 else (1000, int(rnd.choice([1, 2, 4, 8])))
+        otyp.append((int(rnd.choice([0, 4000, 16000])), milli, num, spec, 0.004))
+    typ = (ksim.Typical * len(otyp))()
+    for i, (cpu, milli, num, sp, freq) in enumerate(otyp):
+        typ[i].cpu_milli, typ[i].gpu_milli, typ[i].gpu_count = cpu, milli, num
+        typ[i].type_mask, typ[i].freq = _mask(sp, vocab), freq
+    case.update(typical=typ, typical_n=len(otyp), otypical=otyp)
+    want, want_state, _ = O.run_events(case["onodes"], otyp, case["oevents"], policy=O.POL_FGD, gpu_sel=O.SEL_FGD,
+                                       threads=16)
+    got, state = run_engine(case, "FGD", HMEMO, wgs=1)  # run_mode 5: k_hmemo or an error, never another path
+    assert got == want
+    check_state(state, want_state)
+
+
+@pytest.mark.parametrize("knobs", [{"KSIM_VARIANT": "hprune=-1"}, {"KSIM_VARIANT": "hmodel=0"},
+                                   {"KSIM_VARIANT": "hmodel=0,hprune=100000"}, {"KSIM_VARIANT": "hl2=1"}],
                          ids=["prune-all", "whole-table", "r04-form", "l2"])
 @pytest.mark.parametrize("trace_name", ["gpuspec33", "gpuspec10", "default"])
 def test_hmemo_list_and_table_forms(trace_name, knobs, monkeypatch):
     # r05: k_hmemo's F list without the groups no class of which passes Filter on d (by default for tables of
     # more than 64 typical pods; -1: every replica), and per GPU model the typical table cut to the pods that
-    # accept the model plus the precomputed NA bin (typed replicas; KSIM_HMODEL=0 the whole table), and the
-    # per-(class, block) second maxima (KSIM_HL2=1: one workgroup per replica only, compiled out of the wide form):
+    # accept the model plus the precomputed NA bin (typed replicas; hmodel=0 the whole table), and the
+    # per-(class, block) second maxima (hl2=1: one workgroup per replica only, compiled out of the wide form):
     # every form decides as the oracle does, one workgroup per replica and the wide form
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)

@@ -395,9 +395,9 @@ def test_full_openb_baselines(default_trace, name, pol, sel):
 @pytest.mark.parametrize("name,pol,sel", POLICIES[1:], ids=[p[0] for p in POLICIES[1:]])
 def test_full_openb_baselines_single_workgroup(default_trace, name, pol, sel, scan1, monkeypatch):
     # one workgroup per replica, create-only stream, no report: the 256-thread k_scan1 (the paper
-    # sweep's cheap-policy groups), node records in LDS or (KSIM_SCAN1=2) in VGPRs; bit-exact per
+    # sweep's cheap-policy groups), node records in LDS or (KSIM_VARIANT=scan1=2) in VGPRs; bit-exact per
     # event and in the final state
-    monkeypatch.setenv("KSIM_SCAN1", scan1)
+    monkeypatch.setenv("KSIM_VARIANT", "scan1=%s" % scan1)
     rp = default_trace.replay(seed=44)
     arr, n = default_trace.typical()
     eng = ksim.Engine(default_trace.num_nodes, 1, wgs_per_replica=1)

@@ -168,13 +168,14 @@ def test_errors(default_trace):
     eng.close()
 
 
-@pytest.mark.parametrize("env", [{"KSIM_PF_MEMO": "0"}, {"KSIM_PF_MEMO_VER0": str(0x3fff - 3)}, {"KSIM_PF_GUESS": "0"}],
+@pytest.mark.parametrize("env", [{"KSIM_VARIANT": "pf_memo=0"}, {"KSIM_TEST": "pf_memo_ver0=%d" % (0x3fff - 3)},
+                                 {"KSIM_TEST": "pf_guess=0"}],
                          ids=["memo-off", "version-wrap", "no-guess"])
 def test_pf_memo_off_and_version_wrap(default_trace, monkeypatch, env):
     # k_replay<PWR+FGD> keeps every class's Filter + Score of every slot in LDS while the slot's record is
     # unchanged (the default): without the memo, and with the slot versions starting three changes before
     # their 14-bit field wraps (every entry of a wrapping slot is forgotten first), the decisions stay the
-    # oracle's -- the subset replay at the default K and at K = 1.  KSIM_PF_GUESS=0: no class ever has a
+    # oracle's -- the subset replay at the default K and at K = 1.  KSIM_TEST=pf_guess=0: no class ever has a
     # guessed NormalizeScore range, so every step with two or more feasible nodes takes the miss round (and its
     # owner the re-evaluation when its winner is not the virtual node)
     for k, v in env.items():

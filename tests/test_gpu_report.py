@@ -178,6 +178,9 @@ def test_report_concurrent_groups_side_streams(default_trace, monkeypatch, side)
         launches, streams = eng.last_run_launches()
         assert launches == 2 and streams == min(2, int(side))
         assert eng.last_report_ms() > 0
+        # the cheap launch waited for every FGD workgroup's start flag, and the gate opened within its bound
+        assert eng.last_run_gate() == (1, 0)
+        assert eng.last_run_kernels() == ["k_hmemo", "k_scan1_mix"]
         got = [(eng.results(r), eng.reports(r)) for r in range(len(cfgs))]
     finally:
         eng.close()

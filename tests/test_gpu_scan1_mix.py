@@ -4,7 +4,7 @@ A concurrent run (the paper sweep's shape: every group at one workgroup per repl
 BestFit, DotProduct (merge / max), GpuPacking, GpuClustering and hash-Random replicas one launch with
 the policy chosen per workgroup, longest stream first, on one side stream.  Bar: every event and the
 final state bit-exact against the oracle (the same device functions as k_scan1 / k_replay), with and
-without the merge (KSIM_SCAN1_MIX=0: one k_scan1 launch per policy).
+without the merge (KSIM_VARIANT=scan1_mix=0: one k_scan1 launch per policy).
 """
 import pytest
 
@@ -44,7 +44,7 @@ def check_state(state, want_state):
 @pytest.mark.parametrize("report", [False, True], ids=["plain", "report"])
 @pytest.mark.parametrize("mix", ["1", "0"], ids=["mix", "per-policy"])
 def test_cheap_groups_in_one_launch(trace, mix, report, monkeypatch):
-    monkeypatch.setenv("KSIM_SCAN1_MIX", mix)
+    monkeypatch.setenv("KSIM_VARIANT", "scan1_mix=%s" % mix)
     rp = trace.replay(seed=44)
     arr, n = trace.typical()
     eng = ksim.Engine(trace.num_nodes, len(CASES), wgs_per_replica=1)
@@ -83,7 +83,7 @@ def test_cheap_groups_in_one_launch(trace, mix, report, monkeypatch):
 def test_dotprod_other_configs_keep_their_own_launch(trace, monkeypatch):
     # a DotProduct replica outside the paper's merge / max configuration is not merged (the mix kernel
     # carries only the closed form): its group keeps a k_scan1 launch of its own, beside the merged one
-    monkeypatch.setenv("KSIM_SCAN1_MIX", "1")
+    monkeypatch.setenv("KSIM_VARIANT", "scan1_mix=1")
     rp = trace.replay(seed=45)
     arr, n = trace.typical()
     names = ["BestFit", "DotProd", "GpuPacking"]
@@ -111,7 +111,7 @@ def test_clustering_resumes_from_a_state_with_tags(trace, monkeypatch):
     # GpuClustering's presence bits are built from the tag counts set_nodes gives: replaying the second
     # half of a stream from the state the first half left (tag counts included) decides as the whole
     # replay does.  Both halves run in a mixed launch beside a BestFit replica.
-    monkeypatch.setenv("KSIM_SCAN1_MIX", "1")
+    monkeypatch.setenv("KSIM_VARIANT", "scan1_mix=1")
     rp = trace.replay(seed=46)
     arr, n = trace.typical()
     k = 4000
@@ -146,8 +146,7 @@ def test_nodes_beyond_max_spec_cpu(trace, path, monkeypatch):
     # best_fit_score.go:48-51; NormalizeScore spans any range) and DotProduct's can too (no NormalizeScore: the
     # framework's [0, 100] range check fails the cycle).  Every path -- k_scan1_mix, k_scan1 per policy, k_replay at one and four workgroups per replica (the
     # slices' exchange), k_step -- equals the oracle event by event.
-    monkeypatch.setenv("KSIM_SCAN1_MIX", "1" if path == "mix" else "0")
-    monkeypatch.setenv("KSIM_SCAN1", "0" if path.startswith("replay") else "2")
+    monkeypatch.setenv("KSIM_VARIANT", "scan1_mix=%d,scan1=%d" % (path == "mix", 0 if path.startswith("replay") else 2))
     rp = trace.replay(seed=47)
     arr, n = trace.typical()
     n_ev = 1500

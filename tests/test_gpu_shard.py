@@ -54,8 +54,8 @@ def test_group_fgd_equals_unsharded(default_trace, world):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_group_fgd_step_path_still_equal(default_trace, world, monkeypatch):
-    # KSIM_SHARD_HMEMO=0 keeps round 2's per-pod k_step + gather + commit path for an FGD group
-    monkeypatch.setenv("KSIM_SHARD_HMEMO", "0")
+    # KSIM_VARIANT=shard_hmemo=0 keeps round 2's per-pod k_step + gather + commit path for an FGD group
+    monkeypatch.setenv("KSIM_VARIANT", "shard_hmemo=0")
     rp = default_trace.replay(seed=43)
     n_ev = 600
     g = SH.ShardGroup(rp.nodes, default_trace.typical(), world)
@@ -175,7 +175,7 @@ def _device_rank_main(rank, world, port, n_ev, deletes, q, epoch0=None, n_runs=2
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     if epoch0 is not None:
-        os.environ["KSIM_PEER_EPOCH0"] = epoch0  # the run epoch starts just below its 24-bit wrap
+        os.environ["KSIM_TEST"] = "peer_epoch0=%s" % epoch0  # the run epoch starts just below its 24-bit wrap
     dist.init_process_group("gloo", rank=rank, world_size=world)
     t = ksim.Trace.openb("default")
     rp = t.replay(seed=7)

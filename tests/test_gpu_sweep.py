@@ -28,13 +28,13 @@ POINTS = [20, 40, 60, 80, 90, 100, 110, 120, 130]
 
 @pytest.fixture(scope="module")
 def default_sweep():
-    # the cheap-policy groups with their node records in LDS (KSIM_SCAN1=1); the full sweep below runs
+    # the cheap-policy groups with their node records in LDS (KSIM_VARIANT=scan1=1); the full sweep below runs
     # the default placement (records in VGPRs), so both k_scan1 placements meet the reference's rows
-    os.environ["KSIM_SCAN1"] = "1"
+    os.environ["KSIM_VARIANT"] = "scan1=1"
     try:
         sw = SW.Sweep(SW.plan(traces=["openb_pod_list_default"]))
     finally:
-        del os.environ["KSIM_SCAN1"]
+        del os.environ["KSIM_VARIANT"]
     dev_ms, wall = sw.run()
     curves = sw.curves()
     sw.close()
