@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--rank-share", default="",
                     help="c4 only, 'k/N': time rank k's share of a world-N split of the sweep on this one GPU (the "
                          "1-GPU rehearsal of the N-GPU strong-scaling run: the max over k predicts its time)")
+    ap.add_argument("--no-widen", action="store_true",
+                    help="c4: every replica at one workgroup (no k_memo for a share's longest FGD chains)")
     ap.add_argument("--random-stream", default="hash", choices=["hash", "go"],
                     help="Random policy: the hash contract (default) or the reference's draw structure on Go's "
                          "math/rand stream (k_random_go)")
@@ -333,8 +335,11 @@ def main():
         exps = SW.shard(items, share_k, share_n, SW.plan_costs(items) if share_n > 1 else None)
         # one workgroup per replica unless asked: every policy group then runs concurrently (FGD on k_hmemo, the
         # cheap policies as one k_scan1_mix launch) whatever the share's size -- a share small enough for k_memo
-        # or k_replay at K > 1 would run its groups back to back (profiles/r05/c4_shares/)
-        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs or 1, random_stream=args.random_stream)
+        # or k_replay at K > 1 would run its groups back to back (profiles/r05/c4_shares/).  The share's longest
+        # FGD chains take k_memo at SW.WIDE_K workgroups on the CUs the share leaves free (SW.plan_widths)
+        wide = {} if args.no_widen else SW.plan_widths(exps, SW.plan_costs(exps), SW.plan_costs(exps, "wide"))
+        sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs or 1, random_stream=args.random_stream,
+                         wide=wide)
         eng = sweep.eng
         eng.total_events = sweep.total_events
         eng.memo_replicas = sweep.fgd_replicas()
@@ -445,6 +450,7 @@ def main():
                           "events_per_gpu": total_events, "parallelism": "replicas%d" % world}
         # whole job: every rank's experiments per timed step (the reference: 1020 in ~10 h on 256 vCPU)
         line["experiments_per_s"] = args.replicas * world / (dt / args.steps)
+        line["config"]["widened_fgd"] = len(wide)  # FGD replays on k_memo at SW.WIDE_K workgroups (plan_widths)
         if args.rank_share:
             line["config"]["rank_share"] = args.rank_share
             line["config"]["workload"] += " -- rank %s's share of the LPT split only (%d experiments)" % (

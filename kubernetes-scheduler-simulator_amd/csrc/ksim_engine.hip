@@ -1815,13 +1815,18 @@ struct ksim_engine {
   int* d_m_evo = nullptr;
   int* d_m_evcls = nullptr;     // decider mode: class of each event
   unsigned* d_topg = nullptr;   // decider mode: top granules
-  size_t m_cap2[2] = {0, 0};
+  unsigned* d_m_hkeys = nullptr;  // k_memo with the keys in HBM (MemoPlan::hkeys)
+  size_t m_cap2[3] = {0, 0, 0};
   double* d_th = nullptr;       // FGD score steps (build_score_thresholds), null if unusable
   size_t m_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   struct MemoPlan* mplan = nullptr;  // the FGD replicas' k_memo plan, uploaded before the timed run
   bool mplan_dirty = true;           // events or policies changed since the plan was made
   bool mplan_ok = false;
-  std::vector<int> mplan_reps;
+  std::vector<int> mplan_all;   // the FGD replicas the plans were made for (cache key)
+  std::vector<int> mplan_reps;  // the replicas of the k_memo plan
+  std::vector<int> hplan_reps;  // the replicas of the k_hmemo plan
+  std::vector<int> wgs_hint;    // per replica: workgroups asked by ksim_engine_set_replica_wgs (0: the engine's choice)
+  bool split_fgd = false;       // the wide-hinted FGD replicas on k_memo beside the others on k_hmemo (one run)
   int mplan_max_ev = -1;
   int last_memo = 0;
   // k_hmemo (memoised FGD replay, keys in HBM): the plan and its device tables
@@ -2025,6 +2030,7 @@ static const void* replay_kernel(int pol, int K, bool general) {
 struct MemoPlan {
   int K = 0, Cw = 0, nfw = 0, Cmax = 1;
   bool decider = false;  // workgroup 0 decides, 1..K-1 own the classes
+  bool hkeys = false;    // the keys in HBM (k_memo<..., kHKeys>): classes whose keys do not fit in LDS
   size_t lds = 0;
   std::vector<PodDev> pod;                  // [Rg][Cmax]
   std::vector<int> owner;                   // [Rg][Cmax]
@@ -2035,7 +2041,11 @@ struct MemoPlan {
 // Classes of one replica onto K workgroups, at most Cw slots each.  Classes with the same score
 // request (cpu_nz, milli, num) stay in one workgroup (their candidate states are the same, so one
 // refresh evaluates them once); groups go largest first to the workgroup with the fewest groups.
-static bool memo_assign(const std::vector<PodDev>& cls, int K, int Cw, std::vector<int>& slot_cls, std::vector<int>& owner) {
+// split: a group that fits no workgroup whole is spread over the workgroups with the most free slots
+// (each part's workgroup evaluates the group's candidate states for its own classes: the same keys,
+// the states evaluated once per part) -- the typed gpuspec traces hold groups of up to 60 classes.
+static bool memo_assign(const std::vector<PodDev>& cls, int K, int Cw, std::vector<int>& slot_cls, std::vector<int>& owner,
+                        bool split = false) {
   std::vector<std::pair<std::vector<int32_t>, std::vector<int>>> groups;
   for (int c = 0; c < (int)cls.size(); ++c) {
     const std::vector<int32_t> k{cls[c].cpu_nz, cls[c].milli, cls[c].num};
@@ -2053,89 +2063,118 @@ static bool memo_assign(const std::vector<PodDev>& cls, int K, int Cw, std::vect
     int best = -1;
     for (int w = 0; w < K; ++w)
       if (used[w] + sz <= Cw && (best < 0 || ng[w] < ng[best] || (ng[w] == ng[best] && used[w] < used[best]))) best = w;
-    if (best < 0) return false;
-    for (int c : g.second) {
+    if (best < 0 && !split) return false;
+    for (size_t k = 0; k < g.second.size();) {
+      if (best < 0 || used[best] >= Cw) {  // split: the workgroup with the most free slots
+        best = 0;
+        for (int w = 1; w < K; ++w)
+          if (used[w] < used[best]) best = w;
+        if (used[best] >= Cw) return false;
+        ++ng[best];
+      } else if (k == 0) {
+        ++ng[best];
+      }
+      const int c = g.second[k++];
       slot_cls[(size_t)best * Cw + used[best]] = c;
       owner[c] = (best << 8) | used[best];
       ++used[best];
     }
-    ++ng[best];
   }
   return true;
 }
 
-static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPlan& pl) {
+// forceK > 0: exactly that many workgroups per replica (a wide-hinted group, ksim_engine_set_replica_wgs);
+// hkeys_ok: when no K fits the keys in LDS, the keys may go to HBM (k_memo<..., kHKeys>, classes split over
+// the workgroups as evenly as the slots allow).
+static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPlan& pl, int forceK = 0,
+                      bool hkeys_ok = false) {
   using namespace ksim_memo;
   const int Rg = (int)reps.size();
   if (Rg == 0 || e->N > kMemoMaxRank + 1) return false;
   pl.Cmax = 1;
   for (int r : reps) pl.Cmax = std::max(pl.Cmax, (int)e->h_cls[r].size());
-  int K = e->wgs_req > 0 ? e->wgs_req : std::min(64, e->cus / Rg);
-  if (K < 1 || Rg * K > e->cus) return false;
-  for (;;) {
-    // slots per workgroup: the smallest Cw every replica's classes pack into
-    int Cw = std::max(1, (pl.Cmax + K - 1 - (pl.decider ? 1 : 0)) / std::max(1, K - (pl.decider ? 1 : 0)));
-    std::vector<std::vector<int>> sc(Rg), ow(Rg);
-    const int d0 = pl.decider ? 1 : 0;  // decider mode: classes on workgroups 1..K-1
-    for (;;) {
-      bool ok = Cw <= kMaxCw && K > d0;
+  const int K0 = forceK > 0 ? forceK : e->wgs_req > 0 ? e->wgs_req : std::min(64, e->cus / Rg);
+  if (K0 < 1 || Rg * K0 > e->cus) return false;
+  const int d0 = pl.decider ? 1 : 0;  // decider mode: classes on workgroups 1..K-1
+  std::vector<std::vector<int>> sc(Rg), ow(Rg);
+  // the smallest Cw >= Cw0 every replica's classes pack into (split: parts of a group on several workgroups)
+  auto pack = [&](int K, int Cw0, bool split) {
+    for (int Cw = Cw0; Cw <= kMaxCw; ++Cw) {
+      bool ok = K > d0;
       for (int i = 0; ok && i < Rg; ++i) {
         std::vector<int> s1;
-        ok = memo_assign(e->h_cls[reps[i]], K - d0, Cw, s1, ow[i]);
+        ok = memo_assign(e->h_cls[reps[i]], K - d0, Cw, s1, ow[i], split);
         if (!ok) break;
         sc[i].assign((size_t)K * Cw, -1);
         std::copy(s1.begin(), s1.end(), sc[i].begin() + (size_t)d0 * Cw);
         for (int& o : ow[i]) o += d0 << 8;
       }
-      if (ok || Cw > kMaxCw) break;
-      ++Cw;
+      if (ok) return Cw;
     }
-    int nfw = 0;
-    if (Cw <= kMaxCw)
-      for (int f : {16, 12})  // waves 1..9 need fold buffers on the critical path
-        if (memo_lds(e->N, Cw, f) <= 160 * 1024) { nfw = f; break; }
+    return 0;
+  };
+  auto fold_waves = [&](int Cw, bool hk) {  // waves 1..9 need fold buffers on the critical path
+    for (int f : {16, 12})
+      if (memo_lds(e->N, Cw, f, hk) <= 160 * 1024) return f;
+    return 0;
+  };
+  const void* fcap = (const void*)ksim_memo::k_memo<false, false>;
+  int K = K0, Cw = 0, nfw = 0;
+  bool hk = false;
+  for (;;) {
+    Cw = pack(K, std::max(1, (pl.Cmax + K - 1 - d0) / std::max(1, K - d0)), false);
+    nfw = Cw > 0 ? fold_waves(Cw, false) : 0;
     // every workgroup of the launch must be resident (they exchange granules every step)
-    if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, (const void*)ksim_memo::k_memo<false, false>, memo_lds(e->N, Cw, nfw)))
+    if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw)))
       return false;
-    if (nfw > 0) {
-      pl.K = K;
-      pl.Cw = Cw;
-      pl.nfw = nfw;
-      pl.lds = memo_lds(e->N, Cw, nfw);
-      pl.pod.assign((size_t)Rg * pl.Cmax, PodDev{});
-      pl.owner.assign((size_t)Rg * pl.Cmax, -1);
-      pl.wgcls.assign((size_t)Rg * K * Cw, -1);
-      pl.wgref.assign((size_t)Rg * K * Cw, 0);
-      pl.wggrp.assign((size_t)Rg * K * Cw, 0ull);
-      for (int i = 0; i < Rg; ++i) {
-        const std::vector<PodDev>& cls = e->h_cls[reps[i]];
-        for (size_t c = 0; c < cls.size(); ++c) {
-          pl.pod[(size_t)i * pl.Cmax + c] = cls[c];
-          pl.owner[(size_t)i * pl.Cmax + c] = ow[i][c];
-        }
-        for (int w = 0; w < K; ++w) {
-          const size_t o = ((size_t)i * K + w) * Cw;
-          for (int j = 0; j < Cw; ++j) {
-            const int c = sc[i][(size_t)w * Cw + j];
-            pl.wgcls[o + j] = c;
-            pl.wgref[o + j] = j;
-            if (c < 0) continue;
-            for (int j2 = 0; j2 < j; ++j2) {  // first slot with the same score request
-              const int c2 = sc[i][(size_t)w * Cw + j2];
-              if (c2 >= 0 && cls[c2].cpu_nz == cls[c].cpu_nz && cls[c2].milli == cls[c].milli && cls[c2].num == cls[c].num) {
-                pl.wgref[o + j] = j2;
-                break;
-              }
-            }
-            pl.wggrp[o + pl.wgref[o + j]] |= 1ull << j;
-          }
-        }
+    if (nfw > 0) break;
+    if (hkeys_ok && !pl.decider) {  // the keys in HBM: LDS holds the cluster and the fold buffers only
+      Cw = pack(K, std::max(1, (pl.Cmax + K - 1) / K), true);
+      nfw = Cw > 0 ? fold_waves(Cw, true) : 0;
+      if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw, true))) return false;
+      if (nfw > 0) {
+        hk = true;
+        break;
       }
-      return true;
     }
-    if (e->wgs_req > 0 || K >= 64 || Rg * (K + 1) > e->cus) return false;
+    if (forceK > 0 || e->wgs_req > 0 || K >= 64 || Rg * (K + 1) > e->cus) return false;
     ++K;
   }
+  pl.K = K;
+  pl.Cw = Cw;
+  pl.nfw = nfw;
+  pl.hkeys = hk;
+  pl.lds = memo_lds(e->N, Cw, nfw, hk);
+  pl.pod.assign((size_t)Rg * pl.Cmax, PodDev{});
+  pl.owner.assign((size_t)Rg * pl.Cmax, -1);
+  pl.wgcls.assign((size_t)Rg * K * Cw, -1);
+  pl.wgref.assign((size_t)Rg * K * Cw, 0);
+  pl.wggrp.assign((size_t)Rg * K * Cw, 0ull);
+  for (int i = 0; i < Rg; ++i) {
+    const std::vector<PodDev>& cls = e->h_cls[reps[i]];
+    for (size_t c = 0; c < cls.size(); ++c) {
+      pl.pod[(size_t)i * pl.Cmax + c] = cls[c];
+      pl.owner[(size_t)i * pl.Cmax + c] = ow[i][c];
+    }
+    for (int w = 0; w < K; ++w) {
+      const size_t o = ((size_t)i * K + w) * Cw;
+      for (int j = 0; j < Cw; ++j) {
+        const int c = sc[i][(size_t)w * Cw + j];
+        pl.wgcls[o + j] = c;
+        pl.wgref[o + j] = j;
+        if (c < 0) continue;
+        for (int j2 = 0; j2 < j; ++j2) {  // first slot with the same score request
+          const int c2 = sc[i][(size_t)w * Cw + j2];
+          if (c2 >= 0 && cls[c2].cpu_nz == cls[c].cpu_nz && cls[c2].milli == cls[c].milli && cls[c2].num == cls[c].num) {
+            pl.wgref[o + j] = j2;
+            break;
+          }
+        }
+        pl.wggrp[o + pl.wgref[o + j]] |= 1ull << j;
+      }
+    }
+  }
+  return true;
 }
 
 template <typename T>
@@ -2347,6 +2386,7 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
   const int stride = std::max(max_ev, 1);
   if (!hmemo_plan(e, reps, stride, pl, forceK, forceS)) return KSIM_OK;
   const int Rg = (int)reps.size();
+  e->hplan_reps = reps;
   hipStream_t st = e->stream;
   int rc;
   if ((rc = upload_vec(e->d_h_cg, e->h_cap[0], pl.cg, st))) return rc;
@@ -2378,24 +2418,60 @@ static int prepare_hmemo(ksim_engine* e, const std::vector<int>& reps, int max_e
 
 // Plan and upload the k_memo launch of the FGD replicas (before the timed region of a run; cached
 // until events or policies change).
+static int upload_memo(ksim_engine* e, const std::vector<int>& reps, int max_ev);
+
 static int prepare_memo(ksim_engine* e, int max_ev) {
   if (e->run_mode == 1 || e->run_mode == 2 || e->shard_world > 0) return KSIM_OK;
-  std::vector<int> reps;
+  std::vector<int> reps, wide, narrow;
+  int hint = 0;
   for (int r = 0; r < e->R; ++r)
-    if (e->reps[r].policy == POL_FGD) reps.push_back(r);
-  if (!e->mplan_dirty && reps == e->mplan_reps && max_ev == e->mplan_max_ev) return KSIM_OK;
+    if (e->reps[r].policy == POL_FGD) {
+      reps.push_back(r);
+      (e->wgs_hint[r] > 1 ? wide : narrow).push_back(r);
+      hint = std::max(hint, e->wgs_hint[r]);
+    }
+  if (!e->mplan_dirty && reps == e->mplan_all && max_ev == e->mplan_max_ev) return KSIM_OK;
   e->mplan_dirty = false;
-  e->mplan_reps = reps;
+  e->mplan_all = reps;
   e->mplan_max_ev = max_ev;
   e->mplan_ok = false;
   e->hplan_ok = false;
+  e->split_fgd = false;
+  e->mplan_reps.clear();
+  e->hplan_reps.clear();
   if (reps.empty()) return KSIM_OK;
   if (e->run_mode == 5) return prepare_hmemo(e, reps, max_ev);  // k_hmemo required
   if (!e->mplan) e->mplan = new MemoPlan();
   MemoPlan& pl = *e->mplan;
   // run_mode 4 (or KSIM_VARIANT=memo_decider=1 with run_mode 0): the decider variant of k_memo
   pl.decider = e->run_mode == 4 || (e->run_mode == 0 && variant("memo_decider", 0) == 1);
-  if (!memo_plan(e, reps, pl)) return e->run_mode == 0 ? prepare_hmemo(e, reps, max_ev) : KSIM_OK;
+  // run_mode 0 with some FGD replicas hinted wide (ksim_engine_set_replica_wgs, the paper sweep's longest chains):
+  // those on k_memo at the hinted width (the keys in HBM when they do not fit in LDS), the others on k_hmemo at
+  // one workgroup each, both groups in one concurrent run (run_persistent)
+  if (e->run_mode == 0 && !wide.empty() && !narrow.empty() && !pl.decider) {
+    if (memo_plan(e, wide, pl, hint, true)) {
+      int rc = upload_memo(e, wide, max_ev);
+      if (rc) return rc;
+      rc = prepare_hmemo(e, narrow, max_ev);
+      if (rc) return rc;
+      if (e->hplan_ok && e->hplan->K == 1) {
+        e->split_fgd = true;
+        return KSIM_OK;
+      }
+      e->mplan_ok = false;  // no one-workgroup plan for the others: one plan for every FGD replica, below
+      e->mplan_reps.clear();
+      e->hplan_ok = false;
+    }
+  }
+  const int fk = wide.size() == reps.size() ? hint : 0;  // every FGD replica hinted: that width
+  if (!memo_plan(e, reps, pl, fk, e->run_mode == 3 || fk > 0))
+    return e->run_mode == 0 ? prepare_hmemo(e, reps, max_ev) : KSIM_OK;
+  return upload_memo(e, reps, max_ev);
+}
+
+// Upload the k_memo plan of `reps` (memo_plan made it): the per-class tables, the owner code of every event.
+static int upload_memo(ksim_engine* e, const std::vector<int>& reps, int max_ev) {
+  MemoPlan& pl = *e->mplan;
   const int Rg = (int)reps.size();
   int rc;
   if ((rc = ensure_buf(e->d_m_pod, e->m_cap[0], pl.pod.size()))) return rc;
@@ -2439,6 +2515,8 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
     KSIM_HIP(hipMemcpyAsync(e->d_th, score_table(), sizeof(double) * 102, hipMemcpyHostToDevice, st));
   }
   KSIM_HIP(hipStreamSynchronize(st));  // the host vectors are pageable and short-lived
+  if (pl.hkeys && (rc = ensure_buf(e->d_m_hkeys, e->m_cap2[2], (size_t)Rg * pl.K * pl.Cw * e->N))) return rc;
+  e->mplan_reps = reps;
   e->mplan_ok = true;
   return KSIM_OK;
 }
@@ -2447,9 +2525,12 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
 // per kernel); a nonzero mask selects the general (non-lean) instantiation, which alone carries them.
 static int hdelay_mask() { return (int)(test_knob("hdelay", 0) & 0xff); }
 
-static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, int max_ev) {
+// st: the stream (a concurrent run's side stream, else the engine's); started / gate_epoch: the residency gate's
+// flags (a concurrent run launches the next group once every workgroup of this one has started: a plain launch
+// then, since the device is otherwise idle until the gate opens)
+static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, int max_ev, hipStream_t st,
+                       int* started = nullptr, int gate_epoch = 0) {
   int rc;
-  hipStream_t st = e->stream;
   const int stride = std::max(max_ev, 1);
   KSIM_HIP(hipMemsetAsync(e->d_win, 0, sizeof(unsigned) * (size_t)Rg * stride, st));
   if (pl.decider)
@@ -2478,6 +2559,9 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ma.decider = pl.decider ? 1 : 0;
   ma.ev_cls = e->d_m_evcls;
   ma.topg = e->d_topg;
+  ma.hkeys = pl.hkeys ? e->d_m_hkeys : nullptr;
+  ma.started = started;
+  ma.gate_epoch = gate_epoch;
   ma.skip = variant("skip", 1) != 0;
   ma.delay = hdelay_mask();
   const char* pe = std::getenv("KSIM_PROFILE");
@@ -2497,15 +2581,21 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
     ma.prof = e->d_prof;
   }
-  // the general instantiation for the profile / trace / report / deletes / no score table, else the lean one
-  const bool general = profile || tracing || e->report || !e->d_th ||
+  // the general instantiation for the profile / trace / deletes / no score table, else the lean one (with the
+  // report's stores when the report is on)
+  const bool general = profile || tracing || !e->d_th ||
                        std::any_of(e->mplan_reps.begin(), e->mplan_reps.end(), [&](int r) { return (bool)e->has_delete[r]; });
   // the hdelay test knob: the lean kernel with the stress delays compiled in (or the general one, which has them)
-  const void* f = pl.decider ? (const void*)ksim_memo::k_memo<true, true>
-                  : general ? (const void*)ksim_memo::k_memo<false, true>
-                  : ma.delay ? (const void*)ksim_memo::k_memo<false, false, true> : (const void*)ksim_memo::k_memo<false, false>;
+  using ksim_memo::k_memo;
+  const void* f = pl.decider ? (const void*)k_memo<true, true>
+                  : pl.hkeys ? (general ? (const void*)k_memo<false, true, false, false, true>
+                                        : e->report ? (const void*)k_memo<false, false, false, true, true>
+                                                    : (const void*)k_memo<false, false, false, false, true>)
+                  : general ? (const void*)k_memo<false, true>
+                  : ma.delay ? (const void*)k_memo<false, false, true>
+                  : e->report ? (const void*)k_memo<false, false, false, true> : (const void*)k_memo<false, false>;
   const TypDev* tpp = e->d_tp;
-  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1, ma, tpp);
+  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1 && !started, ma, tpp);
   if (rc) return rc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
@@ -2718,7 +2808,7 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   ma.gate_epoch = gate_epoch;
   if (gated) *gated = false;
   bool any_delete = false;
-  for (const int r : e->mplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
+  for (const int r : e->hplan_reps) any_delete = any_delete || e->has_delete[r];  // the FGD replicas
   if (pl.K > 1) {
     if (any_delete) {
       int rc = ensure_buf(e->d_h_hist, e->h_cap[13], (size_t)Rg * pl.K * stride);
@@ -2739,7 +2829,7 @@ static int launch_hmemo(ksim_engine* e, int Rg, int first, int max_ev, hipStream
   // the large-table instantiations (per-model tables of typed replicas, the F-list pruning) when a replica of
   // the launch has use for them
   bool model = pl.Mtab > 0;
-  for (const int r : e->mplan_reps) model = model || e->reps[r].nt > ma.prune_t;  // the FGD replicas
+  for (const int r : e->hplan_reps) model = model || e->reps[r].nt > ma.prune_t;  // the FGD replicas
   const void* f = pl.K == 1 ? (gen ? (model ? (const void*)k_hmemo<0, true, true> : (const void*)k_hmemo<0, true>)
                                    : (model ? (const void*)k_hmemo<0, false, true> : (const void*)k_hmemo<0, false>))
                   : pl.K <= 64 ? (gen ? (const void*)k_hmemo<1, true> : (const void*)k_hmemo<1, false>)
@@ -2916,6 +3006,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
   e->d_res.assign(n_replicas, nullptr);
   e->n_events.assign(n_replicas, 0);
   e->has_delete.assign(n_replicas, 0);
+  e->wgs_hint.assign(n_replicas, 0);
   e->go_state.assign(n_replicas, {});
   e->h_cls.resize(n_replicas);
   e->h_tp.resize(n_replicas);
@@ -2971,7 +3062,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
                   e->d_cap, e->d_mcap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
-                  e->d_m_evcls, e->d_topg, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
+                  e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
                   e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
   for (void* p : bufs) (void)hipFree(p);
@@ -3150,6 +3241,13 @@ int ksim_engine_set_policy(ksim_engine* e, int replica, int policy, int gpusel, 
   int rc = upload_reps(e);
   if (rc) return rc;
   KSIM_HIP(hipStreamSynchronize(e->stream));
+  return KSIM_OK;
+}
+
+int ksim_engine_set_replica_wgs(ksim_engine* e, int replica, int wgs) {
+  if (!e || replica < 0 || replica >= e->R || wgs < 0 || wgs > 64) return KSIM_EINVAL;
+  e->wgs_hint[replica] = wgs;
+  e->mplan_dirty = true;
   return KSIM_OK;
 }
 
@@ -3685,6 +3783,41 @@ static bool dead_skip(const ksim_engine* e, const std::vector<int>& reps) {
 // One k_replay launch per policy present (the kernel is specialised on the policy);
 // launches of different policies run back to back on the engine stream.
 constexpr int kPolRandomGo = 64;  // run_persistent's group id of the k_random_go replicas
+constexpr int kPolFgdH = 66;      // ... of the one-workgroup FGD replicas on k_hmemo beside wide ones on k_memo (split_fgd)
+
+// The residency gate's host-mapped start flags: n of them, and a fresh epoch the next launch stores into them.
+static int gate_flags(ksim_engine* e, int n, int** d_flags, int* epoch) {
+  if (n > e->started_cap) {
+    if (e->h_started) KSIM_HIP(hipHostFree(e->h_started));
+    e->h_started = nullptr;
+    KSIM_HIP(hipHostMalloc((void**)&e->h_started, sizeof(int) * (size_t)n, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(e->h_started, 0, sizeof(int) * (size_t)n);
+    KSIM_HIP(hipHostGetDevicePointer((void**)&e->d_started, e->h_started, 0));
+    e->started_cap = n;
+  }
+  *d_flags = e->d_started;
+  *epoch = e->gate_epoch = (e->gate_epoch % 0x3fffffff) + 1;
+  return KSIM_OK;
+}
+
+// Wait until the n workgroups of the launch just made have stored `epoch` (bounded: past 2 s the gate gives up,
+// counts it and says so on stderr -- it orders work, it decides nothing).
+static void gate_wait(ksim_engine* e, int n, int epoch, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  volatile int* fl = e->h_started;
+  if (e->last_gate == 0) e->last_gate = 1;
+  for (int w = 0; w < n;) {
+    if (fl[w] == epoch) { ++w; continue; }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      e->last_gate = -1;
+      ++e->gate_timeouts;
+      std::fprintf(stderr, "ksim: residency gate given up after 2 s (%d of %d %s workgroups started); the next "
+                   "groups launch unordered\n", w, n, what);
+      break;
+    }
+    std::this_thread::yield();
+  }
+}
 
 static void note_kernel(ksim_engine* e, const char* name) {
   for (size_t p = 0; p < e->last_kernels.size();) {  // each name once
@@ -3700,7 +3833,13 @@ static void note_kernel(ksim_engine* e, const char* name) {
 static int run_persistent(ksim_engine* e, int max_ev) {
   std::vector<int> order;
   std::vector<std::pair<int, int>> groups;  // (policy, count) in `order`
-  for (int pol = POL_FGD; pol <= POL_PWR_FGD; ++pol) {
+  if (e->split_fgd) {  // the wide FGD replicas (k_memo) first, then the one-workgroup ones (k_hmemo): the plans' orders
+    order = e->mplan_reps;
+    order.insert(order.end(), e->hplan_reps.begin(), e->hplan_reps.end());
+    groups.push_back({POL_FGD, (int)e->mplan_reps.size()});
+    groups.push_back({kPolFgdH, (int)e->hplan_reps.size()});
+  }
+  for (int pol = e->split_fgd ? POL_BESTFIT : POL_FGD; pol <= POL_PWR_FGD; ++pol) {
     int c = 0;
     for (int r = 0; r < e->R; ++r)
       if (e->reps[r].policy == pol && !go_random(e, r)) { order.push_back(r); ++c; }
@@ -3745,7 +3884,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   const bool gen_any = profile || e->report || any_delete;
   for (const auto& gp : groups) {
     if (!concurrent) break;
-    if (gp.first == kPolRandomGo) continue;  // one workgroup per replica
+    if (gp.first == kPolRandomGo || gp.first == kPolFgdH) continue;  // one workgroup per replica
+    if (gp.first == POL_FGD && e->split_fgd) continue;  // the wide k_memo group, launched first behind its gate
     if (gp.first == POL_FGD && e->run_mode != 2 && e->mplan_ok) { concurrent = false; break; }
     if (gp.first == POL_FGD && e->run_mode != 2 && e->hplan_ok) {
       if (e->hplan->K > 1) { concurrent = false; break; }  // a co-resident wide launch
@@ -3867,8 +4007,19 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     if (gp.first == POL_FGD && e->run_mode != 2) {
       if (e->mplan_ok) {  // prepared by prepare_memo (the FGD replicas are the first group of `order`)
         const MemoPlan& pl = *e->mplan;
-        const int rc = launch_memo(e, pl, Rg, first, max_ev);
+        // a concurrent run (split_fgd): on its side stream, the next group launched once all Rg x K workgroups
+        // have started (the gate; without it the later groups' workgroups could hold the CUs a wide replica's
+        // exchange waits on)
+        const bool gate = concurrent && gidx < (int)groups.size();
+        int* flags = nullptr;
+        int epoch = 0;
+        if (gate) {
+          const int rc = gate_flags(e, Rg * pl.K, &flags, &epoch);
+          if (rc) return rc;
+        }
+        const int rc = launch_memo(e, pl, Rg, first, max_ev, gs, flags, epoch);
         if (rc) return rc;
+        if (gate) gate_wait(e, Rg * pl.K, epoch, "FGD k_memo");
         note_kernel(e, "k_memo");
         e->last_K = pl.K;
         e->last_groups = (int)groups.size();
@@ -3878,40 +4029,24 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                                   pl.decider ? " (decider)" : "", Rg, pl.K, pl.Cw, pl.nfw, pl.lds);
         continue;
       }
+    }
+    if ((gp.first == POL_FGD && e->run_mode != 2) || gp.first == kPolFgdH) {
       if (e->hplan_ok) {  // k_hmemo: one workgroup per replica, keys in HBM
         // The residency gate (concurrent groups behind a K = 1 FGD group; KSIM_VARIANT gate=0 off): the long FGD
         // replays take their CUs before any short group's workgroup is dispatched, so none of them waits
         // for a CU that short replays hold.  The host waits for every workgroup's start flag (bounded: a
         // gate that does not open in 2 s lets the launches go on, it orders work, it decides nothing).
-        const bool gate = concurrent && gidx == 1 && groups.size() >= 2 && e->hplan->K == 1 && variant("gate", 1) != 0;
-        if (gate && Rg > e->started_cap) {
-          if (e->h_started) KSIM_HIP(hipHostFree(e->h_started));
-          e->h_started = nullptr;
-          KSIM_HIP(hipHostMalloc((void**)&e->h_started, sizeof(int) * (size_t)Rg, hipHostMallocMapped | hipHostMallocCoherent));
-          std::memset(e->h_started, 0, sizeof(int) * (size_t)Rg);
-          KSIM_HIP(hipHostGetDevicePointer((void**)&e->d_started, e->h_started, 0));
-          e->started_cap = Rg;
+        const bool gate = concurrent && gidx < (int)groups.size() && e->hplan->K == 1 && variant("gate", 1) != 0;
+        int* flags = nullptr;
+        int epoch = 0;
+        if (gate) {
+          const int rc = gate_flags(e, Rg, &flags, &epoch);
+          if (rc) return rc;
         }
-        const int epoch = gate ? (e->gate_epoch = (e->gate_epoch % 0x3fffffff) + 1) : 0;
         bool gated = false;
-        const int rc = launch_hmemo(e, Rg, first, max_ev, gs, gate ? e->d_started : nullptr, epoch, &gated);
+        const int rc = launch_hmemo(e, Rg, first, max_ev, gs, flags, epoch, &gated);
         if (rc) return rc;
-        if (gated) {
-          const auto t0 = std::chrono::steady_clock::now();
-          volatile int* fl = e->h_started;
-          e->last_gate = 1;
-          for (int w = 0; w < Rg;) {
-            if (fl[w] == epoch) { ++w; continue; }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-              e->last_gate = -1;
-              ++e->gate_timeouts;
-              std::fprintf(stderr, "ksim: residency gate given up after 2 s (%d of %d FGD workgroups started); the "
-                           "concurrent groups launch unordered\n", w, Rg);
-              break;
-            }
-            std::this_thread::yield();
-          }
-        }
+        if (gated) gate_wait(e, Rg, epoch, "FGD k_hmemo");
         note_kernel(e, e->hplan->K == 1 ? "k_hmemo" : "k_hmemo_wide");
         e->last_K = e->hplan->K;
         e->last_groups = (int)groups.size();

@@ -83,6 +83,12 @@ struct MemoArgs {
   int delay;                 // the hdelay test knob (general and stress instantiations): 1 every wave before the end-of-step
                              // barrier (wave 0 before it receives the step's granule), 2 the owner's critical waves
                              // before their F, 4 every wave at the step start
+  unsigned* hkeys;           // kHKeys: [launch replica][K][Cw][N] the keys in HBM instead of LDS
+  // Residency gate (a concurrent run's wide FGD group, launched before the other groups): each workgroup stores
+  // `gate_epoch` into started[its block] once it holds its LDS state; the host launches the next group when all
+  // have (ksim_engine.hip run_persistent).  Null: no gate.
+  int* started;
+  int gate_epoch;
 };
 constexpr int kTrace = 4;  // KSIM_PROFILE=2 trace words per workgroup and step
 constexpr int kProfPhases = 24;  // 0-9 phases (thread 0), 10 clock, 11 wall, 12-13 list wave A / C,
@@ -740,9 +746,14 @@ __device__ void memo_decider(const MemoArgs& a, const ReplicaDev& rp, MemoShared
 // the bench and the paper sweeps)
 // compiles them out of the step loop: this kernel's critical path is sensitive to code size and
 // scalar-register pressure (39.1 -> 35.8 ms per C2 launch for the profile hooks alone).
-// kStress: the lean instantiation plus the the hdelay test knob delays (tests only: the dead-class skip is lean-only).
-template <bool kDecider, bool kGeneral, bool kStress = false>
+// kStress: the lean instantiation plus the hdelay test knob's delays (tests only: the dead-class skip is lean-only).
+// kReport (r06): the lean instantiation plus the cluster report's stores (the paper sweep's wide FGD replicas:
+// with the general kernel the report cost them 25 %).  kHKeys (r06): the (class, node) keys in HBM (MemoArgs::hkeys,
+// L2-resident) instead of LDS, for replicas whose classes' keys do not fit beside the cluster (the gpuspec traces:
+// 457 classes); only the key array moves, every other access is the LDS kernel's.
+template <bool kDecider, bool kGeneral, bool kStress = false, bool kReport = false, bool kHKeys = false>
 __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __restrict__ tp_all) {
+  static_assert(!(kDecider && kHKeys), "the decider's scratch aliases the LDS keys");
   constexpr bool kDelays = kGeneral || kStress;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MemoShared& sh = *reinterpret_cast<MemoShared*>(smem);
@@ -756,9 +767,9 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   const int N = a.N, Cw = a.Cw;
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(MemoShared));
-  unsigned* s_keys = reinterpret_cast<unsigned*>(s_nodes + N);
-  double* s_fold = reinterpret_cast<double*>(reinterpret_cast<char*>(s_keys) +
-                                             ((std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15));
+  unsigned* s_keys = kHKeys ? a.hkeys + ((size_t)gi * a.K + w) * Cw * N : reinterpret_cast<unsigned*>(s_nodes + N);
+  double* s_fold = reinterpret_cast<double*>(
+      reinterpret_cast<char*>(s_nodes + N) + (kHKeys ? 0 : (std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15));
   int* s_last = reinterpret_cast<int*>(reinterpret_cast<char*>(s_fold) +
                                        std::max((size_t)a.nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15));
   const PodDev* cls_pod = a.cls_pod + (size_t)gi * a.Cmax;
@@ -786,6 +797,9 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   for (int i = tid; i < rp.nt * 2; i += kMBlock)
     reinterpret_cast<uint4*>(sh.tp)[i] = reinterpret_cast<const uint4*>(tp)[i];
   if (tid == 0) { sh.dirty = -1; sh.stop = 0; sh.nitems = 0; sh.t2a = 0u; sh.t2b = 0u; sh.pay = 0u; sh.crit_done = 0; }
+  // the residency gate: this workgroup has started (a vector store to host memory, system scope)
+  if (a.started != nullptr && tid == 0)
+    __hip_atomic_store(a.started + blockIdx.x, a.gate_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (int i = tid; i < kMaxDeadWords; i += kMBlock) sh.dead[i] = 0u;
   // phase timer (wall clock, 100 MHz): only with a profile buffer, thread 0 of each workgroup
   const bool prof = kGeneral && a.prof != nullptr;
@@ -1250,7 +1264,7 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
           // (results carry name ranks and the affinity tags are applied by k_memo_finish: nothing
           // here waits on global memory)
           if (del && is_w0) gput(rp.res + step, ResultDev{rk, mask, 0, 0, ST_DELETED});
-          if (kGeneral && rp.snap && (del ? is_w0 : own)) {  // cluster report: the state this event left
+          if ((kGeneral || kReport) && rp.snap && (del ? is_w0 : own)) {  // cluster report: the state this event left
             gput_node(rp.snap + step, n);
             gput(rp.prev + step, s_last[rk]);
           }
@@ -1316,8 +1330,8 @@ __global__ void k_memo_finish(ReplicaDev* reps, const int* rep_list, int N) {
 }
 
 // LDS bytes of k_memo's dynamic region (must match the carving in the kernel).
-inline size_t memo_lds(int N, int Cw, int nfw) {
-  const size_t keys = (std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15;
+inline size_t memo_lds(int N, int Cw, int nfw, bool hkeys = false) {
+  const size_t keys = hkeys ? 0 : (std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15;
   const size_t fold = std::max((size_t)nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15);
   return sizeof(MemoShared) + (size_t)N * sizeof(NodeRec) + keys + fold + (size_t)N * 4;
 }

@@ -148,6 +148,7 @@ SIGNATURES = {
     "ksim_engine_set_policy": (C.c_int, [_VP, C.c_int, C.c_int, C.c_int, C.c_uint64]),
     "ksim_engine_set_power_model": (C.c_int, [_VP, C.c_int, _P(PowerModel)]),
     "ksim_engine_set_weights": (C.c_int, [_VP, C.c_int, C.c_int32, C.c_int32]),
+    "ksim_engine_set_replica_wgs": (C.c_int, [_VP, C.c_int, C.c_int]),
     "ksim_trace_power_model": (C.c_int, [_VP, _P(PowerModel)]),
     "ksim_engine_filter_score": (C.c_int, [_VP, C.c_int, _P(Pod), C.c_int32, _P(C.c_uint8), _P(C.c_int32),
                                            _P(C.c_int32)]),
@@ -495,6 +496,11 @@ class Engine:
 
     def set_plugin_cfg(self, r, dim_ext="merge", norm="max"):
         check(lib().ksim_engine_set_plugin_cfg(self.h, r, DIM_EXT[dim_ext], NORM[norm]), "set_plugin_cfg")
+
+    def set_replica_wgs(self, r, wgs):
+        """Workgroups for replica r (0: the engine's choice); an FGD replica hinted wide runs k_memo at that width
+        beside one-workgroup replicas (ksim_engine_set_replica_wgs)."""
+        check(lib().ksim_engine_set_replica_wgs(self.h, r, wgs), "set_replica_wgs")
 
     def set_weights(self, r, w_pwr, w_fgd):
         check(lib().ksim_engine_set_weights(self.h, r, w_pwr, w_fgd), "set_weights")

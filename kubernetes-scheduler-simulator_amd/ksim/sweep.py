@@ -11,6 +11,8 @@ one ksim.Engine: one k_replay launch per policy replays them all, the device com
 event's cluster report, and the host turns the reports into the allocation / fragmentation
 curves of experiments/analysis/merge_*_discrete.py (ksim.analysis).
 """
+import json
+import os
 import time
 
 import numpy as np
@@ -39,23 +41,50 @@ def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
     return [(t, p, s, tune) for t in traces for p in policies for s in seeds]
 
 
-# Cost model of one experiment on one GPU (r04/r05 measurements, profiles/r04/hmemo/c4_fgd_traces.jsonl):
-# FGD replays on k_hmemo at ~4.1 us per event up to ~64 typical pods, growing with the typical table beyond
-# (gpuspec33, 127 typical pods: 9.1 us); the cheap policies on k_scan1 at ~3.3 us per event.
+# Cost model of one experiment on one GPU: its events x the per-event latency of its replay chain, read from the
+# measured table (profiles/r06/c4_costs.jsonl, scripts/r06/c4_costs.py: every trace and policy alone on the GPU, the
+# seed with the most events, the cluster report on) -- FGD on k_hmemo at one workgroup ("one") and on k_memo at
+# WIDE_K workgroups ("wide"), the cheap policies on k_scan1.  Without the table: the r05 constants (FGD ~4.1 us per
+# event up to ~64 typical pods, growing with the typical table beyond; the cheap policies ~3.3 us).
+COST_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                          "profiles", "r06", "c4_costs.jsonl")
 FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
+WIDE_K = 25   # workgroups of a widened FGD replica (k_memo)
+_COSTS = None
 
 
-def experiment_cost_us(policy_dir, events, n_typical):
-    """Estimated replay time of one experiment (us): its events x the policy's per-event latency."""
+def load_costs(path=COST_TABLE):
+    """{(trace, policy, form): us per event} from the measured table ({} when absent)."""
+    global _COSTS
+    if _COSTS is None or path != COST_TABLE:
+        out = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                for ln in f:
+                    d = json.loads(ln)
+                    if d.get("us_per_event"):
+                        out[(d["trace"], d["policy"], d["form"])] = d["us_per_event"]
+        if path != COST_TABLE:
+            return out
+        _COSTS = out
+    return _COSTS
+
+
+def experiment_cost_us(policy_dir, events, n_typical, trace=None, form="one"):
+    """Estimated replay time of one experiment (us): its events x the measured per-event latency of its trace and
+    policy in that form (load_costs), or the r05 constants."""
+    us = load_costs().get((trace, policy_dir, form))
+    if us is not None:
+        return events * us
     if policy_dir == "06-FGD":
-        return events * (FGD_US + FGD_US_PER_TYP * max(0, n_typical - 64))
+        return events * (FGD_US + FGD_US_PER_TYP * max(0, n_typical - 64)) * (0.8 if form == "wide" else 1.0)
     return events * CHEAP_US
 
 
 _EVENTS = {}
 
 
-def plan_costs(items):
+def plan_costs(items, form="one"):
     """Estimated cost of each (trace, policy, seed, tune) experiment: the replay's event count (the
     reference's own stream, ksim.Trace.replay) x experiment_cost_us's latency."""
     traces = {}
@@ -67,7 +96,29 @@ def plan_costs(items):
         k = (t, s, tune)
         if k not in _EVENTS:
             _EVENTS[k] = tr.replay(seed=s, tune_ratio=tune, shuffle=True).n
-        out.append(experiment_cost_us(p, _EVENTS[k], tr.typical()[1]))
+        out.append(experiment_cost_us(p, _EVENTS[k], tr.typical()[1], t, form))
+    return out
+
+
+def plan_widths(items, costs, wide_costs, cus=256, wide_k=WIDE_K, per_cu_cheap=6):
+    """Critical-path-aware widths for one share's experiments (run concurrently on one GPU): the share's time is its
+    longest replay chain, so the FGD replays whose one-workgroup chain is longer than everything else the share
+    holds take k_memo at wide_k workgroups, longest first, while the CUs last -- each widened
+    replica holds wide_k CUs, every other FGD replica one, the cheap replicas per_cu_cheap to a CU.
+    -> {item index: wide_k} for the widened ones."""
+    fgd = sorted((i for i, it in enumerate(items) if it[1] == "06-FGD"), key=lambda i: (-costs[i], i))
+    cheap = [i for i, it in enumerate(items) if it[1] != "06-FGD"]
+    free = cus - len(fgd) - -(-len(cheap) // per_cu_cheap)
+    floor = max((costs[i] for i in cheap), default=0.0)  # the longest chain widening cannot shorten
+    out = {}
+    for n, i in enumerate(fgd):
+        # the share's time if this one stays narrow: its own chain, or the longest widened chain so far
+        if costs[i] <= max([floor] + [wide_costs[j] for j in out]) or wide_costs[i] >= costs[i]:
+            break
+        if free < wide_k - 1:
+            break
+        out[i] = wide_k
+        free -= wide_k - 1
     return out
 
 
@@ -93,9 +144,12 @@ class Sweep:
     policies (k_memo / k_replay) and, when the plan has PWR experiments, one for those (k_step +
     k_step_pwr per pod)."""
 
-    def __init__(self, experiments, device=0, report=True, wgs=0, fgd_batch=0, random_stream="hash"):
+    def __init__(self, experiments, device=0, report=True, wgs=0, fgd_batch=0, random_stream="hash", wide=None):
         """random_stream: "hash" (the Random contract) or "go" (the reference's draw
-        structure on Go's math/rand stream, k_random_go: ksim_engine_set_go_stream)."""
+        structure on Go's math/rand stream, k_random_go: ksim_engine_set_go_stream).  wide: {experiment index:
+        workgroups} -- FGD experiments to replay on k_memo at that width beside the one-workgroup ones
+        (plan_widths; ksim_engine_set_replica_wgs)."""
+        wide = wide or {}
         assert random_stream in ("hash", "go")
         self.exps = list(experiments)
         traces = {}
@@ -129,6 +183,8 @@ class Sweep:
                 arr, n = typ[t]
                 eng.set_typical(r, arr, n)
                 eng.set_policy(r, ALL_POLICY_DIRS[p], seed=s)
+                if i in wide:
+                    eng.set_replica_wgs(r, wide[i])
                 # every experiment: PWR's energy model, and the per-event [Power] report the reference
                 # logs after every event whatever the policy (simulator.go:427)
                 eng.set_power_model(r, traces[t].power_model())
