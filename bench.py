@@ -76,7 +76,7 @@ def profile_rooflines(args, kernels):
         pmc = json.load(f)
     dom = pmc.get("dominant") or {}
     fam = dom.get("kernel", "")  # scripts/pmc_summary.py kernel_of: k_memo, k_hmemo, k_scan1_mix, k_replay<1>, ...
-    names = {"k_hmemo" if k == "k_hmemo_wide" else k for k in kernels}
+    names = {{"k_hmemo_wide": "k_hmemo", "k_memo_hkeys": "k_memo"}.get(k, k) for k in kernels}
     if fam.split("<")[0] not in names:
         return None, None, None
     src = os.path.relpath(pf, ROOT)

@@ -359,7 +359,8 @@ int  ksim_engine_last_run_steps(ksim_engine* e, int64_t* steps);
  * on concurrently (0: back to back on the engine stream).  Introspection for the tests and the bench. */
 int  ksim_engine_last_run_launches(ksim_engine* e, int* launches, int* side_streams);
 /* The replay kernels the last run launched, '+'-joined in launch order ("k_hmemo+k_scan1_mix", "k_memo",
- * "k_step+k_step_pwr", ...), NUL-terminated into out[cap]: KSIM_ERANGE when cap is too small. */
+ * "k_memo_hkeys" (k_memo with its keys in HBM), "k_step+k_step_pwr", ...), NUL-terminated into out[cap]:
+ * KSIM_ERANGE when cap is too small. */
 int  ksim_engine_last_run_kernels(ksim_engine* e, char* out, int cap);
 /* The residency gate of the last run (a paper-sweep run: the concurrent groups launch once every FGD workgroup
  * has started): *gate 0 = no gate, 1 = opened, -1 = given up at its 2 s bound (the groups then

@@ -3945,6 +3945,16 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   if (const char* q = std::getenv("KSIM_SIDE_STREAMS")) nq = std::atoi(q) > 0 ? std::atoi(q) : nq;
   nq = std::max(1, std::min(nq, (int)ksim_engine::kSide));
   unsigned used = 0u;
+  // Stream of concurrent group g: a side stream each (the first one alone on its own, the rest round robin), except
+  // that a split FGD run's wide k_memo group runs on the engine stream itself -- which otherwise only waits -- so the
+  // run needs one stream fewer: three groups on the engine stream and two side streams, within the hardware queues a
+  // process gets (with three side streams two groups shared a queue and ran one after the other: 64 -> 133 ms for a
+  // C4 share, profiles/r06/c4_wide/)
+  const int g_off = concurrent && e->split_fgd ? 1 : 0;
+  auto side_of = [&](int g) {
+    const int j = g - g_off;
+    return j < 0 ? -1 : (j == 0 || nq == 1) ? 0 : 1 + (j - 1) % (nq - 1);
+  };
   if (concurrent) {
     if (!e->ev_fork) KSIM_HIP(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
     KSIM_HIP(hipEventRecord(e->ev_fork, e->stream));
@@ -3957,8 +3967,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   for (const auto& gp : groups) {
     const int Rg = gp.second;
     hipStream_t gs = e->stream;
-    if (concurrent) {
-      const int i = (gidx == 0 || nq == 1) ? 0 : 1 + (gidx - 1) % (nq - 1);
+    if (concurrent && side_of(gidx) >= 0) {
+      const int i = side_of(gidx);
       if (!e->side[i]) {
         KSIM_HIP(hipStreamCreateWithFlags(&e->side[i], hipStreamNonBlocking));
         KSIM_HIP(hipEventCreateWithFlags(&e->side_ev[i], hipEventDisableTiming));
@@ -4020,7 +4030,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         const int rc = launch_memo(e, pl, Rg, first, max_ev, gs, flags, epoch);
         if (rc) return rc;
         if (gate) gate_wait(e, Rg * pl.K, epoch, "FGD k_memo");
-        note_kernel(e, "k_memo");
+        note_kernel(e, pl.hkeys ? "k_memo_hkeys" : "k_memo");
         e->last_K = pl.K;
         e->last_groups = (int)groups.size();
         e->last_memo += Rg;
@@ -4175,13 +4185,14 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     for (size_t g = 0; g < groups.size(); ++g) {
       const int Rg = groups[g].second;
-      const int i = (g == 0 || nq == 1) ? 0 : 1 + ((int)g - 1) % (nq - 1);
+      const int i = side_of((int)g);
+      hipStream_t rs = i < 0 ? e->stream : e->side[i];
       int mev = 0;
       for (int j = f; j < f + Rg; ++j) mev = std::max(mev, e->n_events[order[j]]);
-      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g], e->side[i]));
-      const int rc = run_report(e, mev, e->side[i], e->d_replist + f, Rg);
+      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g], rs));
+      const int rc = run_report(e, mev, rs, e->d_replist + f, Rg);
       if (rc) return rc;
-      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g + 1], e->side[i]));
+      KSIM_HIP(hipEventRecord(e->grp_rev[2 * g + 1], rs));
       f += Rg;
     }
     e->grp_rev_used = (int)groups.size();

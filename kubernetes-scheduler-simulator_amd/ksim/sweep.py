@@ -49,7 +49,8 @@ def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
 COST_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                           "profiles", "r06", "c4_costs.jsonl")
 FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
-WIDE_K = 25   # workgroups of a widened FGD replica (k_memo)
+WIDE_K = 16   # workgroups of a widened FGD replica (k_memo; share 0/8: 50.9 ms at 16 x 13 replicas, 52.0 at 25 x 8)
+PER_CU_CHEAP = 3  # cheap replicas a CU holds without their chains slowing much (6 fit; at 6 a share took 89 ms)
 _COSTS = None
 
 
@@ -100,11 +101,12 @@ def plan_costs(items, form="one"):
     return out
 
 
-def plan_widths(items, costs, wide_costs, cus=256, wide_k=WIDE_K, per_cu_cheap=6):
+def plan_widths(items, costs, wide_costs, cus=256, wide_k=WIDE_K, per_cu_cheap=PER_CU_CHEAP):
     """Critical-path-aware widths for one share's experiments (run concurrently on one GPU): the share's time is its
     longest replay chain, so the FGD replays whose one-workgroup chain is longer than everything else the share
     holds take k_memo at wide_k workgroups, longest first, while the CUs last -- each widened
-    replica holds wide_k CUs, every other FGD replica one, the cheap replicas per_cu_cheap to a CU.
+    replica holds wide_k CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap
+    replicas per_cu_cheap to a CU (profiles/r06/c4_wide/: packed tighter, their chains and the others' slow down).
     -> {item index: wide_k} for the widened ones."""
     fgd = sorted((i for i, it in enumerate(items) if it[1] == "06-FGD"), key=lambda i: (-costs[i], i))
     cheap = [i for i, it in enumerate(items) if it[1] != "06-FGD"]

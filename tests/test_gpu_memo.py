@@ -236,6 +236,42 @@ def test_hmemo_cluster_report(default_trace, wgs):
     assert reps[HMEMO] == reps[SCAN]
 
 
+@pytest.mark.parametrize("form", ["lean", "report", "deletes"])
+def test_memo_keys_in_hbm(form):
+    # r06: gpuspec33 (457 classes, score groups of up to 60 classes) at 25 workgroups per replica: its keys do not
+    # fit in LDS beside the cluster, so k_memo keeps them in HBM and splits the large groups over workgroups --
+    # bit-exact against the oracle in the lean form, the lean form with the report's stores (against k_hmemo's
+    # reports) and the general one (a create / delete stream)
+    t = ksim.Trace.openb("gpuspec33")
+    rp = t.replay(seed=43)
+    arr, n = t.typical()
+    if form == "deletes":
+        evs, oev = helpers.delete_stream(t, rp, 1800, 0.3, seed=2)
+        n_ev = len(evs)
+        want, want_state, _ = O.run_events(helpers.oracle_nodes(t, rp), helpers.oracle_typical(t), oev, policy=O.POL_FGD,
+                                           gpu_sel=O.SEL_FGD, threads=16)
+    else:
+        evs, n_ev = rp.events, 2500
+        want, want_state, _ = oracle_run(t, rp, None, n_ev, O.POL_FGD, O.SEL_FGD)
+    outs = {}
+    for mode, wgs in ((MEMO, 25), (HMEMO, 1)):
+        eng = ksim.Engine(t.num_nodes, 1, run_mode=mode, wgs_per_replica=wgs)
+        eng.set_nodes(0, rp.nodes)
+        eng.set_typical(0, arr, n)
+        eng.set_policy(0, "FGD")
+        if form == "report":
+            eng.set_report(True)
+        eng.load_events(0, evs, n_ev)
+        eng.run()
+        assert eng.last_run_kernels() == (["k_memo_hkeys"] if mode == MEMO else ["k_hmemo"])
+        assert eng.last_run_wgs() == wgs
+        outs[mode] = (eng.results(0), eng.nodes(0), eng.reports(0) if form == "report" else None)
+        eng.close()
+    assert_same(outs[MEMO][0], want, outs[MEMO][1], want_state, None)
+    if form == "report":
+        assert outs[MEMO][2] == outs[HMEMO][2]
+
+
 def test_hmemo_per_model_tables_that_do_not_fit():
     # r05 advisor: a typed replica whose per-model tables exceed their 12-bit offsets (25 GPU models x 200 GPU typical
     # pods accepting every model = 5 000 entries) runs k_hmemo on the whole table, bit-exact, instead of refusing it

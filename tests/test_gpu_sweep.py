@@ -172,3 +172,28 @@ def test_default_sweep_fgd_group_is_memoised():
     path = sw.eng.last_run_path()
     sw.close()
     assert path == "memo+k_replay", path
+
+
+def test_share_with_widened_fgd_rows_identical():
+    # round-5 verdict item 1: an N-GPU share's longest FGD replays on k_memo at WIDE_K workgroups (the gpuspec traces'
+    # keys in HBM, the untyped ones' in LDS) beside the one-workgroup FGD replicas (k_hmemo) and the cheap policies'
+    # k_scan1_mix, all concurrently: three launches, each gated before the next, every row still identical to
+    # expected_results
+    items = SW.plan(traces=["openb_pod_list_gpuspec33", "openb_pod_list_gpushare100", "openb_pod_list_default"],
+                    seeds=[42, 43, 48])
+    wide = {i: SW.WIDE_K for i, e in enumerate(items)
+            if e[1] == "06-FGD" and (e[0], e[2]) in {("openb_pod_list_gpuspec33", 42), ("openb_pod_list_gpushare100", 48)}}
+    assert len(wide) == 2
+    sw = SW.Sweep(items, wgs=1, wide=wide)
+    sw.run()
+    kernels, gate = sw.eng.last_run_kernels(), sw.eng.last_run_gate()
+    launches, streams = sw.eng.last_run_launches()
+    curves = sw.curves()
+    sw.close()
+    assert kernels == ["k_memo_hkeys", "k_hmemo", "k_scan1_mix"], kernels  # gpuspec33's classes: keys in HBM
+    assert launches == 3 and streams == 2 and gate == (1, 0)  # k_memo on the engine stream, two side streams
+    for kind, csv in (("alloc", ALLO), ("frag", FRAG)):
+        mm = SW.row_mismatches({k: v for k, v in curves.items() if k[1] != "01-Random"}, kind, SW.expected_rows(csv))
+        assert len(mm) == 45 and not any(mm.values()), kind
+    ratio_rows = ratio_deviations({k: v for k, v in curves.items() if k[1] != "01-Random"})
+    assert len(ratio_rows) == 45 and max(ratio_rows.values()) <= RATIO_TOL
