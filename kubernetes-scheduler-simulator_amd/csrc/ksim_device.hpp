@@ -154,7 +154,7 @@ struct ReplicaDev {
   int2* pws;             // [N]
   int32_t w_pwr, w_fgd;
   int32_t has_pw;        // an energy model was given: the cluster report adds the [Power] terms
-  int32_t pad_pw;
+  int32_t n_local;       // the replica's node count (a node-sharded k_replay group: each shard's own)
   const int32_t* mcap;   // [N] allocatable memory, MiB (the Unreserve guard)
 };
 

@@ -715,11 +715,15 @@ void k_replay(ksim_replay::ReplayArgs a,
   ReplayShared& sh = *reinterpret_cast<ReplayShared*>(smem);
   const int r = a.rep_list[(int)blockIdx.x / a.K];
   const int w = (int)blockIdx.x % a.K;
+  // the exchange: Kx columns (every workgroup of the replica; a node-sharded group, a.xK: every workgroup of
+  // every shard), this workgroup's column wx
+  const int Kx = a.xK > 0 ? a.xK : a.K;
+  const int wx = (int)blockIdx.x % Kx;
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const ReplicaDev rp = a.reps[r];
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int n_lo = w * a.S;
-  const int ns = max(0, min(a.S, a.N - n_lo));
+  const int ns = max(0, min(a.S, (a.group ? rp.n_local : a.N) - n_lo));
   constexpr bool kTags = kPol == POL_CLUSTERING;  // GpuClustering reads the tag counts per pod step
   const RLayout L = replay_layout(a.S, kPol, kGeneral, kPF ? a.pm_c : 0);
   ReplayFgd& fs = *reinterpret_cast<ReplayFgd*>(smem + L.fgd);  // FGD launches only
@@ -757,7 +761,7 @@ void k_replay(ksim_replay::ReplayArgs a,
   // (null when no replica of the launch has a delete event: nothing ever reads it)
   int2* hist = (kGeneral && a.hist) ? a.hist + (size_t)(r * a.K + w) * a.hist_stride : nullptr;
   NodeRec* const snap = kGeneral ? rp.snap : nullptr;
-  unsigned long long* gr = a.gran + (size_t)(blockIdx.x / a.K) * 2 * a.K * kGranW;
+  unsigned long long* gr = a.gran + (size_t)(blockIdx.x / Kx) * 2 * Kx * kGranW;
 
   for (int i = tid; i < ns; i += kRBlock) store_node(&s_nodes[i], load_node(rp.nodes + n_lo + i));
   if (kTags)
@@ -814,11 +818,11 @@ void k_replay(ksim_replay::ReplayArgs a,
   // Wave 0, lane k: the granules of workgroups k, k+64, .. (< K) of the pending exchange
   // (relaxed agent-scope loads).
   auto poll_once = [&](GranV<kS>& g) {
-    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * Kx * kGranW;
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
       const int k = lane + 64 * j;
-      if (k < a.K) {
+      if (k < Kx) {
         g.g0[j] = gload(slot + (size_t)k * kGranW + 0);
         g.g1[j] = gload(slot + (size_t)k * kGranW + 1);
         g.g2[j] = gload(slot + (size_t)k * kGranW + 2);
@@ -835,13 +839,13 @@ void k_replay(ksim_replay::ReplayArgs a,
   // (x: an earlier poll when `have`, issued before the evaluation's last barrier so its latency overlaps the wait)
   auto pf_collect = [&](unsigned long long (&x)[kS][7], bool have, int* gc, int* ge, int* gl, int* gh,
                         unsigned long long* W0, unsigned long long* W1) -> bool {
-    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    const unsigned long long* slot = gr + (size_t)(p_seq & 1) * Kx * kGranW;
     const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
     auto load = [&]() {
 #pragma unroll
       for (int j = 0; j < kS; ++j) {
         const int k = lane + 64 * j;
-        if (k < a.K) {
+        if (k < Kx) {
 #pragma unroll
           for (int q = 0; q < 7; ++q) x[j][q] = gload(slot + (size_t)k * kGranW + q);
         }
@@ -854,7 +858,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         bool t = true;
 #pragma unroll
         for (int q = 0; q < 7; ++q) t = t && (x[j][q] & ~0xffffffffull) == tag;
-        r = r && (lane + 64 * j >= a.K || t);
+        r = r && (lane + 64 * j >= Kx || t);
       }
       return r;
     };
@@ -871,7 +875,7 @@ void k_replay(ksim_replay::ReplayArgs a,
     unsigned long long b0 = 0ull, b1 = 0ull;
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
-      if (lane + 64 * j < a.K) {
+      if (lane + 64 * j < Kx) {
         const unsigned long long k0 = ((x[j][1] & 0xffffffffull) << 32) | (x[j][0] & 0xffffffffull);
         const unsigned long long k1 = ((x[j][3] & 0xffffffffull) << 32) | (x[j][2] & 0xffffffffull);
         const unsigned st = (unsigned)x[j][6];
@@ -895,18 +899,18 @@ void k_replay(ksim_replay::ReplayArgs a,
     return ok;
   };
   auto pf_miss_round = [&](unsigned long long mine, unsigned long long* W) -> bool {
-    unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    unsigned long long* slot = gr + (size_t)(p_seq & 1) * Kx * kGranW;
     const unsigned long long tag = (unsigned long long)(unsigned)(p_seq + 1) << 32;
     if (lane == 0) {
-      gstore(slot + (size_t)w * kGranW + 7, tag | (mine & 0xffffffffull));
-      gstore(slot + (size_t)w * kGranW + 8, tag | (mine >> 32));
+      gstore(slot + (size_t)wx * kGranW + 7, tag | (mine & 0xffffffffull));
+      gstore(slot + (size_t)wx * kGranW + 8, tag | (mine >> 32));
     }
     unsigned long long x0[kS], x1[kS];
     auto load = [&]() {
 #pragma unroll
       for (int j = 0; j < kS; ++j) {
         const int k = lane + 64 * j;
-        if (k < a.K) {
+        if (k < Kx) {
           x0[j] = gload(slot + (size_t)k * kGranW + 7);
           x1[j] = gload(slot + (size_t)k * kGranW + 8);
         }
@@ -916,7 +920,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       bool r = true;
 #pragma unroll
       for (int j = 0; j < kS; ++j)
-        r = r && (lane + 64 * j >= a.K || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
+        r = r && (lane + 64 * j >= Kx || ((x0[j] & ~0xffffffffull) == tag && (x1[j] & ~0xffffffffull) == tag));
       return r;
     };
     load();
@@ -930,7 +934,7 @@ void k_replay(ksim_replay::ReplayArgs a,
     unsigned long long b = 0ull;
 #pragma unroll
     for (int j = 0; j < kS; ++j)
-      if (lane + 64 * j < a.K) {
+      if (lane + 64 * j < Kx) {
         const unsigned long long k = ((x1[j] & 0xffffffffull) << 32) | (x0[j] & 0xffffffffull);
         b = k > b ? k : b;
       }
@@ -941,7 +945,7 @@ void k_replay(ksim_replay::ReplayArgs a,
   // this workgroup's own totals (K == 1); g holds an earlier poll.  Returns the winning key.
   auto exchange = [&](GranV<kS>& g, int* gc, int* ge, int* gl, int* gh, bool* ok) -> unsigned long long {
     *ok = true;
-    if (a.K == 1) {
+    if (Kx == 1) {
       *gc = p_st0; *ge = p_st1; *gl = p_st2; *gh = p_st3;
       return p_key;
     }
@@ -950,7 +954,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       bool r = true;
 #pragma unroll
       for (int j = 0; j < kS; ++j)
-        r = r && (lane + 64 * j >= a.K || ((g.g0[j] & ~0xffffffffull) == tag && (g.g1[j] & ~0xffffffffull) == tag &&
+        r = r && (lane + 64 * j >= Kx || ((g.g0[j] & ~0xffffffffull) == tag && (g.g1[j] & ~0xffffffffull) == tag &&
                                           (g.g2[j] & ~0xffffffffull) == tag));
       return r;
     };
@@ -966,7 +970,7 @@ void k_replay(ksim_replay::ReplayArgs a,
     unsigned long long best = 0ull;
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
-      const bool in = lane + 64 * j < a.K;
+      const bool in = lane + 64 * j < Kx;
       const unsigned st = in ? (unsigned)(g.g2[j] & 0xffffffffull) : 0u;
       const int cj = (int)(st & 0x1ffff);
       c += cj;
@@ -1027,7 +1031,7 @@ void k_replay(ksim_replay::ReplayArgs a,
               rp.prev[p_step] = s_last[p_b];
               s_last[p_b] = p_step;
             }
-            out.node = n_lo + p_b;
+            out.node = a.group ? (int)key_rank(W) : n_lo + p_b;
             out.gpu_mask = p_mask;
             hrec = make_int2(n_lo + p_b, p_mask + 1);
           }
@@ -1036,7 +1040,16 @@ void k_replay(ksim_replay::ReplayArgs a,
     }
     if (lane == 0) {
       if (hist) hist[p_step] = hrec;
-      if (writer) rp.res[p_step] = out;
+      if (writer) {
+        rp.res[p_step] = out;
+      } else if (a.group && w == 0) {  // a shard that does not own the winner names it (the owner's record rules)
+        // (the owner's shard -- its ranks are [node_off, node_off + n_local) -- has its owning workgroup write)
+        const uint32_t rk = key_rank(W);
+        if (rk - (uint32_t)rp.node_off >= (uint32_t)rp.n_local) {
+          out.node = (int)rk;
+          rp.res[p_step] = out;
+        }
+      }
     }
   };
 
@@ -1073,7 +1086,7 @@ void k_replay(ksim_replay::ReplayArgs a,
     const unsigned long long p_key1 = sh.pf_key1;
     const int4 p_g = sh.pf_g;
     unsigned long long W0 = p_key, W1 = p_key1;
-    if (a.K > 1 && !pf_collect(x, have, &gc, &ge, &gl, &gh, &W0, &W1)) return false;
+    if (Kx > 1 && !pf_collect(x, have, &gc, &ge, &gl, &gh, &W0, &W1)) return false;
     const bool m0 = gc <= 1 || (gl == p_g.x && gh == p_g.y);  // at most one feasible node: no normalisation
     const bool m1 = !m0 && gl == p_g.z && gh == p_g.w;
     unsigned long long W = m0 ? W0 : W1, mine = m0 ? p_key : p_key1;
@@ -1081,7 +1094,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       if (prof && lane == 0) sh.prof[9] += 1ull;  // KSIM_PROFILE: misses (low half), re-evaluations (high)
       mine = pf_rekey(gl, gh);
       W = mine;
-      if (a.K > 1 && !pf_miss_round(mine, &W)) return false;
+      if (Kx > 1 && !pf_miss_round(mine, &W)) return false;
     }
     if (gc > 1 && lane == 0 && a.pf_guess) {  // the class's most recent ranges (every workgroup updates alike)
       int4& t = s_gtab[p_cls & (kPfGuess - 1)];
@@ -1164,7 +1177,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         ok = pf_resolve(x, false, false, &redo);
       } else {
         GranV<kS> g{};
-        if (a.K > 1) poll_once(g);
+        if (Kx > 1) poll_once(g);
         int gc, ge, gl, gh;
         const unsigned long long W = exchange(g, &gc, &ge, &gl, &gh, &ok);
         if (ok) commit(W, gc, ge, gl, gh);
@@ -1334,7 +1347,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         }
         __syncthreads();
         mark(2);
-        if (!kPF && pend && a.K > 1 && wv == 0 && c0 == 0) poll_once(pg);
+        if (!kPF && pend && Kx > 1 && wv == 0 && c0 == 0) poll_once(pg);
         if (tid == 0) sh.nitems = 0;  // every thread has read tot; the next writer is past a barrier
         // fgd_score.go:100-141: every candidate lane scores itself; the node keeps the max,
         // ties to the lowest GPU index (fgd_score.go:128 keeps the first max)
@@ -1388,7 +1401,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       }
     } else if constexpr (kPwr) {
       // PWR: eight lanes per node (lane g <-> GPU g), the raw score biased into the key field
-      if (pend && a.K > 1 && wv == 0) poll_once(pg);
+      if (pend && Kx > 1 && wv == 0) poll_once(pg);
       for (int c0 = 0; c0 < nsv; c0 += kFChunk) {
         const int cn = min(kFChunk, nsv - c0);
         const int i = c0 + (tid >> 3), g = tid & 7;
@@ -1419,7 +1432,7 @@ void k_replay(ksim_replay::ReplayArgs a,
         route(valid && g == 0, i, feas, perr, (int)raw, k);
       }
     } else {
-      if (pend && a.K > 1 && wv == 0) poll_once(pg);
+      if (pend && Kx > 1 && wv == 0) poll_once(pg);
       for (int c0 = 0; c0 < nsv; c0 += kChunk) {
         const int cn = min(kChunk, nsv - c0);
         const int i = c0 + tid;
@@ -1439,11 +1452,11 @@ void k_replay(ksim_replay::ReplayArgs a,
         route(tid < cn, i, feas, e1, raw, k);
       }
     }
-    if (kPF && pend && a.K > 1 && wv == 0) {  // the pending round's granules: loads in flight over the barrier
-      const unsigned long long* slot = gr + (size_t)(p_seq & 1) * a.K * kGranW;
+    if (kPF && pend && Kx > 1 && wv == 0) {  // the pending round's granules: loads in flight over the barrier
+      const unsigned long long* slot = gr + (size_t)(p_seq & 1) * Kx * kGranW;
 #pragma unroll
       for (int j = 0; j < kS; ++j)
-        if (lane + 64 * j < a.K) {
+        if (lane + 64 * j < Kx) {
 #pragma unroll
           for (int q = 0; q < 7; ++q) px[j][q] = gload(slot + (size_t)(lane + 64 * j) * kGranW + q);
         }
@@ -1456,7 +1469,7 @@ void k_replay(ksim_replay::ReplayArgs a,
       if (pend) {
         if (wv == 0) {
           bool redo = false;
-          const bool ok = pf_resolve(px, a.K > 1, true, &redo);
+          const bool ok = pf_resolve(px, Kx > 1, true, &redo);
           if (lane == 0) {
             sh.pf_redo = redo ? 1 : 0;
             sh.pend_valid = 0;
@@ -1511,8 +1524,8 @@ void k_replay(ksim_replay::ReplayArgs a,
         const unsigned long long mk = sh.agg_key, mk1 = sh.agg_key1;
         const int c = sh.agg_cnt, e = sh.agg_err, l = sh.agg_lo, h = sh.agg_hi;
         if (lane == 0) {
-          if (a.K > 1) {
-            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW + (size_t)w * kGranW;
+          if (Kx > 1) {
+            unsigned long long* slot = gr + (size_t)(seq & 1) * Kx * kGranW + (size_t)wx * kGranW;
             const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
             gstore(slot + 0, tag | (mk & 0xffffffffull));
             gstore(slot + 1, tag | (mk >> 32));
@@ -1590,14 +1603,14 @@ void k_replay(ksim_replay::ReplayArgs a,
       if (ok) {
         if (lane == 0) {
           // publish this step first: granules {tag, key lo32}, {tag, key hi32}, {tag, err|hi|lo|cnt}
-          if (a.K > 1) {
-            unsigned long long* slot = gr + (size_t)(seq & 1) * a.K * kGranW;
+          if (Kx > 1) {
+            unsigned long long* slot = gr + (size_t)(seq & 1) * Kx * kGranW;
             const unsigned long long tag = (unsigned long long)(unsigned)(seq + 1) << 32;
             // bit 17 (BestFit): the slice's feasible raw scores are not all equal (its max is mk's score)
             const unsigned stat = ((unsigned)e << 31) | (l < h ? 1u << 17 : 0u) | ((unsigned)c & 0x1ffff);
-            gstore(slot + (size_t)w * kGranW + 0, tag | (mk & 0xffffffffull));
-            gstore(slot + (size_t)w * kGranW + 1, tag | (mk >> 32));
-            gstore(slot + (size_t)w * kGranW + 2, tag | stat);
+            gstore(slot + (size_t)wx * kGranW + 0, tag | (mk & 0xffffffffull));
+            gstore(slot + (size_t)wx * kGranW + 1, tag | (mk >> 32));
+            gstore(slot + (size_t)wx * kGranW + 2, tag | stat);
           }
           reset_agg();
         }
@@ -1902,6 +1915,9 @@ struct ksim_engine {
   int shard_world = 0;        // 0: not sharded
   unsigned long long* d_ggran = nullptr;  // a node-sharded group's exchange granules (engine 0 of the group)
   void* d_hgargs = nullptr;               // its per-shard k_hmemo arguments
+  unsigned long long* d_rgran = nullptr;  // a node-sharded k_replay group's exchange granules (engine 0)
+  ReplicaDev* d_rgreps = nullptr;         // its shards' replicas, and their list
+  int* d_rglist = nullptr;
   // one shard per process (ksim_shard_peer_handle / ksim_engine_set_shard_peers): this shard's exchange
   // buffer (uncached device memory, exported by IPC), the peers' buffers mapped here, the run epoch
   unsigned long long* d_pgran = nullptr;
@@ -3024,6 +3040,7 @@ int ksim_engine_create(const ksim_config* cfg, int n_nodes, int n_replicas, ksim
     rp.gpusel = SEL_FGD;
     rp.tp = e->d_tp + (size_t)r * kMaxTypical;
     rp.nodes = e->d_nodes + (size_t)r * n_nodes;
+    rp.n_local = n_nodes;
     rp.tags = e->d_tags + (size_t)r * e->tags_stride;
     rp.cap = e->d_cap + (size_t)r * n_nodes;
     rp.mcap = e->d_mcap + (size_t)r * n_nodes;
@@ -3064,7 +3081,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -4128,6 +4145,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
     }
     e->last_pf_memo = pm_c;
     ksim_replay::ReplayArgs ra;
+    ra.xK = 0;
+    ra.group = 0;
     ra.pm_c = pm_c;
     {
       const long v = test_knob("pf_memo_ver0", 0);
@@ -4547,6 +4566,103 @@ static bool hmemo_group_eligible(ksim_engine* const* engines, int world) {
   return true;
 }
 
+// The cheap policies' node-sharded group on k_replay slices (r06, round-5 verdict item 7): every shard's K slices in
+// ONE launch, one exchange of Kt = world x K columns per pod step (the keys carry global name ranks, so the max is
+// selectHost over the union, generic_scheduler.go:187-212; BestFit's NormalizeScore range rides in the same granules
+// as in the unsharded k_replay, plugin_utils.go:48-74).  Lean runs only: one replica per shard,
+// a create-only stream, no report, no profile.
+static bool replay_group_eligible(ksim_engine* const* engines, int world) {
+  const int pol = engines[0]->reps[0].policy;
+  if (pol < POL_BESTFIT || pol > POL_RANDOM || variant("shard_replay", 1) == 0) return false;
+  for (int k = 0; k < world; ++k) {
+    const ksim_engine* e = engines[k];
+    if (e->R != 1 || e->reps[0].policy != pol || e->report || e->run_mode == 1 || e->has_delete[0] || go_random(e, 0))
+      return false;
+  }
+  const char* pe = std::getenv("KSIM_PROFILE");
+  return !(pe && pe[0] != '0');
+}
+
+// KSIM_OK with *done = false: the group does not fit (the caller keeps the per-pod k_step path).
+static int run_replay_group(ksim_engine* const* engines, int world, int max_ev, bool* done) {
+  using namespace ksim_replay;
+  *done = false;
+  ksim_engine* e0 = engines[0];
+  int N = 1;  // slices cover the largest shard
+  for (int k = 0; k < world; ++k) N = std::max(N, engines[k]->N);
+  const int pol = e0->reps[0].policy;
+  // slices of about 384 nodes (choose_wgs), at most 256 columns in all
+  int K = std::max(1, std::min(256 / world, (N + 383) / 384));
+  K = std::min(K, std::max(1, e0->cus / world));
+  int S = (N + K - 1) / K;
+  while (replay_lds(S, pol, false) > 160 * 1024 && (K + 1) * world <= std::min(256, e0->cus)) {
+    ++K;
+    S = (N + K - 1) / K;
+  }
+  const int Kt = world * K;
+  if (Kt < 2 || replay_lds(S, pol, false) > 160 * 1024) return KSIM_OK;
+  const void* f = replay_kernel(pol, Kt, false);
+  const size_t lds = replay_lds(S, pol, false);
+  if (Kt > resident_cap(e0, f, lds)) return KSIM_OK;
+  hipStream_t st = e0->stream;
+  KSIM_HIP(hipSetDevice(e0->device));
+  int rc;
+  if (!e0->d_rgran) KSIM_HIP(hipMalloc(&e0->d_rgran, sizeof(unsigned long long) * 2 * 256 * kGranW));
+  if (!e0->d_rgreps) KSIM_HIP(hipMalloc(&e0->d_rgreps, sizeof(ReplicaDev) * 16));
+  if (!e0->d_rglist) {
+    KSIM_HIP(hipMalloc(&e0->d_rglist, sizeof(int) * 16));
+    std::vector<int> id(16);
+    std::iota(id.begin(), id.end(), 0);
+    KSIM_HIP(hipMemcpy(e0->d_rglist, id.data(), sizeof(int) * 16, hipMemcpyHostToDevice));
+  }
+  bool skip = true;
+  for (int k = 0; k < world; ++k) {
+    ksim_engine* e = engines[k];
+    KSIM_HIP(hipStreamSynchronize(e->stream));
+    KSIM_HIP(hipMemcpyAsync(e->d_nodes, e->d_nodes_init, sizeof(NodeRec) * (size_t)e->N, hipMemcpyDeviceToDevice, st));
+    KSIM_HIP(hipMemcpyAsync(e->d_tags, e->d_tags_init, sizeof(uint16_t) * e->tags_stride, hipMemcpyDeviceToDevice, st));
+    KSIM_HIP(hipMemsetAsync(e->d_res[0], 0xff, sizeof(ResultDev) * (size_t)std::max(e->n_events[0], 1), st));
+    KSIM_HIP(hipMemcpyAsync(e0->d_rgreps + k, e->d_reps, sizeof(ReplicaDev), hipMemcpyDeviceToDevice, st));
+    skip = skip && dead_skip(e, std::vector<int>{0});
+  }
+  ReplayArgs ra;
+  std::memset(&ra, 0, sizeof ra);
+  ra.reps = e0->d_rgreps;
+  ra.rep_list = e0->d_rglist;
+  ra.N = N;
+  ra.K = K;
+  ra.S = S;
+  ra.gran = e0->d_rgran;
+  ra.hist = nullptr;
+  ra.hist_stride = std::max(max_ev, 1);
+  ra.fail = e0->d_fail;
+  ra.prof = nullptr;
+  ra.skip = skip ? 1 : 0;
+  ra.pf_guess = 1;
+  ra.xK = Kt;
+  ra.group = 1;
+  KSIM_HIP(hipMemsetAsync(e0->d_rgran, 0, sizeof(unsigned long long) * 2 * (size_t)Kt * kGranW, st));
+  KSIM_HIP(hipMemsetAsync(e0->d_fail, 0, sizeof(int), st));
+  KSIM_HIP(hipEventRecord(e0->ev0, st));
+  const TypDev* tp = e0->d_tp;  // (the cheap policies read no typical table)
+  if ((rc = launch_persistent(f, Kt, kRBlock, lds, st, e0->coop, ra, tp))) return rc;
+  KSIM_HIP(hipEventRecord(e0->ev1, st));
+  KSIM_HIP(hipStreamSynchronize(st));
+  int fail = 0;
+  KSIM_HIP(hipMemcpy(&fail, e0->d_fail, sizeof(int), hipMemcpyDeviceToHost));
+  if (fail) return KSIM_ESTATE;
+  float ms = 0;
+  KSIM_HIP(hipEventElapsedTime(&ms, e0->ev0, e0->ev1));
+  for (int k = 0; k < world; ++k) {
+    engines[k]->last_ms = ms;
+    engines[k]->last_steps = max_ev;
+    engines[k]->last_K = K;
+    engines[k]->last_kernels = "k_replay_group";
+  }
+  *done = true;
+  return KSIM_OK;
+}
+
 // KSIM_OK with *done = false: the group does not fit k_hmemo (the caller keeps the per-pod k_step path).
 static int run_hmemo_group(ksim_engine* const* engines, int world, int max_ev, bool* done) {
   using namespace ksim_hmemo;
@@ -4653,6 +4769,11 @@ int ksim_shard_group_run(ksim_engine* const* engines, int world) {
     const int rc = run_hmemo_group(engines, world, max_ev, &done);
     if (!rc && done)
       for (int k = 0; k < world; ++k) engines[k]->last_kernels = "k_hmemo_group";
+    if (rc || done) return rc;
+  }
+  if (replay_group_eligible(engines, world)) {
+    bool done = false;
+    const int rc = run_replay_group(engines, world, max_ev, &done);
     if (rc || done) return rc;
   }
   for (int k = 0; k < world; ++k) engines[k]->last_kernels = "k_step";

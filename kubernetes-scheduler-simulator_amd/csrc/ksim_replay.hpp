@@ -66,6 +66,12 @@ struct ReplayArgs {
   int pm_c;                  // PWR+FGD: class stride of the per-(class, slot) memo in LDS, 0 = no memo
   unsigned pm_ver0;          // the slots' first version (KSIM_TEST pf_memo_ver0: tests start near the wrap)
   int pf_guess;              // PWR+FGD: learn each class's ranges (KSIM_TEST pf_guess=0: never -- every scored step misses)
+  // A node-sharded group in one launch (ksim_shard_group_run, lean cheap policies): rep_list / reps name one
+  // replica per shard, a.K slices each; xK = every shard's slices together, the exchange's columns (0: a.K, one
+  // replica's), and results carry global name ranks -- the owner of the winner reports, every other shard's
+  // first workgroup names the winner (ksim.shard.merge_results)
+  int xK;
+  int group;
 };
 constexpr int kProfPhases = 12;  // 0-7 phases, 8 poll spins, 10 core cycles, 11 wall ticks
 

@@ -78,7 +78,10 @@ def test_group_all_policies_vs_oracle(default_trace, name, pol, sel):
     g.load_events(rp.events, n_ev)
     g.run()
     got = g.results()
+    kernels = g.engines[0].last_run_kernels()
     g.close()
+    # FGD on k_hmemo slices, the other policies on k_replay slices (r06), each one launch for the group
+    assert kernels == (["k_hmemo_group"] if name == "FGD" else ["k_replay_group"]), kernels
     onodes = helpers.oracle_subset(default_trace, rp, keep)
     want, _, _ = O.run_events(onodes, helpers.oracle_typical(default_trace),
                               helpers.oracle_events(default_trace, rp, n_ev), policy=pol, gpu_sel=sel, seed=3,
