@@ -48,11 +48,29 @@ struct NodeV {
   KSIM_HD int pods_left() const { return (int)(int16_t)(meta & 0xffffu); }
   KSIM_HD int gpu_cnt() const { return (int)((meta >> 16) & 0xffu); }
   KSIM_HD int gpu_type() const { return (int)(meta >> 24); }
-  KSIM_HD int total() const {
-    int t = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t += gl(i);
-    return t;
+  // The eight milli-left lanes as packed 16-bit pairs (v_pk_* on gfx950).  Every record keeps 0 <= gl <= 1000 and
+  // gl = 0 on the lanes past gpu_cnt (set_nodes; a Bind touches only the node's own GPUs), which the packed
+  // reductions below rely on: they fold all eight lanes with no per-lane `g < gpu_cnt` test.
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  KSIM_HD static u16x2 pk(uint32_t w) {
+    u16x2 v;
+    __builtin_memcpy(&v, &w, 4);
+    return v;
+  }
+  KSIM_HD int total() const {  // (<= 8000: no packed lane overflows)
+    const u16x2 t = (pk(g[0]) + pk(g[1])) + (pk(g[2]) + pk(g[3]));
+    return (int)t.x + (int)t.y;
+  }
+  KSIM_HD int gl_max() const {  // the most milli left on one GPU (0 with no GPU)
+    const u16x2 m = __builtin_elementwise_max(__builtin_elementwise_max(pk(g[0]), pk(g[1])),
+                                              __builtin_elementwise_max(pk(g[2]), pk(g[3])));
+    return m.x > m.y ? (int)m.x : (int)m.y;
+  }
+  KSIM_HD int gl_full() const {  // GPUs with all 1000 milli left: gl - 999 saturated at 0 is 1 there and 0 below
+    const u16x2 k = {(unsigned short)999, (unsigned short)999};
+    const u16x2 t = (__builtin_elementwise_sub_sat(pk(g[0]), k) + __builtin_elementwise_sub_sat(pk(g[1]), k)) +
+                    (__builtin_elementwise_sub_sat(pk(g[2]), k) + __builtin_elementwise_sub_sat(pk(g[3]), k));
+    return (int)t.x + (int)t.y;
   }
 };
 
@@ -474,16 +492,10 @@ KSIM_HD bool filter_scan(const NodeV& n, const PodDev& p) {
   if (p.milli > 0) {
     const int cnt = n.gpu_cnt();
     bool dev = (cnt != 0) & (((p.tmask >> n.gpu_type()) & 1u) != 0u) & (p.num > 0);
-    if (p.num == 1) {
-      bool any = false;
-#pragma unroll
-      for (int g = 0; g < kMaxGpu; ++g) any = any | ((g < cnt) & (n.gl(g) >= p.milli));
-      dev = dev & any;
-    } else if (p.milli == kMilli) {
-      int slots = 0;
-#pragma unroll
-      for (int g = 0; g < kMaxGpu; ++g) slots += ((g < cnt) & (n.gl(g) == kMilli)) ? 1 : 0;
-      dev = dev & (slots >= p.num);
+    if (p.num == 1) {  // some GPU holds the share (packed max over the lanes; p.milli >= 1)
+      dev = dev & (n.gl_max() >= p.milli);
+    } else if (p.milli == kMilli) {  // enough whole GPUs
+      dev = dev & (n.gl_full() >= p.num);
     } else {
       dev = dev & filter_node(n, p);  // a partial multi-GPU request (no trace has one)
     }
@@ -786,9 +798,7 @@ KSIM_HD int dotprod_merge_max(const NodeV& n, const PodDev& p) {
 KSIM_HD int packing_score(const NodeV& n, const PodDev& p, bool* err) {
   *err = false;
   const int cnt = n.gpu_cnt();
-  int ff = 0;
-#pragma unroll
-  for (int g = 0; g < kMaxGpu; ++g) ff += (g < cnt && n.gl(g) == kMilli) ? 1 : 0;
+  const int ff = n.gl_full();
   if (ff == cnt) {
     const int s = 100 / 3 - ff;
     return s > ff ? s : ff;
