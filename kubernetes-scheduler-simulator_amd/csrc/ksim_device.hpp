@@ -803,6 +803,31 @@ KSIM_HD int packing_score(const NodeV& n, const PodDev& p, bool* err) {
     const int s = 100 / 3 - ff;
     return s > ff ? s : ff;
   }
+  // The two request shapes of the traces in closed form over the packed lanes (the loop below is the general one):
+  if (p.milli == kMilli && p.num >= 1) {  // num whole GPUs: each pick is a full GPU (the least milli >= 1000): ffuse = num
+    if (ff < p.num) {
+      *err = true;
+      return 0;
+    }
+    const int s = 100 / 2 - p.num;
+    return s > 100 / 3 ? s : 100 / 3;
+  }
+  if (p.num == 1) {  // one share: the least milli left >= p.milli (lanes below it, and the absent ones, map high)
+    const NodeV::u16x2 k = {(unsigned short)(0x8000 - p.milli), (unsigned short)(0x8000 - p.milli)};
+    const NodeV::u16x2 f = {(unsigned short)0x8000, (unsigned short)0x8000};
+    auto w = [&](uint32_t x) { return (NodeV::pk(x) + k) ^ f; };  // gl - milli if gl >= milli, else >= 0x8000
+    const NodeV::u16x2 m = __builtin_elementwise_min(__builtin_elementwise_min(w(n.g[0]), w(n.g[1])),
+                                                     __builtin_elementwise_min(w(n.g[2]), w(n.g[3])));
+    const int d = m.x < m.y ? (int)m.x : (int)m.y;
+    if (d > kMilli) {
+      *err = true;
+      return 0;
+    }
+    const int bv = d + p.milli;
+    if (bv == kMilli) return 100 / 2 - 1 > 100 / 3 ? 100 / 2 - 1 : 100 / 3;
+    const int s = 100 - (bv * 100 / kMilli) / 10;
+    return s > 100 / 2 ? s : 100 / 2;
+  }
   unsigned taken = 0u;
   int ffuse = 0, req = p.num, r = 0;
   for (int k = 0; k < kMaxGpu && req > 0; ++k) {

@@ -140,6 +140,13 @@ def test_cheap_scores_and_exclusive_fuzz(dm):
             assert e1.value == e2.value and (e1.value or a == b)
             assert dm.dm_exclusive(g8, cnt, milli, num) == L.orc_allocate_exclusive_gpu_id(C.byref(node),
                                                                                             C.byref(pr))
+        if milli > 0:  # GpuPacking's closed forms (whole GPUs, one share) against its general loop's shapes too
+            for m2, n2 in ((milli, num), (1000, 0), (1000, rnd.choice([1, 2, 3])), (rnd.choice([1, 300, 999, 1000]), 1)):
+                pr2 = O.pod_res(cpu, m2, n2, "")
+                e1, e2 = C.c_int(0), C.c_int(0)
+                a = dm.dm_packing(g8, cnt, cpu, m2, n2, C.byref(e1))
+                b = L.orc_packing_score(C.byref(node), C.byref(pr2), C.byref(e2))
+                assert e1.value == e2.value and (e1.value or a == b), (gl, cnt, m2, n2, a, b)
         tags = [rnd.choice([0, 0, 0, 1, 2]) for _ in range(9)]
         tag = -1 if num == 0 else (0 if (num == 1 and milli < 1000) else num)
         want = L.orc_clustering_score(C.byref(node), C.byref(pr), tag, (C.c_int32 * 9)(*tags))
