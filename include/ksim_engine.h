@@ -366,6 +366,9 @@ int  ksim_engine_last_run_kernels(ksim_engine* e, char* out, int cap);
  * has started): *gate 0 = no gate, 1 = opened, -1 = given up at its 2 s bound (the groups then
  * launch unordered, and a note goes to stderr); *timeouts = gates given up over the engine's life. */
 int  ksim_engine_last_run_gate(ksim_engine* e, int* gate, long long* timeouts);
+/* Replicas of the last run whose cluster report ran overlapped (a throughput-bound cheap group of a paper-sweep run:
+ * each replica's report as soon as its replay ends), 0 when none. */
+int  ksim_engine_last_run_report_overlap(ksim_engine* e, int* replicas);
 /* Workgroups per replica used by the last run. */
 int  ksim_engine_last_run_wgs(ksim_engine* e, int* wgs_per_replica);
 /* Execution path of the last run: KSIM_PATH_REPLAY (k_replay, every node scanned per pod),

@@ -1829,6 +1829,10 @@ struct ksim_engine {
   int* d_m_evcls = nullptr;     // decider mode: class of each event
   unsigned* d_topg = nullptr;   // decider mode: top granules
   unsigned* d_m_hkeys = nullptr;  // k_memo with the keys in HBM (MemoPlan::hkeys)
+  unsigned long long* d_done = nullptr;  // [2 + R] the overlapped report's queue (ksim_scan1.hpp Scan1Args::done)
+  int done_cap = 0;
+  unsigned done_epoch = 0;
+  hipEvent_t ev_ovl = nullptr;    // the queue's tickets zeroed (the report's stream waits on it)
   size_t m_cap2[3] = {0, 0, 0};
   double* d_th = nullptr;       // FGD score steps (build_score_thresholds), null if unusable
   size_t m_cap[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1889,6 +1893,7 @@ struct ksim_engine {
   int* h_started = nullptr;   // residency gate: host-mapped flags, one per FGD workgroup (hipHostMalloc)
   int* d_started = nullptr;   // its device address
   int started_cap = 0, gate_epoch = 0;
+  int last_ovl = 0;           // replicas the last run's overlapped report took (k_report_overlap)
   int last_gate = 0;          // the last run's residency gate: 0 none, 1 opened, -1 given up at its bound (stderr note)
   long long gate_timeouts = 0;  // gates given up at their bound, over the engine's life
   std::string last_kernels;    // the replay kernels the last run launched, '+'-joined in launch order
@@ -3081,7 +3086,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist, e->d_done};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -3089,6 +3094,7 @@ void ksim_engine_destroy(ksim_engine* e) {
     if (e->tev_side[i]) (void)hipEventDestroy(e->tev_side[i]);
   }
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_ovl) (void)hipEventDestroy(e->ev_ovl);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
   if (e->ev_mid) (void)hipEventDestroy(e->ev_mid);
@@ -3981,6 +3987,18 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       KSIM_HIP(hipEventRecord(e->tev_fork, e->stream));
     }
   }
+  // The overlapped report (KSIM_VARIANT report_overlap=0 off): a cheap group with more replicas than the CUs the FGD
+  // groups leave can hold at once runs in waves of workgroups, so its last replicas end well after its first ones; its
+  // replicas then report one by one as each ends (k_report_overlap, behind the first group on that group's stream)
+  // instead of all after the last one.  ovl[g]: the group gets the queue and that report.
+  std::vector<char> ovl(groups.size(), 0);
+  int fgd_cus = 0;  // CUs the FGD groups hold (a k_memo / k_hmemo workgroup fills a CU's registers)
+  for (const auto& gp : groups) {
+    if (gp.first == kPolFgdH) fgd_cus += gp.second;
+    else if (gp.first == POL_FGD && e->run_mode != 2)
+      fgd_cus += gp.second * (e->mplan_ok ? e->mplan->K : e->hplan_ok ? e->hplan->K : 1);
+  }
+  unsigned ovl_epoch = 0;
   for (const auto& gp : groups) {
     const int Rg = gp.second;
     hipStream_t gs = e->stream;
@@ -4019,8 +4037,33 @@ static int run_persistent(ksim_engine* e, int max_ev) {
                                 : (reg1 ? (const void*)k_scan1_mix<false, true> : (const void*)k_scan1_mix<false, false>);
       const size_t lds = ksim_scan1::scan1_lds(e->N, ksim_scan1::kPolMix, e->report, reg1);
       ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N,
-                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0};
+                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0,
+                               nullptr, 0};
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      if (concurrent && e->report && gidx > 1 && variant("report_overlap", 1) != 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, ksim_scan1::kBlock, lds) != hipSuccess) {
+          (void)hipGetLastError();
+          nb = 0;
+        }
+        // (KSIM_TEST report_overlap=1: whatever the size, for the parity tests)
+        if (nb > 0 && (Rg > std::max(0, e->cus - fgd_cus) * nb || test_knob("report_overlap", 0) != 0)) {
+          if (Rg > e->done_cap) {
+            if (e->d_done) KSIM_HIP(hipFree(e->d_done));
+            KSIM_HIP(hipMalloc(&e->d_done, sizeof(unsigned long long) * (2 + (size_t)Rg)));
+            KSIM_HIP(hipMemset(e->d_done, 0, sizeof(unsigned long long) * (2 + (size_t)Rg)));
+            e->done_cap = Rg;
+          }
+          if (!e->ev_ovl) KSIM_HIP(hipEventCreateWithFlags(&e->ev_ovl, hipEventDisableTiming));
+          KSIM_HIP(hipMemsetAsync(e->d_done, 0, 2 * sizeof(unsigned long long), gs));  // tickets; entries keep epochs
+          KSIM_HIP(hipEventRecord(e->ev_ovl, gs));
+          ovl[gidx - 1] = 1;
+          e->last_ovl += Rg;
+          ovl_epoch = e->done_epoch = e->done_epoch % 0x7fffffffu + 1;
+          sa.done = e->d_done;
+          sa.epoch = ovl_epoch;
+        }
+      }
       void* params[] = {(void*)&sa};
       KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
       note_kernel(e, "k_scan1_mix");
@@ -4093,7 +4136,8 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       const void* f = scan1_fn(gp.first, e->report, reg);
       const size_t lds = ksim_scan1::scan1_lds(e->N, gp.first, e->report, reg);
       ksim_scan1::Scan1Args sa{e->d_reps, e->d_replist + first, e->N,
-                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0};
+                               dead_skip(e, std::vector<int>(order.begin() + first, order.begin() + first + Rg)) ? 1 : 0,
+                               nullptr, 0};
       KSIM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       void* params[] = {(void*)&sa};
       KSIM_HIP(hipLaunchKernel(f, dim3(Rg), dim3(ksim_scan1::kBlock), params, lds, gs));
@@ -4208,9 +4252,21 @@ static int run_persistent(ksim_engine* e, int max_ev) {
       hipStream_t rs = i < 0 ? e->stream : e->side[i];
       int mev = 0;
       for (int j = f; j < f + Rg; ++j) mev = std::max(mev, e->n_events[order[j]]);
+      if (ovl[g]) {  // behind the first group on its stream, each replica's report as soon as its replay ends
+        const int i0 = side_of(0);
+        rs = i0 < 0 ? e->stream : e->side[i0];
+        KSIM_HIP(hipStreamWaitEvent(rs, e->ev_ovl, 0));
+      }
       KSIM_HIP(hipEventRecord(e->grp_rev[2 * g], rs));
-      const int rc = run_report(e, mev, rs, e->d_replist + f, Rg);
-      if (rc) return rc;
+      if (ovl[g]) {
+        hipLaunchKernelGGL(ksim_rep::k_report_overlap, dim3(std::min(Rg, std::max(1, e->cus - e->cus / 16))), dim3(ksim_rep::kScanBlock),
+                           0, rs, (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N,
+                           (const int*)(e->d_replist + f), Rg, e->d_done, ovl_epoch, e->d_fail);
+        KSIM_HIP(hipGetLastError());
+      } else {
+        const int rc = run_report(e, mev, rs, e->d_replist + f, Rg);
+        if (rc) return rc;
+      }
       KSIM_HIP(hipEventRecord(e->grp_rev[2 * g + 1], rs));
       f += Rg;
     }
@@ -4261,6 +4317,7 @@ int ksim_engine_run(ksim_engine* e) {
   e->last_launches = 0;
   e->last_streams = 0;
   e->last_gate = 0;
+  e->last_ovl = 0;
   e->last_kernels.clear();
   int rc = prepare_memo(e, max_ev);
   if (rc) return rc;
@@ -4896,6 +4953,12 @@ int ksim_engine_last_run_gate(ksim_engine* e, int* gate, long long* timeouts) {
   if (!e || !gate || !timeouts) return KSIM_EINVAL;
   *gate = e->last_gate;
   *timeouts = e->gate_timeouts;
+  return KSIM_OK;
+}
+
+int ksim_engine_last_run_report_overlap(ksim_engine* e, int* replicas) {
+  if (!e || !replicas) return KSIM_EINVAL;
+  *replicas = e->last_ovl;
   return KSIM_OK;
 }
 

@@ -83,16 +83,8 @@ __device__ __forceinline__ void store_rep(RepAcc* o, const __int128 (&f)[kFields
   o->cnt[kFields - kFx] = 0;
 }
 
-// grid (ceil(E_max / kDeltaBlock), R): the report delta of every event.
-__global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
-                                                              const int* list) {
-  const int r = list ? list[blockIdx.y] : (int)blockIdx.y;  // list: one concurrent group's replicas
-  const ReplicaDev rp = reps[r];
-  if (!rp.rep) return;
-  __shared__ TypDev s_tp[kMaxTypical];
-  stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
-  const int e = (int)blockIdx.x * kDeltaBlock + (int)threadIdx.x;
-  if (e >= rp.n_events) return;
+// The report delta of event e of a replica (s_tp: its typical table in LDS).
+__device__ __forceinline__ void report_delta_event(const ReplicaDev& rp, const TypDev* s_tp, int e) {
   __int128 d[kFields];
 #pragma unroll
   for (int k = 0; k < kFields; ++k) d[k] = 0;
@@ -117,6 +109,19 @@ __global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* 
     d[15] = a[15] - b[15];
   }
   store_rep(rp.rep + e, d);
+}
+
+// grid (ceil(E_max / kDeltaBlock), R): the report delta of every event.
+__global__ __launch_bounds__(kDeltaBlock) void k_report_delta(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
+                                                              const int* list) {
+  const int r = list ? list[blockIdx.y] : (int)blockIdx.y;  // list: one concurrent group's replicas
+  const ReplicaDev rp = reps[r];
+  if (!rp.rep) return;
+  __shared__ TypDev s_tp[kMaxTypical];
+  stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
+  const int e = (int)blockIdx.x * kDeltaBlock + (int)threadIdx.x;
+  if (e >= rp.n_events) return;
+  report_delta_event(rp, s_tp, e);
 }
 
 __device__ __forceinline__ __int128 shfl_up128(__int128 v, int o) {
@@ -173,15 +178,9 @@ __device__ __forceinline__ void block_excl_scan_fields(__int128 (&v)[kFields], _
 // block scan gives each chunk's start, a second pass writes the running sums -- each record read twice and
 // written once (r05; the r01-r04 form took one read-sum and one read-write pass per field, 32 passes over
 // the records).
-__global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
-                                                            int N, const int* list) {
-  const int r = list ? list[blockIdx.x] : (int)blockIdx.x;
-  const ReplicaDev rp = reps[r];
-  if (!rp.rep) return;
-  __shared__ TypDev s_tp[kMaxTypical];
+__device__ __forceinline__ void report_scan_replica(const ReplicaDev& rp, const TypDev* s_tp, int N) {
   __shared__ __int128 s_w[kScanBlock / 64][kFields];
   __shared__ __int128 s_base[kFields];
-  stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
   const int tid = (int)threadIdx.x;
   // the cluster as run() starts it (analysis.go:80-98 over the initial state)
   {
@@ -220,6 +219,62 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
       // the power fields stay 0 without an energy model (k_report_delta wrote 0; the sums are 0 too)
       rep_set(o, k, run[k]);
     }
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
+                                                            int N, const int* list) {
+  const int r = list ? list[blockIdx.x] : (int)blockIdx.x;
+  const ReplicaDev rp = reps[r];
+  if (!rp.rep) return;
+  __shared__ TypDev s_tp[kMaxTypical];
+  stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
+  report_scan_replica(rp, s_tp, N);
+}
+
+// The report of one group's replicas in the order their replays end (a grid of 15/16 of the CUs at most, launched
+// behind another group on another stream; a workgroup fills a CU's registers, so a replay workgroup not yet
+// dispatched always finds a CU): each workgroup takes the next ticket (queue[1]), waits for the
+// replay kernel's entry in that slot (queue[2 + slot] = epoch << 32 | position, stored after the replica's last store,
+// released at agent scope), acquires, and runs k_report_delta's and k_report_scan's work for that replica; then the
+// next ticket, until all Rg are taken.  A throughput-bound group (more replicas than the device holds at once)
+// otherwise reports only after its last replica ends.  Every wait is bounded (~seconds: *fail, the run returns
+// KSIM_ESTATE).  Measured at C4 (profiles/r06/ovl): a grid of 64 / 128 / 192 / 240 workgroups ends the run at
+// 79.0 / 73.8 / 72.5 / 72.3 ms (75.4 with the report after the group): the backlog the FGD group leaves is
+// throughput-bound up to ~200 workgroups, then the last replica's own report (~0.8 ms) is the tail.
+__global__ __launch_bounds__(kScanBlock) void k_report_overlap(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
+                                                               int N, const int* list, int Rg,
+                                                               unsigned long long* queue, unsigned epoch, int* fail) {
+  __shared__ int s_b;
+  __shared__ TypDev s_tp[kMaxTypical];
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const int slot = (int)__hip_atomic_fetch_add(queue + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int b = -1;
+      if (slot < Rg) {
+        unsigned spins = 0;
+        unsigned long long x;
+        while (((x = __hip_atomic_load(queue + 2 + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != epoch) {
+          if (++spins > (1u << 26)) { atomicOr(fail, 64); break; }
+          __builtin_amdgcn_s_sleep(8);
+        }
+        if ((x >> 32) == epoch) b = (int)(unsigned)x;
+      }
+      s_b = b;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int b = s_b;
+    if (b < 0) return;
+    const int r = list[b];
+    const ReplicaDev rp = reps[r];
+    if (rp.rep) {
+      stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
+      for (int e = (int)threadIdx.x; e < rp.n_events; e += kScanBlock) report_delta_event(rp, s_tp, e);
+      __syncthreads();
+      report_scan_replica(rp, s_tp, N);
+    }
+    __syncthreads();  // (s_b, s_tp and the scan's LDS are reused by the next replica)
   }
 }
 

@@ -41,6 +41,12 @@ struct Scan1Args {
   const int* rep_list;  // replica of each workgroup
   int N;
   int skip;             // the dead-class skip (every replica's classes fit kDeadWords x 32 bits)
+  // The overlapped report's queue (ksim_report.hpp k_report_overlap; null: none): once a workgroup's replay --
+  // results, report records, final state -- is visible device-wide, it takes the next slot (done[0], a ticket zeroed
+  // before the run) and stores epoch << 32 | its position in the launch there (done[2 + slot]); the report takes
+  // replicas in that order, while the longer ones still run.
+  unsigned long long* done;
+  unsigned epoch;
 };
 constexpr int kDeadWords = 32;  // dead-class bitmask: class ids < 1024
 
@@ -253,6 +259,15 @@ __device__ __forceinline__ void scan1_body(const Scan1Args& a, const ReplicaDev&
       if (tid + kBlock * k < N) store_node(rp.nodes + tid + kBlock * k, rn[k]);
   } else {
     for (int i = tid; i < N; i += kBlock) store_node(rp.nodes + i, load_node(&s_nodes[i]));
+  }
+  if (a.done) {  // every wave's stores drained and released at agent scope, the barrier, then the queue entry
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long slot = __hip_atomic_fetch_add(a.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done + 2 + slot, (unsigned long long)a.epoch << 32 | blockIdx.x, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -166,6 +166,7 @@ SIGNATURES = {
     "ksim_engine_last_run_wgs": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_last_run_launches": (C.c_int, [_VP, _P(C.c_int), _P(C.c_int)]),
     "ksim_engine_last_run_gate": (C.c_int, [_VP, _P(C.c_int), _P(C.c_longlong)]),
+    "ksim_engine_last_run_report_overlap": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_last_run_kernels": (C.c_int, [_VP, C.c_char_p, C.c_int]),
     "ksim_engine_last_run_path": (C.c_int, [_VP, _P(C.c_int)]),
     "ksim_engine_set_report": (C.c_int, [_VP, C.c_int]),
@@ -686,6 +687,12 @@ class Engine:
         g, t = C.c_int(0), C.c_longlong(0)
         check(lib().ksim_engine_last_run_gate(self.h, C.byref(g), C.byref(t)), "last_run_gate")
         return g.value, t.value
+
+    def last_run_report_overlap(self):
+        """Replicas whose cluster report the last run() overlapped with the longer replays (0: none)."""
+        n = C.c_int(0)
+        check(lib().ksim_engine_last_run_report_overlap(self.h, C.byref(n)), "last_run_report_overlap")
+        return n.value
 
     def last_run_wgs(self):
         k = C.c_int(0)

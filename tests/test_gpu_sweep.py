@@ -197,3 +197,27 @@ def test_share_with_widened_fgd_rows_identical():
         assert len(mm) == 45 and not any(mm.values()), kind
     ratio_rows = ratio_deviations({k: v for k, v in curves.items() if k[1] != "01-Random"})
     assert len(ratio_rows) == 45 and max(ratio_rows.values()) <= RATIO_TOL
+
+
+@pytest.mark.parametrize("overlap", ["1", "0"], ids=["overlapped", "after"])
+def test_overlapped_report_rows_identical(overlap, monkeypatch):
+    # the cheap group's cluster report replica by replica as each replay ends (k_report_overlap, behind the FGD
+    # group on its stream; forced here, on the full sweep it runs when the cheap group outnumbers the free CUs) and
+    # after the whole group (KSIM_VARIANT report_overlap=0): every row identical to expected_results either way
+    if overlap == "1":
+        monkeypatch.setenv("KSIM_TEST", "report_overlap=1")
+    else:
+        monkeypatch.setenv("KSIM_VARIANT", "report_overlap=0")
+    sw = SW.Sweep(SW.plan(traces=["openb_pod_list_default", "openb_pod_list_gpushare40"], seeds=[42, 44, 47]), wgs=1)
+    for _ in range(2):  # the second run reuses the queue (its entries carry the run's epoch)
+        sw.run()
+        n_ovl = sw.eng.last_run_report_overlap()
+        curves = sw.curves()
+        assert n_ovl == (30 if overlap == "1" else 0), n_ovl
+        for kind, csv in (("alloc", ALLO), ("frag", FRAG)):
+            mm = SW.row_mismatches({k: v for k, v in curves.items() if k[1] != "01-Random"}, kind,
+                                   SW.expected_rows(csv))
+            assert len(mm) == 30 and not any(mm.values()), kind
+        ratio_rows = ratio_deviations({k: v for k, v in curves.items() if k[1] != "01-Random"})
+        assert len(ratio_rows) == 30 and max(ratio_rows.values()) <= RATIO_TOL
+    sw.close()
