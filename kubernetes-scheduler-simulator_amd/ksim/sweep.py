@@ -43,14 +43,20 @@ def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
 
 # Cost model of one experiment on one GPU: its events x the per-event latency of its replay chain, read from the
 # measured table (profiles/r06/c4_costs.jsonl, scripts/r06/c4_costs.py: every trace and policy alone on the GPU, the
-# seed with the most events, the cluster report on) -- FGD on k_hmemo at one workgroup ("one") and on k_memo at
-# WIDE_K workgroups ("wide"), the cheap policies on k_scan1.  Without the table: the r05 constants (FGD ~4.1 us per
-# event up to ~64 typical pods, growing with the typical table beyond; the cheap policies ~3.3 us).
+# seed with the most events, the cluster report on) -- FGD on k_hmemo at one workgroup ("one") and on k_memo at K
+# workgroups ("wide<K>"), the cheap policies on k_scan1.  Without the table: the r05 constants (FGD ~4.1 us per
+# event up to ~64 typical pods, growing with the typical table beyond, 0.8x widened; the cheap policies ~3.3 us).
 COST_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                           "profiles", "r06", "c4_costs.jsonl")
 FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
-WIDE_K = 16   # workgroups of a widened FGD replica (k_memo; share 0/8: 50.9 ms at 16 x 13 replicas, 52.0 at 25 x 8)
-PER_CU_CHEAP = 3  # cheap replicas a CU holds without their chains slowing much (6 fit; at 6 a share took 89 ms)
+# The widths plan_widths chooses from, per share: (workgroups of a widened FGD replica, cheap replicas planned per
+# CU, how much the cheap chains slow down packed that tight).  k_memo at 12 workgroups is within 1-3 % of 16 for the
+# long traces (profiles/r06/c4_wide/wide_k_r06.jsonl), so a share with more long FGD chains than 16-wide slots widens
+# more of them at 12 and packs the cheap replicas 6 to a CU (their chains ~1.4x longer: share 0/4 ends at 56.3 ms
+# against 60.4; profiles/r06/c4_shares/widths_r06.txt); share 0/8 widens all of its long chains at 16 either way.
+WIDTHS = ((16, 3, 1.0), (12, 6, 1.4))
+WIDE_K, PER_CU_CHEAP = WIDTHS[0][0], WIDTHS[0][1]
+WIDEN_MARGIN = 0.9
 _COSTS = None
 
 
@@ -64,7 +70,10 @@ def load_costs(path=COST_TABLE):
                 for ln in f:
                     d = json.loads(ln)
                     if d.get("us_per_event"):
-                        out[(d["trace"], d["policy"], d["form"])] = d["us_per_event"]
+                        form = d["form"]
+                        if form == "wide":  # the r06 table's first form: one width, in wgs_req
+                            form = "wide%d" % d["wgs_req"]
+                        out[(d["trace"], d["policy"], form)] = d["us_per_event"]
         if path != COST_TABLE:
             return out
         _COSTS = out
@@ -78,7 +87,7 @@ def experiment_cost_us(policy_dir, events, n_typical, trace=None, form="one"):
     if us is not None:
         return events * us
     if policy_dir == "06-FGD":
-        return events * (FGD_US + FGD_US_PER_TYP * max(0, n_typical - 64)) * (0.8 if form == "wide" else 1.0)
+        return events * (FGD_US + FGD_US_PER_TYP * max(0, n_typical - 64)) * (0.8 if form.startswith("wide") else 1.0)
     return events * CHEAP_US
 
 
@@ -101,27 +110,49 @@ def plan_costs(items, form="one"):
     return out
 
 
-def plan_widths(items, costs, wide_costs, cus=256, wide_k=WIDE_K, per_cu_cheap=PER_CU_CHEAP):
-    """Critical-path-aware widths for one share's experiments (run concurrently on one GPU): the share's time is its
-    longest replay chain, so the FGD replays whose one-workgroup chain is longer than everything else the share
-    holds take k_memo at wide_k workgroups, longest first, while the CUs last -- each widened
-    replica holds wide_k CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap
-    replicas per_cu_cheap to a CU (profiles/r06/c4_wide/: packed tighter, their chains and the others' slow down).
-    -> {item index: wide_k} for the widened ones."""
+def _widen(items, costs, wide_costs, cus, wide_k, per_cu_cheap, cheap_slow):
+    """One width's greedy plan: the FGD replays whose one-workgroup chain is longer than everything else the share
+    holds take k_memo at wide_k workgroups, longest first, while the CUs last -- each widened replica holds wide_k
+    CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap replicas per_cu_cheap to
+    a CU.  -> (predicted share time: the longest chain after widening, {item index: wide_k})."""
     fgd = sorted((i for i, it in enumerate(items) if it[1] == "06-FGD"), key=lambda i: (-costs[i], i))
     cheap = [i for i, it in enumerate(items) if it[1] != "06-FGD"]
     free = cus - len(fgd) - -(-len(cheap) // per_cu_cheap)
-    floor = max((costs[i] for i in cheap), default=0.0)  # the longest chain widening cannot shorten
+    floor = max((costs[i] for i in cheap), default=0.0) * cheap_slow  # the longest chain widening cannot shorten
     out = {}
-    for n, i in enumerate(fgd):
-        # the share's time if this one stays narrow: its own chain, or the longest widened chain so far
-        if costs[i] <= max([floor] + [wide_costs[j] for j in out]) or wide_costs[i] >= costs[i]:
+    for i in fgd:
+        # the share's time if this one stays narrow: its own chain, or the longest widened chain so far.  A chain
+        # within WIDEN_MARGIN of that is widened too while CUs last: beside the others on a full GPU every chain runs
+        # 3-5 % longer than alone, so a narrow chain just under the widened ones ends after them (share 1/8, 9
+        # widened: 51.2 ms; share 0/8, 12 widened: 48.3; profiles/r06/c4_shares/widths_r06.txt)
+        if costs[i] <= WIDEN_MARGIN * max([floor] + [wide_costs[j] for j in out]) or wide_costs[i] >= costs[i]:
             break
         if free < wide_k - 1:
             break
         out[i] = wide_k
         free -= wide_k - 1
-    return out
+    narrow = max((costs[i] for i in fgd if i not in out), default=0.0)
+    return max([floor, narrow] + [wide_costs[j] for j in out]), out
+
+
+def plan_widths(items, costs, wide_costs, cus=256, widths=WIDTHS):
+    """Critical-path-aware widths for one share's experiments (run concurrently on one GPU): the share's time is its
+    longest replay chain, so its longest FGD chains replay on k_memo at several workgroups.  Each
+    candidate of `widths` ((wide_k, per_cu_cheap, cheap_slow), WIDTHS) is planned greedily (_widen); the one with the
+    shortest predicted share time wins, ties to the one widening more, then to the first.  wide_costs: {wide_k: a cost
+    per item at that width} (plan_costs(items, "wide<K>")).  -> {item index: workgroups} for the widened ones."""
+    best = None
+    for n, (wide_k, per_cu, slow) in enumerate(widths):
+        t, out = _widen(items, costs, wide_costs[wide_k], cus, wide_k, per_cu, slow)
+        key = (t, -len(out), n)
+        if best is None or key < best[0]:
+            best = (key, out)
+    return best[1] if best else {}
+
+
+def plan_wide_costs(items, widths=WIDTHS):
+    """{wide_k: plan_costs(items, "wide<K>")} for every width of `widths`."""
+    return {k: plan_costs(items, "wide%d" % k) for k in sorted({w[0] for w in widths})}
 
 
 def shard(items, rank, world, costs=None):

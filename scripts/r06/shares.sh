@@ -8,6 +8,6 @@ for N in 8 4 2; do
   for ((k = 0; k < N; k++)); do
     timeout -k 10 120 python3 -u bench.py --config c4 --rank-share $k/$N --no-cpu-baseline --steps 3 --warmup 1 "$@" \
       > $O/share_${k}of${N}.json 2> $O/share_${k}of${N}.err || { echo "share $k/$N rc=$?"; tail -5 $O/share_${k}of${N}.err; exit 1; }
-    python3 -c "import json; d = json.load(open('$O/share_${k}of${N}.json')); print('$k/$N', d['config']['replicas_per_gpu'], d['config'].get('widened_fgd'), round(d['ms_per_step'], 2), d['roofline']['kernel'], d.get('residency_gate'))"
+    python3 -c "import json; d = json.load(open('$O/share_${k}of${N}.json')); print('$k/$N', d['config']['replicas_per_gpu'], d['config'].get('widened_fgd'), d['config'].get('wide_k'), round(d['ms_per_step'], 2), d['roofline']['kernel'], d.get('residency_gate'))"
   done
 done
