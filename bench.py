@@ -336,7 +336,7 @@ def main():
         # one workgroup per replica unless asked: every policy group then runs concurrently (FGD on k_hmemo, the
         # cheap policies as one k_scan1_mix launch) whatever the share's size -- a share small enough for k_memo
         # or k_replay at K > 1 would run its groups back to back (profiles/r05/c4_shares/).  The share's longest
-        # FGD chains take k_memo at 16 or 12 workgroups on the CUs the share leaves free (SW.plan_widths)
+        # FGD chains take k_memo at 12-32 workgroups each on the CUs the share leaves free (SW.plan_widths)
         wide = {} if args.no_widen else SW.plan_widths(exps, SW.plan_costs(exps), SW.plan_wide_costs(exps))
         sweep = SW.Sweep(exps, device=local, report=True, wgs=args.wgs or 1, random_stream=args.random_stream,
                          wide=wide)
@@ -451,7 +451,7 @@ def main():
         # whole job: every rank's experiments per timed step (the reference: 1020 in ~10 h on 256 vCPU)
         line["experiments_per_s"] = args.replicas * world / (dt / args.steps)
         line["config"]["widened_fgd"] = len(wide)  # FGD replays on k_memo at several workgroups (plan_widths)
-        line["config"]["wide_k"] = max(wide.values(), default=0)
+        line["config"]["wide_k"] = {str(k): sum(1 for v in wide.values() if v == k) for k in sorted(set(wide.values()))}
         if args.rank_share:
             line["config"]["rank_share"] = args.rank_share
             line["config"]["workload"] += " -- rank %s's share of the LPT split only (%d experiments)" % (

@@ -1829,11 +1829,12 @@ struct ksim_engine {
   int* d_m_evcls = nullptr;     // decider mode: class of each event
   unsigned* d_topg = nullptr;   // decider mode: top granules
   unsigned* d_m_hkeys = nullptr;  // k_memo with the keys in HBM (MemoPlan::hkeys)
+  int* d_m_wgmap = nullptr;       // k_memo: each block's launch position << 8 | workgroup (MemoArgs::wg_map)
   unsigned long long* d_done = nullptr;  // [2 + R] the overlapped report's queue (ksim_scan1.hpp Scan1Args::done)
   int done_cap = 0;
   unsigned done_epoch = 0;
   hipEvent_t ev_ovl = nullptr;    // the queue's tickets zeroed (the report's stream waits on it)
-  size_t m_cap2[3] = {0, 0, 0};
+  size_t m_cap2[4] = {0, 0, 0, 0};
   double* d_th = nullptr;       // FGD score steps (build_score_thresholds), null if unusable
   size_t m_cap[7] = {0, 0, 0, 0, 0, 0, 0};
   struct MemoPlan* mplan = nullptr;  // the FGD replicas' k_memo plan, uploaded before the timed run
@@ -2049,14 +2050,16 @@ static const void* replay_kernel(int pol, int K, bool general) {
 
 // ---- k_memo planning (memoised FGD replay, ksim_memo.hpp) ----
 struct MemoPlan {
-  int K = 0, Cw = 0, nfw = 0, Cmax = 1;
+  int K = 0, Cw = 0, nfw = 0, Cmax = 1;  // K: the most workgroups of a replica
+  int nwg = 0;                            // workgroups of the launch (Σ Kr)
+  std::vector<int> Kr, wgoff;             // [Rg] each replica's workgroups (r06: per replica), its first block
   bool decider = false;  // workgroup 0 decides, 1..K-1 own the classes
   bool hkeys = false;    // the keys in HBM (k_memo<..., kHKeys>): classes whose keys do not fit in LDS
   size_t lds = 0;
   std::vector<PodDev> pod;                  // [Rg][Cmax]
   std::vector<int> owner;                   // [Rg][Cmax]
-  std::vector<int> wgcls, wgref;            // [Rg][K][Cw]
-  std::vector<unsigned long long> wggrp;    // [Rg][K][Cw]
+  std::vector<int> wgcls, wgref;            // [nwg][Cw] (block wgoff[i] + w)
+  std::vector<unsigned long long> wggrp;    // [nwg][Cw]
 };
 
 // Classes of one replica onto K workgroups, at most Cw slots each.  Classes with the same score
@@ -2105,26 +2108,33 @@ static bool memo_assign(const std::vector<PodDev>& cls, int K, int Cw, std::vect
 }
 
 // forceK > 0: exactly that many workgroups per replica (a wide-hinted group, ksim_engine_set_replica_wgs);
-// hkeys_ok: when no K fits the keys in LDS, the keys may go to HBM (k_memo<..., kHKeys>, classes split over
-// the workgroups as evenly as the slots allow).
+// forceKr: that many for each replica (r06: the hints differ); hkeys_ok: when no K fits the keys in LDS, the keys
+// may go to HBM (k_memo<..., kHKeys>, classes split over the workgroups as evenly as the slots allow).
 static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPlan& pl, int forceK = 0,
-                      bool hkeys_ok = false) {
+                      bool hkeys_ok = false, const std::vector<int>* forceKr = nullptr) {
   using namespace ksim_memo;
   const int Rg = (int)reps.size();
   if (Rg == 0 || e->N > kMemoMaxRank + 1) return false;
   pl.Cmax = 1;
   for (int r : reps) pl.Cmax = std::max(pl.Cmax, (int)e->h_cls[r].size());
   const int K0 = forceK > 0 ? forceK : e->wgs_req > 0 ? e->wgs_req : std::min(64, e->cus / Rg);
-  if (K0 < 1 || Rg * K0 > e->cus) return false;
+  std::vector<int> Kr(Rg, K0);
+  if (forceKr) Kr = *forceKr;
+  if ((int)Kr.size() != Rg) return false;
+  auto total = [&]() { int t = 0; for (int k : Kr) t += k; return t; };
+  auto kmax = [&]() { return *std::max_element(Kr.begin(), Kr.end()); };
+  if (*std::min_element(Kr.begin(), Kr.end()) < 1 || kmax() > 64 || total() > e->cus) return false;
+  const bool forced = forceK > 0 || forceKr != nullptr;
   const int d0 = pl.decider ? 1 : 0;  // decider mode: classes on workgroups 1..K-1
   std::vector<std::vector<int>> sc(Rg), ow(Rg);
   // the smallest Cw >= Cw0 every replica's classes pack into (split: parts of a group on several workgroups)
-  auto pack = [&](int K, int Cw0, bool split) {
+  auto pack = [&](int Cw0, bool split) {
     for (int Cw = Cw0; Cw <= kMaxCw; ++Cw) {
-      bool ok = K > d0;
+      bool ok = true;
       for (int i = 0; ok && i < Rg; ++i) {
+        const int K = Kr[i];
         std::vector<int> s1;
-        ok = memo_assign(e->h_cls[reps[i]], K - d0, Cw, s1, ow[i], split);
+        ok = K > d0 && memo_assign(e->h_cls[reps[i]], K - d0, Cw, s1, ow[i], split);
         if (!ok) break;
         sc[i].assign((size_t)K * Cw, -1);
         std::copy(s1.begin(), s1.end(), sc[i].begin() + (size_t)d0 * Cw);
@@ -2134,51 +2144,61 @@ static bool memo_plan(const ksim_engine* e, const std::vector<int>& reps, MemoPl
     }
     return 0;
   };
+  auto cw0 = [&](int dd) {  // the fewest slots per workgroup that can hold every replica's classes
+    int c = 1;
+    for (int i = 0; i < Rg; ++i) c = std::max(c, ((int)e->h_cls[reps[i]].size() + Kr[i] - 1 - dd) / std::max(1, Kr[i] - dd));
+    return c;
+  };
   auto fold_waves = [&](int Cw, bool hk) {  // waves 1..9 need fold buffers on the critical path
     for (int f : {16, 12})
       if (memo_lds(e->N, Cw, f, hk) <= 160 * 1024) return f;
     return 0;
   };
   const void* fcap = (const void*)ksim_memo::k_memo<false, false>;
-  int K = K0, Cw = 0, nfw = 0;
+  int Cw = 0, nfw = 0;
   bool hk = false;
   for (;;) {
-    Cw = pack(K, std::max(1, (pl.Cmax + K - 1 - d0) / std::max(1, K - d0)), false);
+    Cw = pack(cw0(d0), false);
     nfw = Cw > 0 ? fold_waves(Cw, false) : 0;
     // every workgroup of the launch must be resident (they exchange granules every step)
-    if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw)))
+    if (nfw > 0 && kmax() > 1 && total() > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw)))
       return false;
     if (nfw > 0) break;
     if (hkeys_ok && !pl.decider) {  // the keys in HBM: LDS holds the cluster and the fold buffers only
-      Cw = pack(K, std::max(1, (pl.Cmax + K - 1) / K), true);
+      Cw = pack(cw0(0), true);
       nfw = Cw > 0 ? fold_waves(Cw, true) : 0;
-      if (nfw > 0 && K > 1 && Rg * K > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw, true))) return false;
+      if (nfw > 0 && kmax() > 1 && total() > resident_cap(e, fcap, memo_lds(e->N, Cw, nfw, true))) return false;
       if (nfw > 0) {
         hk = true;
         break;
       }
     }
-    if (forceK > 0 || e->wgs_req > 0 || K >= 64 || Rg * (K + 1) > e->cus) return false;
-    ++K;
+    const int K = Kr[0];
+    if (forced || e->wgs_req > 0 || K >= 64 || Rg * (K + 1) > e->cus) return false;
+    std::fill(Kr.begin(), Kr.end(), K + 1);
   }
-  pl.K = K;
+  pl.K = kmax();
+  pl.nwg = total();
+  pl.Kr = Kr;
+  pl.wgoff.assign(Rg, 0);
+  for (int i = 1; i < Rg; ++i) pl.wgoff[i] = pl.wgoff[i - 1] + Kr[i - 1];
   pl.Cw = Cw;
   pl.nfw = nfw;
   pl.hkeys = hk;
   pl.lds = memo_lds(e->N, Cw, nfw, hk);
   pl.pod.assign((size_t)Rg * pl.Cmax, PodDev{});
   pl.owner.assign((size_t)Rg * pl.Cmax, -1);
-  pl.wgcls.assign((size_t)Rg * K * Cw, -1);
-  pl.wgref.assign((size_t)Rg * K * Cw, 0);
-  pl.wggrp.assign((size_t)Rg * K * Cw, 0ull);
+  pl.wgcls.assign((size_t)pl.nwg * Cw, -1);
+  pl.wgref.assign((size_t)pl.nwg * Cw, 0);
+  pl.wggrp.assign((size_t)pl.nwg * Cw, 0ull);
   for (int i = 0; i < Rg; ++i) {
     const std::vector<PodDev>& cls = e->h_cls[reps[i]];
     for (size_t c = 0; c < cls.size(); ++c) {
       pl.pod[(size_t)i * pl.Cmax + c] = cls[c];
       pl.owner[(size_t)i * pl.Cmax + c] = ow[i][c];
     }
-    for (int w = 0; w < K; ++w) {
-      const size_t o = ((size_t)i * K + w) * Cw;
+    for (int w = 0; w < Kr[i]; ++w) {
+      const size_t o = ((size_t)pl.wgoff[i] + w) * Cw;
       for (int j = 0; j < Cw; ++j) {
         const int c = sc[i][(size_t)w * Cw + j];
         pl.wgcls[o + j] = c;
@@ -2444,12 +2464,10 @@ static int upload_memo(ksim_engine* e, const std::vector<int>& reps, int max_ev)
 static int prepare_memo(ksim_engine* e, int max_ev) {
   if (e->run_mode == 1 || e->run_mode == 2 || e->shard_world > 0) return KSIM_OK;
   std::vector<int> reps, wide, narrow;
-  int hint = 0;
   for (int r = 0; r < e->R; ++r)
     if (e->reps[r].policy == POL_FGD) {
       reps.push_back(r);
       (e->wgs_hint[r] > 1 ? wide : narrow).push_back(r);
-      hint = std::max(hint, e->wgs_hint[r]);
     }
   if (!e->mplan_dirty && reps == e->mplan_all && max_ev == e->mplan_max_ev) return KSIM_OK;
   e->mplan_dirty = false;
@@ -2467,10 +2485,12 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
   // run_mode 4 (or KSIM_VARIANT=memo_decider=1 with run_mode 0): the decider variant of k_memo
   pl.decider = e->run_mode == 4 || (e->run_mode == 0 && variant("memo_decider", 0) == 1);
   // run_mode 0 with some FGD replicas hinted wide (ksim_engine_set_replica_wgs, the paper sweep's longest chains):
-  // those on k_memo at the hinted width (the keys in HBM when they do not fit in LDS), the others on k_hmemo at
+  // those on k_memo, each at its hinted width (the keys in HBM when they do not fit in LDS), the others on k_hmemo at
   // one workgroup each, both groups in one concurrent run (run_persistent)
   if (e->run_mode == 0 && !wide.empty() && !narrow.empty() && !pl.decider) {
-    if (memo_plan(e, wide, pl, hint, true)) {
+    std::vector<int> kr;  // each wide replica at its own hinted width
+    for (int r : wide) kr.push_back(e->wgs_hint[r]);
+    if (memo_plan(e, wide, pl, 0, true, &kr)) {
       int rc = upload_memo(e, wide, max_ev);
       if (rc) return rc;
       rc = prepare_hmemo(e, narrow, max_ev);
@@ -2484,8 +2504,10 @@ static int prepare_memo(ksim_engine* e, int max_ev) {
       e->hplan_ok = false;
     }
   }
-  const int fk = wide.size() == reps.size() ? hint : 0;  // every FGD replica hinted: that width
-  if (!memo_plan(e, reps, pl, fk, e->run_mode == 3 || fk > 0))
+  std::vector<int> kr;  // every FGD replica hinted: each at its width
+  if (wide.size() == reps.size())
+    for (int r : reps) kr.push_back(e->wgs_hint[r]);
+  if (!memo_plan(e, reps, pl, 0, e->run_mode == 3 || !kr.empty(), kr.empty() ? nullptr : &kr))
     return e->run_mode == 0 ? prepare_hmemo(e, reps, max_ev) : KSIM_OK;
   return upload_memo(e, reps, max_ev);
 }
@@ -2518,7 +2540,7 @@ static int upload_memo(ksim_engine* e, const std::vector<int>& reps, int max_ev)
       if (ec[i] < 0) continue;
       const int o = pl.owner[(size_t)gi * pl.Cmax + ec[i]];
       const int w = o >> 8, slot = o & 0xff;
-      const int ref = pl.wgref[((size_t)gi * pl.K + w) * pl.Cw + slot];
+      const int ref = pl.wgref[((size_t)pl.wgoff[gi] + w) * pl.Cw + slot];
       evo[(size_t)gi * stride + i] = (w << 16) | (ref << 8) | slot;
     }
   }
@@ -2535,8 +2557,13 @@ static int upload_memo(ksim_engine* e, const std::vector<int>& reps, int max_ev)
     KSIM_HIP(hipMalloc(&e->d_th, sizeof(double) * 102));
     KSIM_HIP(hipMemcpyAsync(e->d_th, score_table(), sizeof(double) * 102, hipMemcpyHostToDevice, st));
   }
+  std::vector<int> wgmap((size_t)pl.nwg);
+  for (int gi = 0; gi < Rg; ++gi)
+    for (int w = 0; w < pl.Kr[gi]; ++w) wgmap[(size_t)pl.wgoff[gi] + w] = (gi << 8) | w;
+  if ((rc = ensure_buf(e->d_m_wgmap, e->m_cap2[3], wgmap.size()))) return rc;
+  KSIM_HIP(hipMemcpyAsync(e->d_m_wgmap, wgmap.data(), sizeof(int) * wgmap.size(), hipMemcpyHostToDevice, st));
   KSIM_HIP(hipStreamSynchronize(st));  // the host vectors are pageable and short-lived
-  if (pl.hkeys && (rc = ensure_buf(e->d_m_hkeys, e->m_cap2[2], (size_t)Rg * pl.K * pl.Cw * e->N))) return rc;
+  if (pl.hkeys && (rc = ensure_buf(e->d_m_hkeys, e->m_cap2[2], (size_t)pl.nwg * pl.Cw * e->N))) return rc;
   e->mplan_reps = reps;
   e->mplan_ok = true;
   return KSIM_OK;
@@ -2559,6 +2586,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   ksim_memo::MemoArgs ma;
   ma.reps = e->d_reps;
   ma.rep_list = e->d_replist + first;
+  ma.wg_map = e->d_m_wgmap;
   ma.N = e->N;
   ma.K = pl.K;
   ma.Cw = pl.Cw;
@@ -2592,14 +2620,14 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   const int TS = std::min(max_ev, 4000);
   constexpr int kT = ksim_memo::kTrace;
   if (tracing) {
-    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * kT * (size_t)Rg * pl.K * TS));
-    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * kT * (size_t)Rg * pl.K * TS, st));
+    KSIM_HIP(hipMalloc(&d_trace, sizeof(unsigned long long) * kT * (size_t)pl.nwg * TS));
+    KSIM_HIP(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * kT * (size_t)pl.nwg * TS, st));
     ma.trace = d_trace;
     ma.trace_steps = TS;
   }
   if (profile) {
-    if ((rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)Rg * pl.K * ksim_memo::kProfPhases))) return rc;
-    KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)Rg * pl.K * ksim_memo::kProfPhases, st));
+    if ((rc = ensure_buf(e->d_prof, e->prof_cap, (size_t)pl.nwg * ksim_memo::kProfPhases))) return rc;
+    KSIM_HIP(hipMemsetAsync(e->d_prof, 0, sizeof(unsigned long long) * (size_t)pl.nwg * ksim_memo::kProfPhases, st));
     ma.prof = e->d_prof;
   }
   // the general instantiation for the profile / trace / deletes / no score table, else the lean one (with the
@@ -2616,7 +2644,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
                   : ma.delay ? (const void*)k_memo<false, false, true>
                   : e->report ? (const void*)k_memo<false, false, false, true> : (const void*)k_memo<false, false>;
   const TypDev* tpp = e->d_tp;
-  rc = launch_persistent(f, Rg * pl.K, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1 && !started, ma, tpp);
+  rc = launch_persistent(f, pl.nwg, ksim_memo::kMBlock, pl.lds, st, e->coop && pl.K > 1 && !started, ma, tpp);
   if (rc) return rc;
   hipLaunchKernelGGL(ksim_memo::k_memo_finish, dim3((unsigned)((stride + 255) / 256), (unsigned)Rg), dim3(256), 0, st,
                      e->d_reps, (const int*)(e->d_replist + first), e->N);
@@ -2625,8 +2653,8 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
     // per step: owner's start -> publish, publish -> each other workgroup's receive, receive -> start
     // (s_memrealtime, 100 MHz); replica 0 only
     KSIM_HIP(hipStreamSynchronize(st));
-    const int K = pl.K;
-    std::vector<unsigned long long> h((size_t)kT * Rg * K * TS);
+    const int K = pl.Kr[0];
+    std::vector<unsigned long long> h((size_t)kT * pl.nwg * TS);
     KSIM_HIP(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     KSIM_HIP(hipFree(d_trace));
     std::vector<int> evo((size_t)TS);
@@ -2662,7 +2690,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
   }
   if (profile) {
     KSIM_HIP(hipStreamSynchronize(st));
-    const int nb = Rg * pl.K, P = ksim_memo::kProfPhases;
+    const int nb = pl.nwg, P = ksim_memo::kProfPhases;
     std::vector<unsigned long long> h((size_t)nb * P);
     KSIM_HIP(hipMemcpy(h.data(), e->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
     static const char* names[] = {"init", "A:crit-F+list", "syncA", "B:publish", "B:eval", "syncB", "C:keys", "top2",
@@ -2690,7 +2718,7 @@ static int launch_memo(ksim_engine* e, const MemoPlan& pl, int Rg, int first, in
                                     "owner: prefetch done", "crit F all done", "keys", "result written",
                                     "granule stored"};
       // owner phases: summed over the K workgroups of a replica (one owner per step)
-      std::fprintf(stderr, " %s %.3f;", extra[ph - 12], ph >= 15 ? sum / std::max(nb / pl.K, 1) : sum / nb);
+      std::fprintf(stderr, " %s %.3f;", extra[ph - 12], ph >= 15 ? sum / std::max(Rg, 1) : sum / nb);
     }
     if (pl.decider) {  // the deciders' own phases (workgroup 0 of each replica)
       static const char* dn[] = {"list + top wait", "F", "decide + bind", "end barrier"};
@@ -3084,7 +3112,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_pod, e->d_res1, e->d_feas, e->d_score, e->d_gpu, e->d_gran, e->d_hist, e->d_fail, e->d_prof, e->d_replist,
                   e->d_cap, e->d_mcap, e->d_last, e->d_send, e->d_recv, e->d_ptrs, e->d_m_pod, e->d_m_owner, e->d_m_wgcls,
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
-                  e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
+                  e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_m_wgmap, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
                   e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist, e->d_done};
   for (void* p : bufs) (void)hipFree(p);
@@ -3996,7 +4024,7 @@ static int run_persistent(ksim_engine* e, int max_ev) {
   for (const auto& gp : groups) {
     if (gp.first == kPolFgdH) fgd_cus += gp.second;
     else if (gp.first == POL_FGD && e->run_mode != 2)
-      fgd_cus += gp.second * (e->mplan_ok ? e->mplan->K : e->hplan_ok ? e->hplan->K : 1);
+      fgd_cus += e->mplan_ok ? e->mplan->nwg : gp.second * (e->hplan_ok ? e->hplan->K : 1);
   }
   unsigned ovl_epoch = 0;
   for (const auto& gp : groups) {
@@ -4084,12 +4112,12 @@ static int run_persistent(ksim_engine* e, int max_ev) {
         int* flags = nullptr;
         int epoch = 0;
         if (gate) {
-          const int rc = gate_flags(e, Rg * pl.K, &flags, &epoch);
+          const int rc = gate_flags(e, pl.nwg, &flags, &epoch);
           if (rc) return rc;
         }
         const int rc = launch_memo(e, pl, Rg, first, max_ev, gs, flags, epoch);
         if (rc) return rc;
-        if (gate) gate_wait(e, Rg * pl.K, epoch, "FGD k_memo");
+        if (gate) gate_wait(e, pl.nwg, epoch, "FGD k_memo");
         note_kernel(e, pl.hkeys ? "k_memo_hkeys" : "k_memo");
         e->last_K = pl.K;
         e->last_groups = (int)groups.size();

@@ -58,15 +58,18 @@ constexpr int kDItems = kLag * 9;
 
 struct MemoArgs {
   ReplicaDev* reps;
-  const int* rep_list;   // replica of each group of K workgroups
-  int N, K, Cw;
+  const int* rep_list;   // replica of each launch position
+  // launch position << 8 | workgroup index within the replica, per block: a replica's workgroups are consecutive
+  // blocks, K of them (r06: K may differ per replica -- the paper sweep's widened FGD replicas, MemoPlan::Kr)
+  const int* wg_map;
+  int N, K, Cw;          // K: the most workgroups of a replica
   int nfw;               // waves with a fold buffer (F evaluators)
   int Cmax;              // class table stride
   const PodDev* cls_pod;     // [launch replica][Cmax] representative request of each class
   const int* cls_owner;      // [launch replica][Cmax] (workgroup << 8) | slot
-  const int* wg_cls;         // [launch replica][K][Cw] class of each slot, -1 empty
-  const int* wg_ref;         // [launch replica][K][Cw] first slot with the same score request
-  const unsigned long long* wg_grp;  // [launch replica][K][Cw] slots sharing the request (on the first)
+  const int* wg_cls;         // [block][Cw] class of each slot, -1 empty
+  const int* wg_ref;         // [block][Cw] first slot with the same score request
+  const unsigned long long* wg_grp;  // [block][Cw] slots sharing the request (on the first)
   const int* ev_owner;       // [launch replica][win_stride] owner code of each event's class, -1 delete
   const double* th;          // [102] FGD score steps, or null: the direct sigmoid expression
   unsigned* win;             // [launch replica][win_stride] winner granules, zeroed before launch
@@ -83,7 +86,7 @@ struct MemoArgs {
   int delay;                 // the hdelay test knob (general and stress instantiations): 1 every wave before the end-of-step
                              // barrier (wave 0 before it receives the step's granule), 2 the owner's critical waves
                              // before their F, 4 every wave at the step start
-  unsigned* hkeys;           // kHKeys: [launch replica][K][Cw][N] the keys in HBM instead of LDS
+  unsigned* hkeys;           // kHKeys: [block][Cw][N] the keys in HBM instead of LDS
   // Residency gate (a concurrent run's wide FGD group, launched before the other groups): each workgroup stores
   // `gate_epoch` into started[its block] once it holds its LDS state; the host launches the next group when all
   // have (ksim_engine.hip run_persistent).  Null: no gate.
@@ -758,22 +761,23 @@ __global__ __launch_bounds__(kMBlock) void k_memo(MemoArgs a, const TypDev* __re
   extern __shared__ __attribute__((aligned(16))) char smem[];
   MemoShared& sh = *reinterpret_cast<MemoShared*>(smem);
   constexpr int kLW = kMWaves - 1;  // the list wave
-  const int gi = (int)blockIdx.x / a.K;  // replica position in this launch
+  const int gw = a.wg_map[blockIdx.x];
+  const int gi = gw >> 8;  // replica position in this launch
   const int r = a.rep_list[gi];
-  const int w = (int)blockIdx.x % a.K;
+  const int w = gw & 0xff;
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const ReplicaDev rp = a.reps[r];
   const TypDev* __restrict__ tp = tp_all + (size_t)r * kMaxTypical;
   const int N = a.N, Cw = a.Cw;
   const int* rank2idx = reinterpret_cast<const int*>(rp.tags + (size_t)N * kTagStride);
   NodeRec* s_nodes = reinterpret_cast<NodeRec*>(smem + sizeof(MemoShared));
-  unsigned* s_keys = kHKeys ? a.hkeys + ((size_t)gi * a.K + w) * Cw * N : reinterpret_cast<unsigned*>(s_nodes + N);
+  unsigned* s_keys = kHKeys ? a.hkeys + (size_t)blockIdx.x * Cw * N : reinterpret_cast<unsigned*>(s_nodes + N);
   double* s_fold = reinterpret_cast<double*>(
       reinterpret_cast<char*>(s_nodes + N) + (kHKeys ? 0 : (std::max((size_t)Cw * N * 4, sizeof(DeciderScratch)) + 15) & ~(size_t)15));
   int* s_last = reinterpret_cast<int*>(reinterpret_cast<char*>(s_fold) +
                                        std::max((size_t)a.nfw * kFoldBuf * 8, ((size_t)N * 8 + 15) & ~(size_t)15));
   const PodDev* cls_pod = a.cls_pod + (size_t)gi * a.Cmax;
-  const size_t wgo = ((size_t)gi * a.K + w) * Cw;
+  const size_t wgo = (size_t)blockIdx.x * Cw;
   unsigned* win = a.win + (size_t)gi * a.win_stride;
   const int* evo = a.ev_owner + (size_t)gi * a.win_stride;
   const bool is_w0 = w == 0;

@@ -49,13 +49,16 @@ def plan(traces=TRACES, policies=tuple(POLICY_DIRS), seeds=SEEDS, tune=1.3):
 COST_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                           "profiles", "r06", "c4_costs.jsonl")
 FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
-# The widths plan_widths chooses from, per share: (workgroups of a widened FGD replica, cheap replicas planned per
-# CU, how much the cheap chains slow down packed that tight).  k_memo at 12 workgroups is within 1-3 % of 16 for the
-# long traces (profiles/r06/c4_wide/wide_k_r06.jsonl), so a share with more long FGD chains than 16-wide slots widens
-# more of them at 12 and packs the cheap replicas 6 to a CU (their chains ~1.4x longer: share 0/4 ends at 56.3 ms
-# against 60.4; profiles/r06/c4_shares/widths_r06.txt); share 0/8 widens all of its long chains at 16 either way.
-WIDTHS = ((16, 3, 1.0), (12, 6, 1.4))
-WIDE_K, PER_CU_CHEAP = WIDTHS[0][0], WIDTHS[0][1]
+# The widths plan_widths chooses from: k_memo workgroups of a widened FGD replica (per replica since r06: the engine
+# launches each at its own width), and how tight the cheap replicas pack -- (replicas planned per CU, how much their
+# chains slow down packed that tight: share 0/4 at 6 to a CU, its cheap group 32.6 -> 50.9 ms;
+# profiles/r06/c4_shares/widths_r06.txt).  The measured costs per width are in the table (gpushare100 alone: 56.2 ms
+# on k_hmemo, 50.7 / 49.8 / 48.8 / 45.8 ms at 12 / 16 / 24 / 32 workgroups).
+WIDE_KS = (12, 16, 24, 32)
+CHEAP_PACKS = ((3, 1.0), (6, 1.4))
+# A chain within WIDEN_MARGIN of the share's predicted time is widened too while CUs last: beside the others on a full
+# GPU every chain runs 3-5 % longer than alone, so a narrow chain just under the widened ones ends after them (share
+# 1/8 with 9 widened: 51.2 ms; share 0/8 with 12: 48.3; profiles/r06/c4_shares/widths_r06.txt)
 WIDEN_MARGIN = 0.9
 _COSTS = None
 
@@ -110,49 +113,56 @@ def plan_costs(items, form="one"):
     return out
 
 
-def _widen(items, costs, wide_costs, cus, wide_k, per_cu_cheap, cheap_slow):
-    """One width's greedy plan: the FGD replays whose one-workgroup chain is longer than everything else the share
-    holds take k_memo at wide_k workgroups, longest first, while the CUs last -- each widened replica holds wide_k
-    CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap replicas per_cu_cheap to
-    a CU.  -> (predicted share time: the longest chain after widening, {item index: wide_k})."""
+def plan_widths(items, costs, wide_costs, cus=256, ks=WIDE_KS, packs=CHEAP_PACKS, margin=WIDEN_MARGIN):
+    """Critical-path-aware widths for one share's experiments (run concurrently on one GPU).  The
+    share's time is its longest replay chain: the cheap chains (cheap_slow x the longest, for the packing), the FGD
+    chains left on k_hmemo at one workgroup, and the widened ones on k_memo at their width.  Each widened replica holds
+    its workgroups' CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap replicas
+    per_cu to a CU.  For each packing, the shortest predicted time T that fits the CUs: every FGD chain longer than T
+    widened at the fewest workgroups that bring it under T; then the chains within `margin` of T at the fewest
+    workgroups that shorten them, longest first, while CUs last.  The packing with the shorter T wins (ties: the
+    first).  wide_costs: {K: a cost per item at K workgroups} (plan_wide_costs).
+    -> {item index: workgroups} for the widened ones."""
     fgd = sorted((i for i, it in enumerate(items) if it[1] == "06-FGD"), key=lambda i: (-costs[i], i))
     cheap = [i for i, it in enumerate(items) if it[1] != "06-FGD"]
-    free = cus - len(fgd) - -(-len(cheap) // per_cu_cheap)
-    floor = max((costs[i] for i in cheap), default=0.0) * cheap_slow  # the longest chain widening cannot shorten
-    out = {}
-    for i in fgd:
-        # the share's time if this one stays narrow: its own chain, or the longest widened chain so far.  A chain
-        # within WIDEN_MARGIN of that is widened too while CUs last: beside the others on a full GPU every chain runs
-        # 3-5 % longer than alone, so a narrow chain just under the widened ones ends after them (share 1/8, 9
-        # widened: 51.2 ms; share 0/8, 12 widened: 48.3; profiles/r06/c4_shares/widths_r06.txt)
-        if costs[i] <= WIDEN_MARGIN * max([floor] + [wide_costs[j] for j in out]) or wide_costs[i] >= costs[i]:
-            break
-        if free < wide_k - 1:
-            break
-        out[i] = wide_k
-        free -= wide_k - 1
-    narrow = max((costs[i] for i in fgd if i not in out), default=0.0)
-    return max([floor, narrow] + [wide_costs[j] for j in out]), out
-
-
-def plan_widths(items, costs, wide_costs, cus=256, widths=WIDTHS):
-    """Critical-path-aware widths for one share's experiments (run concurrently on one GPU): the share's time is its
-    longest replay chain, so its longest FGD chains replay on k_memo at several workgroups.  Each
-    candidate of `widths` ((wide_k, per_cu_cheap, cheap_slow), WIDTHS) is planned greedily (_widen); the one with the
-    shortest predicted share time wins, ties to the one widening more, then to the first.  wide_costs: {wide_k: a cost
-    per item at that width} (plan_costs(items, "wide<K>")).  -> {item index: workgroups} for the widened ones."""
+    ks = sorted(k for k in ks if k in wide_costs)
     best = None
-    for n, (wide_k, per_cu, slow) in enumerate(widths):
-        t, out = _widen(items, costs, wide_costs[wide_k], cus, wide_k, per_cu, slow)
-        key = (t, -len(out), n)
-        if best is None or key < best[0]:
-            best = (key, out)
+    for n, (per_cu, slow) in enumerate(packs):
+        budget = cus - len(fgd) - -(-len(cheap) // per_cu)
+        floor = max((costs[i] for i in cheap), default=0.0) * slow
+        cands = sorted({floor} | {costs[i] for i in fgd} | {wide_costs[k][i] for k in ks for i in fgd})
+        for T in cands:
+            if T < floor:
+                continue
+            out, need, ok = {}, 0, True
+            for i in fgd:
+                if costs[i] <= T:
+                    break
+                k = next((k for k in ks if wide_costs[k][i] <= T), None)
+                if k is None:
+                    ok = False
+                    break
+                out[i] = k
+                need += k - 1
+            if not ok or need > budget:
+                continue
+            for i in fgd:
+                if costs[i] <= margin * T:
+                    break
+                k = next((k for k in ks if wide_costs[k][i] < costs[i]), None)
+                if i in out or k is None or need + k - 1 > budget:
+                    continue
+                out[i] = k
+                need += k - 1
+            if best is None or (T, n) < best[0]:
+                best = ((T, n), out)
+            break
     return best[1] if best else {}
 
 
-def plan_wide_costs(items, widths=WIDTHS):
-    """{wide_k: plan_costs(items, "wide<K>")} for every width of `widths`."""
-    return {k: plan_costs(items, "wide%d" % k) for k in sorted({w[0] for w in widths})}
+def plan_wide_costs(items, ks=WIDE_KS):
+    """{K: plan_costs(items, "wide<K>")} for every width of `ks`."""
+    return {k: plan_costs(items, "wide%d" % k) for k in ks}
 
 
 def shard(items, rank, world, costs=None):

@@ -1,8 +1,8 @@
 """One C4 share (--rank-share k/N's experiments and plan_widths' widened FGD replicas) run whole and by part --
 the widened FGD replicas alone (k_memo), the other FGD replicas alone (k_hmemo), the cheap policies alone
 (k_scan1_mix) -- device ms (best of 3) and the launched kernels; KSIM_GROUP_TIMES=1 adds each group's end.
-Usage: python3 scripts/r06/share_parts.py k/N [wide K] [cheap replicas per CU] [whole]  (no K: plan_widths' choice
-among SW.WIDTHS; K 0: none widened)"""
+Usage: python3 scripts/r06/share_parts.py k/N [wide K] [cheap replicas per CU] [whole]  (no K: plan_widths' choice;
+K: every widened replica at K; K 0: none widened)"""
 import json
 import os
 import sys
@@ -18,22 +18,19 @@ only_whole = len(sys.argv) > 4
 items = SW.plan()
 exps = SW.shard(items, k, n, SW.plan_costs(items))
 costs = SW.plan_costs(exps)
+wcosts = SW.plan_wide_costs(exps)
 if kw is None:
-    wcosts = SW.plan_wide_costs(exps)
     wide = SW.plan_widths(exps, costs, wcosts)
-    kw = max(wide.values(), default=0)
-    pc = {k: p for k, p, _ in SW.WIDTHS}.get(kw, pc)
-    wcosts = wcosts.get(kw, costs)
 elif kw == 0:
-    wide, wcosts = {}, costs
+    wide = {}
 else:
-    wcosts = SW.plan_costs(exps, "wide%d" % kw)
-    wide = SW.plan_widths(exps, costs, {kw: wcosts}, widths=((kw, pc, 1.0),))
-print(json.dumps({"share": sys.argv[1], "experiments": len(exps), "wide": len(wide), "wide_k": kw, "per_cu_cheap": pc,
+    wide = SW.plan_widths(exps, costs, wcosts, ks=(kw,), packs=((pc, 1.0),))
+wc = {i: wcosts[k][i] for i, k in wide.items()}
+print(json.dumps({"share": sys.argv[1], "experiments": len(exps), "wide": len(wide), "wide_k": sorted(wide.values()), "per_cu_cheap": pc,
                   "wide_exps": [exps[i][:3] for i in sorted(wide)],
                   "est_ms": {"narrow_fgd_max": max((costs[i] for i, e in enumerate(exps) if e[1] == "06-FGD" and i not in wide),
                                                    default=0) / 1000,
-                             "wide_max": max((wcosts[i] for i in wide), default=0) / 1000,
+                             "wide_max": max(wc.values(), default=0) / 1000,
                              "cheap_max": max((costs[i] for i, e in enumerate(exps) if e[1] != "06-FGD"), default=0) / 1000}}),
       flush=True)
 parts = {"whole": list(range(len(exps))), "wide": sorted(wide),

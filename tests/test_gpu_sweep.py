@@ -174,17 +174,17 @@ def test_default_sweep_fgd_group_is_memoised():
     assert path == "memo+k_replay", path
 
 
-@pytest.mark.parametrize("wide_k", [16, 12])
-def test_share_with_widened_fgd_rows_identical(wide_k):
-    # round-5 verdict item 1: an N-GPU share's longest FGD replays on k_memo at one of SW.WIDTHS' widths (the gpuspec
-    # traces' keys in HBM, the untyped ones' in LDS) beside the one-workgroup FGD replicas (k_hmemo) and the cheap
-    # policies' k_scan1_mix, all concurrently: three launches, each gated before the next, every row still identical
-    # to expected_results
-    assert {16, 12} == {k for k, _, _ in SW.WIDTHS}
+@pytest.mark.parametrize("widths", [(16, 16), (12, 12), (24, 32), (32, 12)], ids=lambda w: "%d-%d" % w)
+def test_share_with_widened_fgd_rows_identical(widths):
+    # round-5 verdict item 1: an N-GPU share's longest FGD replays on k_memo, each at its own width (SW.WIDE_KS; the
+    # gpuspec traces' keys in HBM, the untyped ones' in LDS) beside the one-workgroup FGD replicas (k_hmemo) and the
+    # cheap policies' k_scan1_mix, all concurrently: three launches, each gated before the next, every row still
+    # identical to expected_results
+    assert set(widths) <= set(SW.WIDE_KS)
     items = SW.plan(traces=["openb_pod_list_gpuspec33", "openb_pod_list_gpushare100", "openb_pod_list_default"],
                     seeds=[42, 43, 48])
-    wide = {i: wide_k for i, e in enumerate(items)
-            if e[1] == "06-FGD" and (e[0], e[2]) in {("openb_pod_list_gpuspec33", 42), ("openb_pod_list_gpushare100", 48)}}
+    pick = {("openb_pod_list_gpuspec33", 42): widths[0], ("openb_pod_list_gpushare100", 48): widths[1]}
+    wide = {i: pick[(e[0], e[2])] for i, e in enumerate(items) if e[1] == "06-FGD" and (e[0], e[2]) in pick}
     assert len(wide) == 2
     sw = SW.Sweep(items, wgs=1, wide=wide)
     sw.run()
