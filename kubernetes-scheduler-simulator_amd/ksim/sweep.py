@@ -52,14 +52,18 @@ FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
 # The widths plan_widths chooses from: k_memo workgroups of a widened FGD replica (per replica since r06: the engine
 # launches each at its own width), and how tight the cheap replicas pack -- (replicas planned per CU, how much their
 # chains slow down packed that tight: share 0/4 at 6 to a CU, its cheap group 32.6 -> 50.9 ms;
-# profiles/r06/c4_shares/widths_r06.txt).  The measured costs per width are in the table (gpushare100 alone: 56.2 ms
-# on k_hmemo, 50.7 / 49.8 / 48.8 / 45.8 ms at 12 / 16 / 24 / 32 workgroups).
-WIDE_KS = (12, 16, 24, 32)
+# profiles/r06/c4_shares/widths_r06.txt).  The measured costs per width are in the table (gpushare80 alone: 60.7 ms
+# on k_hmemo, 56.9 / 54.3 / 48.3 / 46.8 / 44.2 / 41.6 ms at 6 / 8 / 12 / 16 / 24 / 32 workgroups).
+WIDE_KS = (6, 8, 12, 16, 24, 32)
 CHEAP_PACKS = ((3, 1.0), (6, 1.4))
 # A chain within WIDEN_MARGIN of the share's predicted time is widened too while CUs last: beside the others on a full
 # GPU every chain runs 3-5 % longer than alone, so a narrow chain just under the widened ones ends after them (share
 # 1/8 with 9 widened: 51.2 ms; share 0/8 with 12: 48.3; profiles/r06/c4_shares/widths_r06.txt)
 WIDEN_MARGIN = 0.9
+# CUs the plan leaves unused: the three launches do not pack the device perfectly, and a plan that fills all 256 lost
+# the cheap group's residency (its last replicas waited for CUs: share 1/4 69.6 ms, 2/8 63.4); 16 spare restored it
+# (54.4 / 46.8 ms), 32 the same (54.4 / 46.5; profiles/r06/c4_shares/slack_r06.txt)
+CU_SLACK = 32
 _COSTS = None
 
 
@@ -76,6 +80,8 @@ def load_costs(path=COST_TABLE):
                         form = d["form"]
                         if form == "wide":  # the r06 table's first form: one width, in wgs_req
                             form = "wide%d" % d["wgs_req"]
+                        if form.startswith("wide") and not d.get("kernels", ["k_memo"])[0].startswith("k_memo"):
+                            continue  # no k_memo plan at that width (the engine fell back): not a width to plan
                         out[(d["trace"], d["policy"], form)] = d["us_per_event"]
         if path != COST_TABLE:
             return out
@@ -113,12 +119,14 @@ def plan_costs(items, form="one"):
     return out
 
 
-def plan_widths(items, costs, wide_costs, cus=256, ks=WIDE_KS, packs=CHEAP_PACKS, margin=WIDEN_MARGIN):
+def plan_widths(items, costs, wide_costs, cus=256, ks=WIDE_KS, packs=CHEAP_PACKS, margin=WIDEN_MARGIN,
+                slack=CU_SLACK):
     """Critical-path-aware widths for one share's experiments (run concurrently on one GPU).  The
     share's time is its longest replay chain: the cheap chains (cheap_slow x the longest, for the packing), the FGD
     chains left on k_hmemo at one workgroup, and the widened ones on k_memo at their width.  Each widened replica holds
     its workgroups' CUs, every other FGD replica one (k_memo and k_hmemo fill a CU's registers), the cheap replicas
-    per_cu to a CU.  For each packing, the shortest predicted time T that fits the CUs: every FGD chain longer than T
+    per_cu to a CU, `slack` CUs left over.  For each packing, the shortest predicted time T that fits the CUs: every FGD
+    chain longer than T
     widened at the fewest workgroups that bring it under T; then the chains within `margin` of T at the fewest
     workgroups that shorten them, longest first, while CUs last.  The packing with the shorter T wins (ties: the
     first).  wide_costs: {K: a cost per item at K workgroups} (plan_wide_costs).
@@ -128,7 +136,7 @@ def plan_widths(items, costs, wide_costs, cus=256, ks=WIDE_KS, packs=CHEAP_PACKS
     ks = sorted(k for k in ks if k in wide_costs)
     best = None
     for n, (per_cu, slow) in enumerate(packs):
-        budget = cus - len(fgd) - -(-len(cheap) // per_cu)
+        budget = cus - slack - len(fgd) - -(-len(cheap) // per_cu)
         floor = max((costs[i] for i in cheap), default=0.0) * slow
         cands = sorted({floor} | {costs[i] for i in fgd} | {wide_costs[k][i] for k in ks for i in fgd})
         for T in cands:
@@ -161,8 +169,17 @@ def plan_widths(items, costs, wide_costs, cus=256, ks=WIDE_KS, packs=CHEAP_PACKS
 
 
 def plan_wide_costs(items, ks=WIDE_KS):
-    """{K: plan_costs(items, "wide<K>")} for every width of `ks`."""
-    return {k: plan_costs(items, "wide%d" % k) for k in ks}
+    """{K: plan_costs(items, "wide<K>")} for every width of `ks`; an FGD experiment whose trace the table holds but
+    not at that width (k_memo has no plan for it: gpuspec33's keys at 6 workgroups) costs inf there."""
+    table = load_costs()
+    out = {}
+    for k in ks:
+        c = plan_costs(items, "wide%d" % k)
+        if table:
+            c = [v if it[1] != "06-FGD" or (it[0], it[1], "wide%d" % k) in table else float("inf")
+                 for v, it in zip(c, items)]
+        out[k] = c
+    return out
 
 
 def shard(items, rank, world, costs=None):

@@ -20,7 +20,7 @@ exps = SW.shard(items, k, n, SW.plan_costs(items))
 costs = SW.plan_costs(exps)
 wcosts = SW.plan_wide_costs(exps)
 if kw is None:
-    wide = SW.plan_widths(exps, costs, wcosts)
+    wide = SW.plan_widths(exps, costs, wcosts, slack=int(os.environ.get("SHARE_SLACK", SW.CU_SLACK)))
 elif kw == 0:
     wide = {}
 else:

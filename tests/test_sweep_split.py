@@ -75,7 +75,7 @@ def test_widths_fit_the_cus_and_take_the_longest_fgd_chains(plan, world):
         n_fgd = sum(1 for e in sh if e[1] == "06-FGD")
         n_cheap = len(sh) - n_fgd
         loosest = max(p for p, _ in SW.CHEAP_PACKS)
-        assert n_fgd + sum(kw - 1 for kw in wide.values()) + -(-n_cheap // loosest) <= 256
+        assert n_fgd + sum(kw - 1 for kw in wide.values()) + -(-n_cheap // loosest) <= 256 - SW.CU_SLACK
         # the widened ones are the longest FGD chains, and each is shorter widened
         narrow = [c[i] for i in range(len(sh)) if sh[i][1] == "06-FGD" and i not in wide]
         assert min(c[i] for i in wide) >= max(narrow, default=0.0)
@@ -87,8 +87,8 @@ def test_widths_fit_the_cus_and_take_the_longest_fgd_chains(plan, world):
         assert SW.plan_widths(items, costs, wide_costs) == {}
     if world == 8:  # room for the longest chains (gpushare100) at 24 or 32 workgroups
         assert seen & {24, 32}, seen
-    if world == 4:  # more long chains than CUs at 16: all at 12
-        assert seen == {12}, seen
+    if world == 4:  # more long chains than CUs at 16: 12 and narrower
+        assert 12 in seen and max(seen) <= 12, seen
 
 
 def test_widths_take_the_fewest_workgroups_under_the_predicted_time():
@@ -97,12 +97,12 @@ def test_widths_take_the_fewest_workgroups_under_the_predicted_time():
     wide = {12: [80.0, 70.0, 40.0, 60.0], 16: [70.0, 60.0, 38.0, 60.0], 32: [62.0, 59.0, 35.0, 60.0]}
     one = ((3, 1.0),)
     # T = 62: item 0 needs 32 workgroups, item 1 16 (the fewest under 62), item 2 is under the cheap chain (60)
-    assert SW.plan_widths(items, costs, wide, packs=one, margin=1.0) == {0: 32, 1: 16}
+    assert SW.plan_widths(items, costs, wide, packs=one, margin=1.0, slack=0) == {0: 32, 1: 16}
     # fewer CUs: 3 FGD + 1 cheap + 31 + 15 = 50 > 44, so T = 70 (item 0 at 16, item 1 at 12)
-    assert SW.plan_widths(items, costs, wide, cus=44, packs=one, margin=1.0) == {0: 16, 1: 12}
-    assert SW.plan_widths(items, costs, wide, cus=3, packs=one) == {}  # no CUs to spare
+    assert SW.plan_widths(items, costs, wide, cus=44, packs=one, margin=1.0, slack=0) == {0: 16, 1: 12}
+    assert SW.plan_widths(items, costs, wide, cus=3, packs=one, slack=0) == {}  # no CUs to spare
     # the margin widens item 2 too (50 > 0.75 x 62) at the fewest workgroups that shorten it
-    assert SW.plan_widths(items, costs, wide, packs=one, margin=0.75) == {0: 32, 1: 16, 2: 12}
+    assert SW.plan_widths(items, costs, wide, packs=one, margin=0.75, slack=0) == {0: 32, 1: 16, 2: 12}
 
 
 def test_widths_choose_the_shorter_packing():
@@ -112,10 +112,10 @@ def test_widths_choose_the_shorter_packing():
     wide = {12: [62.0, 60.0] + [40.0] * 6, 32: [50.0, 48.0] + [40.0] * 6}
     packs = ((3, 1.0), (6, 1.4))
     # T = 60 needs item 0 at 32 and item 1 at 12 (42 CUs beyond one each), T = 62 both at 12 (22)
-    assert SW.plan_widths(items, costs, wide, cus=30, packs=packs, margin=1.0) == {0: 12, 1: 12}
+    assert SW.plan_widths(items, costs, wide, cus=30, packs=packs, margin=1.0, slack=0) == {0: 12, 1: 12}
     # 45 CUs: packed 3 to a CU the cheap replicas leave 41 (T 62), 6 to a CU 42 (T 60, over their 56): the tighter wins
-    assert SW.plan_widths(items, costs, wide, cus=45, packs=packs, margin=1.0) == {0: 32, 1: 12}
-    assert SW.plan_widths(items, costs, wide, cus=45, packs=packs[:1], margin=1.0) == {0: 12, 1: 12}
+    assert SW.plan_widths(items, costs, wide, cus=45, packs=packs, margin=1.0, slack=0) == {0: 32, 1: 12}
+    assert SW.plan_widths(items, costs, wide, cus=45, packs=packs[:1], margin=1.0, slack=0) == {0: 12, 1: 12}
 
 
 def test_costs_come_from_the_measured_table(plan):
