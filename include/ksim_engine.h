@@ -240,7 +240,8 @@ int  ksim_engine_set_weights(ksim_engine* e, int replica, int32_t w_pwr, int32_t
 /* Workgroups per replica for one replica (0: the engine's choice, the default; at most 64).  An FGD replica with
  * wgs > 1 in an auto-mode engine whose other FGD replicas take one workgroup each runs k_memo at that width (the
  * keys in HBM when they do not fit in LDS) concurrently with the others -- the paper sweep's longest replay
- * chains on more CUs.  Decisions are the same bits either way. */
+ * chains on more CUs.  Each such replica keeps its own width: one k_memo launch holds replicas of
+ * different widths.  Decisions are the same bits either way. */
 int  ksim_engine_set_replica_wgs(ksim_engine* e, int replica, int wgs);
 /* DotProduct's dimExtMethod / normMethod (the score plugin's and Open-Gpu-Share's args, which the
  * reference harness sets alike: generate_config_and_run.py:269-277).  Replaces

@@ -4405,7 +4405,8 @@ int ksim_engine_run(ksim_engine* e) {
     int fail = 0;
     KSIM_HIP(hipMemcpy(&fail, e->d_fail, sizeof(int), hipMemcpyDeviceToHost));
     if (fail & 2) return KSIM_ERANGE;  // a raw PWR score outside the 24-bit key field
-    if (fail & ~3) std::fprintf(stderr, "ksim: a k_hmemo bulk wait timed out (fail bits 0x%x)\n", fail);
+    if (fail & 60) std::fprintf(stderr, "ksim: a memoised kernel's LDS wait timed out (fail bits 0x%x)\n", fail);
+    if (fail & 64) std::fprintf(stderr, "ksim: the overlapped report waited too long for a replay (fail bits 0x%x)\n", fail);
     if (fail) return KSIM_ESTATE;  // a granule poll or an LDS wait timed out
   }
   return KSIM_OK;
