@@ -97,7 +97,11 @@ def test_full_paper_sweep_vs_expected_results():
     sw = SW.Sweep(SW.plan())
     dev_ms, wall = sw.run()
     curves = sw.curves()
+    # the cheap group (850 replicas, more than the CUs beside the FGD group hold at once) reports replica by replica
+    # through k_report_overlap's queue, each of its workgroups taking several replicas
+    n_ovl = sw.eng.last_run_report_overlap()
     sw.close()
+    assert n_ovl == 850, n_ovl
     worst = {}
     for t in SW.TRACES:
         for p in SW.POLICY_DIRS:
