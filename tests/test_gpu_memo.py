@@ -318,3 +318,47 @@ def test_hmemo_list_and_table_forms(trace_name, knobs, monkeypatch):
     for wgs in (0, 6):
         res, state = engine_run(t, rp, None, n_ev, "FGD", run_mode=HMEMO, wgs=wgs)
         assert_same(res, want, state, want_state, None)
+
+
+@pytest.mark.parametrize("form", ["lean", "report", "deletes"])
+def test_memo_replicas_at_their_own_widths(form):
+    # r06: one k_memo launch holding replicas of different widths (ksim_engine_set_replica_wgs per replica; the
+    # block map MemoArgs::wg_map): three seeds at 4, 12 and 25 workgroups, each bit-exact against the oracle in the
+    # lean form, with the report's stores (against the one-workgroup k_hmemo's reports) and in the general form
+    t = ksim.Trace.openb("default")
+    arr, n = t.typical()
+    widths = (4, 12, 25)
+    cases = []
+    for s in (42, 45, 49):
+        rp = t.replay(seed=s)
+        if form == "deletes":
+            evs, oev = helpers.delete_stream(t, rp, 1500, 0.3, seed=s)
+            n_ev = len(evs)
+            want = O.run_events(helpers.oracle_nodes(t, rp), helpers.oracle_typical(t), oev, policy=O.POL_FGD,
+                                gpu_sel=O.SEL_FGD, threads=16)
+        else:
+            evs, n_ev = rp.events, 2000
+            want = oracle_run(t, rp, None, n_ev, O.POL_FGD, O.SEL_FGD)
+        cases.append((rp, evs, n_ev, want))
+    outs = {}
+    for mode in (MEMO, HMEMO):
+        eng = ksim.Engine(t.num_nodes, len(cases), run_mode=mode, wgs_per_replica=0 if mode == MEMO else 1)
+        for r, (rp, evs, n_ev, _) in enumerate(cases):
+            eng.set_nodes(r, rp.nodes)
+            eng.set_typical(r, arr, n)
+            eng.set_policy(r, "FGD")
+            if mode == MEMO:
+                eng.set_replica_wgs(r, widths[r])
+            eng.load_events(r, evs, n_ev)
+        if form == "report":
+            eng.set_report(True)
+        eng.run()
+        kern = eng.last_run_kernels()
+        assert kern[0] in (("k_memo", "k_memo_hkeys") if mode == MEMO else ("k_hmemo",)), kern
+        outs[mode] = [(eng.results(r), eng.nodes(r), eng.reports(r) if form == "report" else None)
+                      for r in range(len(cases))]
+        eng.close()
+    for r, (_, _, _, (want, want_state, _)) in enumerate(cases):
+        assert_same(outs[MEMO][r][0], want, outs[MEMO][r][1], want_state, None)
+        if form == "report":
+            assert outs[MEMO][r][2] == outs[HMEMO][r][2], r
