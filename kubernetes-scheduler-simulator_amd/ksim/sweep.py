@@ -53,8 +53,8 @@ FGD_US, FGD_US_PER_TYP, CHEAP_US = 4.1, 0.055, 3.3
 # launches each at its own width), and how tight the cheap replicas pack -- (replicas planned per CU, how much their
 # chains slow down packed that tight: share 0/4 at 6 to a CU, its cheap group 32.6 -> 50.9 ms;
 # profiles/r06/c4_shares/widths_r06.txt).  The measured costs per width are in the table (gpushare80 alone: 60.7 ms
-# on k_hmemo, 56.9 / 54.3 / 48.3 / 46.8 / 44.2 / 41.6 ms at 6 / 8 / 12 / 16 / 24 / 32 workgroups).
-WIDE_KS = (6, 8, 12, 16, 24, 32)
+# on k_hmemo, 56.9 / 54.3 / 48.3 / 46.8 / 44.2 / 41.6 / 41.3 / 39.5 ms at 6 / 8 / 12 / 16 / 24 / 32 / 48 / 64 workgroups).
+WIDE_KS = (6, 8, 12, 16, 24, 32, 48, 64)
 CHEAP_PACKS = ((3, 1.0), (6, 1.4))
 # A chain within WIDEN_MARGIN of the share's predicted time is widened too while CUs last: beside the others on a full
 # GPU every chain runs 3-5 % longer than alone, so a narrow chain just under the widened ones ends after them (share
@@ -62,7 +62,8 @@ CHEAP_PACKS = ((3, 1.0), (6, 1.4))
 WIDEN_MARGIN = 0.9
 # CUs the plan leaves unused: the three launches do not pack the device perfectly, and a plan that fills all 256 lost
 # the cheap group's residency (its last replicas waited for CUs: share 1/4 69.6 ms, 2/8 63.4); 16 spare restored it
-# (54.4 / 46.8 ms), 32 the same (54.4 / 46.5; profiles/r06/c4_shares/slack_r06.txt)
+# (54.4 / 46.8 ms), 32 the same (54.4 / 46.5; profiles/r06/c4_shares/slack_r06.txt).  16 for every share predicts
+# shorter shares but measured the same (N = 8 45.6-49.3 ms, N = 4 53.3-54.5: summary_r06sh12_slack16_k64.txt)
 CU_SLACK = 32
 _COSTS = None
 
