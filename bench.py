@@ -310,10 +310,12 @@ def main():
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
-        if args.sharded and ndev < world:
-            # shard processes sharing a device (a 1-GPU box rehearsing the multi-process sharded mode): the
-            # data path is the device exchange, the launcher's own barrier / reductions go over gloo (RCCL
-            # refuses two ranks on one device)
+        if ndev < world:
+            # ranks sharing a device (a box with fewer GPUs than ranks rehearsing the N-GPU run, replicas or the
+            # multi-process sharded mode): the launcher's own barrier / reductions go over gloo (RCCL refuses two
+            # ranks on one device); the data path has no collective either way
+            print("bench: %d ranks on %d device(s): ranks share devices, gloo for the barrier" % (world, ndev),
+                  file=sys.stderr)
             local = local % max(ndev, 1)
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
