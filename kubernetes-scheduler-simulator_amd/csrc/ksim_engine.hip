@@ -1831,6 +1831,8 @@ struct ksim_engine {
   unsigned* d_m_hkeys = nullptr;  // k_memo with the keys in HBM (MemoPlan::hkeys)
   int* d_m_wgmap = nullptr;       // k_memo: each block's launch position << 8 | workgroup (MemoArgs::wg_map)
   unsigned long long* d_done = nullptr;  // [2 + R] the overlapped report's queue (ksim_scan1.hpp Scan1Args::done)
+  __int128* d_ragg = nullptr;     // [R][kScanPartsMax][2][kFields] the multi-workgroup report scan's part sums
+  size_t ragg_cap = 0;
   int done_cap = 0;
   unsigned done_epoch = 0;
   hipEvent_t ev_ovl = nullptr;    // the queue's tickets zeroed (the report's stream waits on it)
@@ -3114,7 +3116,7 @@ void ksim_engine_destroy(ksim_engine* e) {
                   e->d_m_wgref, e->d_m_wggrp, e->d_win, e->d_m_evo, e->d_th, e->d_pw, e->d_cpum, e->d_pws,
                   e->d_m_evcls, e->d_topg, e->d_m_hkeys, e->d_m_wgmap, e->d_h_cg, e->d_h_cls, e->d_h_cgrp, e->d_h_gpod, e->d_h_evc, e->d_h_st,
                   e->d_h_ns, e->d_h_nstate, e->d_h_gsc, e->d_h_mtoff, e->d_h_mtab, e->d_h_na, e->d_h_keys, e->d_h_l1, e->d_h_l2, e->d_h_cnt, e->d_h_prof,
-                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist, e->d_done};
+                  e->d_h_hist, e->d_go, e->d_ggran, e->d_hgargs, e->d_rgran, e->d_rgreps, e->d_rglist, e->d_done, e->d_ragg};
   for (void* p : bufs) (void)hipFree(p);
   for (int i = 0; i < ksim_engine::kSide; ++i) {
     if (e->side[i]) (void)hipStreamDestroy(e->side[i]);
@@ -3601,6 +3603,25 @@ static int run_report(ksim_engine* e, int max_ev, hipStream_t st, const int* lis
   hipLaunchKernelGGL(ksim_rep::k_report_delta, grid, dim3(ksim_rep::kDeltaBlock), 0, st,
                      (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, list);
   KSIM_HIP(hipGetLastError());
+  // the scan over B workgroups per replica when a few replicas would leave most CUs idle behind one workgroup's pass
+  // (about a CU-full of workgroups, parts of >= 2048 events; KSIM_VARIANT report_parts=0: one workgroup each)
+  const int B = variant("report_parts", 1) != 0
+                    ? std::min({ksim_rep::kScanPartsMax, (e->cus + R - 1) / R, max_ev / 2048}) : 1;
+  if (B > 1) {
+    const size_t n = (size_t)e->R * ksim_rep::kScanPartsMax * 2 * ksim_rep::kFields;
+    if (n > e->ragg_cap) {
+      if (e->d_ragg) KSIM_HIP(hipFree(e->d_ragg));
+      KSIM_HIP(hipMalloc(&e->d_ragg, sizeof(__int128) * n));
+      e->ragg_cap = n;
+    }
+    hipLaunchKernelGGL(ksim_rep::k_report_part, dim3((unsigned)B, (unsigned)R), dim3(ksim_rep::kScanBlock), 0, st,
+                       (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N, list, e->d_ragg);
+    KSIM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ksim_rep::k_report_apply, dim3((unsigned)B, (unsigned)R), dim3(ksim_rep::kScanBlock), 0, st,
+                       (const ReplicaDev*)e->d_reps, e->N, list, (const __int128*)e->d_ragg);
+    KSIM_HIP(hipGetLastError());
+    return KSIM_OK;
+  }
   hipLaunchKernelGGL(ksim_rep::k_report_scan, dim3(R), dim3(ksim_rep::kScanBlock), 0, st,
                      (const ReplicaDev*)e->d_reps, (const TypDev*)e->d_tp, e->N, list);
   KSIM_HIP(hipGetLastError());

@@ -173,6 +173,36 @@ __device__ __forceinline__ void block_excl_scan_fields(__int128 (&v)[kFields], _
   __syncthreads();
 }
 
+// Events [e0, e1) of a replica: every thread a contiguous chunk -- its records' sums (all fields at once), one block
+// exclusive scan for each chunk's start, then the running sums from `base` on (in place).  Each record read twice and
+// written once.
+__device__ __forceinline__ void report_run_sums(const ReplicaDev& rp, int e0, int e1, const __int128* base,
+                                                __int128 (*s_w)[kFields]) {
+  const int tid = (int)threadIdx.x;
+  const int per = (e1 - e0 + kScanBlock - 1) / kScanBlock;
+  const int lo = min(e1, e0 + tid * per), hi = min(e1, lo + per);
+  __int128 run[kFields];
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) run[k] = 0;
+  for (int e = lo; e < hi; ++e) {
+    const RepAcc* o = rp.rep + e;
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) run[k] += rep_get(o, k);
+  }
+  block_excl_scan_fields(run, s_w, nullptr);
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) run[k] += base[k];
+  for (int e = lo; e < hi; ++e) {
+    RepAcc* o = rp.rep + e;
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) {
+      run[k] += rep_get(o, k);
+      // the power fields stay 0 without an energy model (k_report_delta wrote 0; the sums are 0 too)
+      rep_set(o, k, run[k]);
+    }
+  }
+}
+
 // grid R: the initial cluster's report, then the inclusive prefix over the events (in place).  Every
 // thread owns a contiguous chunk of events: one pass sums the chunk's records (all fields at once), one
 // block scan gives each chunk's start, a second pass writes the running sums -- each record read twice and
@@ -196,30 +226,7 @@ __device__ __forceinline__ void report_scan_replica(const ReplicaDev& rp, const 
     }
     block_excl_scan_fields(acc, s_w, s_base);
   }
-  // contiguous chunk per thread: local totals, block exclusive scan, then the running sums
-  const int E = rp.n_events;
-  const int per = (E + kScanBlock - 1) / kScanBlock;
-  const int lo = min(E, tid * per), hi = min(E, lo + per);
-  __int128 run[kFields];
-#pragma unroll
-  for (int k = 0; k < kFields; ++k) run[k] = 0;
-  for (int e = lo; e < hi; ++e) {
-    const RepAcc* o = rp.rep + e;
-#pragma unroll
-    for (int k = 0; k < kFields; ++k) run[k] += rep_get(o, k);
-  }
-  block_excl_scan_fields(run, s_w, nullptr);
-#pragma unroll
-  for (int k = 0; k < kFields; ++k) run[k] += s_base[k];
-  for (int e = lo; e < hi; ++e) {
-    RepAcc* o = rp.rep + e;
-#pragma unroll
-    for (int k = 0; k < kFields; ++k) {
-      run[k] += rep_get(o, k);
-      // the power fields stay 0 without an energy model (k_report_delta wrote 0; the sums are 0 too)
-      rep_set(o, k, run[k]);
-    }
-  }
+  report_run_sums(rp, 0, rp.n_events, s_base, s_w);
 }
 
 __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
@@ -230,6 +237,74 @@ __global__ __launch_bounds__(kScanBlock) void k_report_scan(const ReplicaDev* re
   __shared__ TypDev s_tp[kMaxTypical];
   stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
   report_scan_replica(rp, s_tp, N);
+}
+
+// k_report_scan over B workgroups per replica (r06), for groups of few replicas, where one workgroup's pass over a long
+// replica's records ends the run (the N-GPU sweep shares' widened FGD group: 9-15 replicas).  Part b of replica r owns
+// the events [b*pe, (b+1)*pe) and the nodes [b*pn, (b+1)*pn):
+//   k_report_part   its events' sum and its nodes' initial terms' sum -> agg[r][b][1] / agg[r][b][0];
+//   k_report_apply  base = every part's node sum + the event sums of the parts before it, then the running sums.
+// Integer adds, so the same values as k_report_scan's in any grouping.  agg: [R][kScanPartsMax][2][kFields].
+constexpr int kScanPartsMax = 64;
+__device__ __forceinline__ __int128* scan_agg(__int128* agg, int r, int b, int part) {
+  return agg + (((size_t)r * kScanPartsMax + b) * 2 + part) * kFields;
+}
+__global__ __launch_bounds__(kScanBlock) void k_report_part(const ReplicaDev* reps, const TypDev* __restrict__ tp_all,
+                                                            int N, const int* list, __int128* agg) {
+  const int B = (int)gridDim.x, b = (int)blockIdx.x;
+  const int r = list ? list[blockIdx.y] : (int)blockIdx.y;
+  const ReplicaDev rp = reps[r];
+  if (!rp.rep) return;
+  __shared__ TypDev s_tp[kMaxTypical];
+  __shared__ __int128 s_w[kScanBlock / 64][kFields];
+  __shared__ __int128 s_tot[kFields];
+  stage_typical(tp_all + (size_t)r * kMaxTypical, rp.nt, s_tp);
+  const int tid = (int)threadIdx.x;
+  __int128 acc[kFields];
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) acc[k] = 0;
+  const int pn = (N + B - 1) / B, n0 = min(N, b * pn), n1 = min(N, n0 + pn);
+  const PowerDev* pw = rp.has_pw ? rp.pw : nullptr;
+  for (int i = n0 + tid; i < n1; i += kScanBlock) {
+    __int128 f[kFields];
+    node_term(load_node(rp.init + i), rp.cap[i], s_tp, rp.ncpu, rp.nt, pw, rp.cpum[i], f);
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) acc[k] += f[k];
+  }
+  block_excl_scan_fields(acc, s_w, s_tot);
+  if (tid < kFields) scan_agg(agg, r, b, 0)[tid] = s_tot[tid];
+  const int E = rp.n_events, pe = (E + B - 1) / B, e0 = min(E, b * pe), e1 = min(E, e0 + pe);
+  const int per = (e1 - e0 + kScanBlock - 1) / kScanBlock;
+  const int lo = min(e1, e0 + tid * per), hi = min(e1, lo + per);
+#pragma unroll
+  for (int k = 0; k < kFields; ++k) acc[k] = 0;
+  for (int e = lo; e < hi; ++e) {
+    const RepAcc* o = rp.rep + e;
+#pragma unroll
+    for (int k = 0; k < kFields; ++k) acc[k] += rep_get(o, k);
+  }
+  block_excl_scan_fields(acc, s_w, s_tot);
+  if (tid < kFields) scan_agg(agg, r, b, 1)[tid] = s_tot[tid];
+}
+__global__ __launch_bounds__(kScanBlock) void k_report_apply(const ReplicaDev* reps, int N, const int* list,
+                                                             const __int128* agg) {
+  const int B = (int)gridDim.x, b = (int)blockIdx.x;
+  const int r = list ? list[blockIdx.y] : (int)blockIdx.y;
+  const ReplicaDev rp = reps[r];
+  if (!rp.rep) return;
+  (void)N;
+  __shared__ __int128 s_w[kScanBlock / 64][kFields];
+  __shared__ __int128 s_base[kFields];
+  const int tid = (int)threadIdx.x;
+  if (tid < kFields) {
+    __int128 v = 0;
+    for (int q = 0; q < B; ++q) v += scan_agg(const_cast<__int128*>(agg), r, q, 0)[tid];
+    for (int q = 0; q < b; ++q) v += scan_agg(const_cast<__int128*>(agg), r, q, 1)[tid];
+    s_base[tid] = v;
+  }
+  __syncthreads();
+  const int E = rp.n_events, pe = (E + B - 1) / B, e0 = min(E, b * pe), e1 = min(E, e0 + pe);
+  report_run_sums(rp, e0, e1, s_base, s_w);
 }
 
 // The report of one group's replicas in the order their replays end (a grid of 15/16 of the CUs at most, launched
